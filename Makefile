@@ -1,0 +1,32 @@
+# libfognet_hip: gfx950 kernels + C ABI.  hipcc cross-compiles without a GPU.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
+SRC_DIR := fognetsimpp_amd/csrc
+SRCS := $(SRC_DIR)/capi.hip $(SRC_DIR)/replay.hip $(SRC_DIR)/decide.hip $(SRC_DIR)/tracegen.hip
+HDRS := include/fognet_hip.h $(SRC_DIR)/internal.h
+OBJDIR := build/obj
+OBJS := $(patsubst $(SRC_DIR)/%.hip,$(OBJDIR)/%.o,$(SRCS))
+LIB := fognetsimpp_amd/libfognet_hip.so
+
+all: $(LIB) oracle
+
+$(OBJDIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -s -C oracle
+
+asm: $(SRC_DIR)/replay.hip $(HDRS)
+	@mkdir -p build/asm
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o build/asm/replay.o -save-temps=obj -Rpass-analysis=kernel-resource-usage
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean asm

@@ -1,0 +1,14 @@
+"""fognetsimpp_amd — MI355X-native engine for FogNetSim++'s offload-decision hot path.
+
+Scope (BASELINE.json north_star): the broker's task-to-fog-node
+argmin (BrokerBaseApp3.cc:265-304) and the fog node's queue update that follows
+each decision (ComputeBrokerApp3.cc:205-320), replayed for thousands of
+independent what-if replications on gfx950 behind the C ABI in
+include/fognet_hip.h (libfognet_hip.so, built in-tree).
+"""
+from ._abi import FognetError, load as _load_lib  # noqa: F401
+from .engine import (BatchResult, BrokerBaseApp3, Context, allocate_outputs, as_device_trace,  # noqa: F401
+                     generate_trace, merge_job_stats, reduce_stats, run_batch, summarize, sweep_params)
+
+__all__ = ["Context", "BrokerBaseApp3", "BatchResult", "run_batch", "reduce_stats", "merge_job_stats",
+           "summarize", "generate_trace", "sweep_params", "allocate_outputs", "as_device_trace", "FognetError"]

@@ -1,0 +1,143 @@
+"""ctypes mirror of include/fognet_hip.h (libfognet_hip C ABI).
+
+The library is built in-tree by ``make`` (see __graft_entry__.build()).  There
+is no CPU fallback: importing the package without the built library raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libfognet_hip.so")
+
+FOGNET_OK = 0
+FOGNET_ERR_ARG = 1
+FOGNET_ERR_NO_NODES = 2
+FOGNET_ERR_DIV0 = 3
+FOGNET_ERR_STATE = 4
+FOGNET_ERR_DEVICE = 5
+FOGNET_ERR_OOM = 6
+FOGNET_ERR_CAPACITY = 7
+FOGNET_ERR_UNSUPPORTED = 8
+
+FOGNET_POLICY_REF_V3 = 1
+TICKS_PER_SECOND = 10**12
+
+
+class RepStats(C.Structure):
+    _fields_ = [
+        ("n_tasks", C.c_int64), ("n_queued", C.c_int64), ("n_started", C.c_int64),
+        ("last_tick", C.c_int64),
+        ("queue_min_ticks", C.c_int64), ("queue_max_ticks", C.c_int64),
+        ("resp_min_ticks", C.c_int64), ("resp_max_ticks", C.c_int64),
+        ("queue_sum_lo", C.c_uint64), ("queue_sum_hi", C.c_uint64),
+        ("queue_sq_lo", C.c_uint64), ("queue_sq_hi", C.c_uint64),
+        ("resp_sum_lo", C.c_uint64), ("resp_sum_hi", C.c_uint64),
+        ("resp_sq_lo", C.c_uint64), ("resp_sq_hi", C.c_uint64),
+        ("events", C.c_int64), ("max_pending", C.c_int32), ("status", C.c_int32),
+    ]
+
+
+def _np_dtype(struct):
+    m = {C.c_int64: np.int64, C.c_uint64: np.uint64, C.c_int32: np.int32, C.c_uint32: np.uint32}
+    fields = []
+    for name, t in struct._fields_:
+        if hasattr(t, "_length_"):
+            fields.append((name, m[t._type_], (t._length_,)))
+        else:
+            fields.append((name, m[t]))
+    dt = np.dtype(fields)
+    assert dt.itemsize == C.sizeof(struct), (dt.itemsize, C.sizeof(struct))
+    return dt
+
+
+REP_STATS_DTYPE = _np_dtype(RepStats)
+
+
+class JobStats(C.Structure):
+    _fields_ = [
+        ("n_reps", C.c_int64), ("n_failed", C.c_int64),
+        ("n_tasks", C.c_int64), ("n_queued", C.c_int64), ("n_started", C.c_int64),
+        ("last_tick", C.c_int64),
+        ("queue_min_ticks", C.c_int64), ("queue_max_ticks", C.c_int64),
+        ("resp_min_ticks", C.c_int64), ("resp_max_ticks", C.c_int64),
+        ("queue_sum", C.c_uint64 * 3), ("queue_sq", C.c_uint64 * 3),
+        ("resp_sum", C.c_uint64 * 3), ("resp_sq", C.c_uint64 * 3),
+        ("events", C.c_int64), ("max_pending", C.c_int64),
+    ]
+
+
+JOB_STATS_DTYPE = _np_dtype(JobStats)
+
+
+class BatchIn(C.Structure):
+    _fields_ = [
+        ("R", C.c_int32), ("T", C.c_int32), ("N", C.c_int32), ("policy", C.c_int32),
+        ("node_stride", C.c_int32), ("ring_capacity", C.c_int32),
+        ("arrive_tick", C.c_void_p), ("req_mips", C.c_void_p), ("mips", C.c_void_p),
+        ("dl_tick", C.c_void_p), ("ul_tick", C.c_void_p), ("init_adv_tick", C.c_void_p),
+    ]
+
+
+class BatchOut(C.Structure):
+    _fields_ = [("node", C.c_void_p), ("status", C.c_void_p), ("start_tick", C.c_void_p),
+                ("done_tick", C.c_void_p), ("stats", C.c_void_p)]
+
+
+class GenParams(C.Structure):
+    _fields_ = [("seed", C.c_uint32), ("req_lo", C.c_int32), ("req_hi", C.c_int32), ("pad", C.c_int32),
+                ("mean_gap_ticks", C.c_void_p), ("lat_scale", C.c_void_p)]
+
+
+# name -> (restype, argtypes); every function declared in include/fognet_hip.h
+P = C.c_void_p
+SIGNATURES = {
+    "fognet_abi_version": (C.c_int, []),
+    "fognet_status_string": (C.c_char_p, [C.c_int]),
+    "fognet_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
+    "fognet_destroy": (None, [P]),
+    "fognet_last_error": (C.c_char_p, [P]),
+    "fognet_decide": (C.c_int, [P, C.c_int, C.c_int32, P, P, C.c_int32, C.POINTER(C.c_int32)]),
+    "fognet_decide_batch_dev": (C.c_int, [P, C.c_int, C.c_int64, C.c_int32, P, P, P, P, P, P]),
+    "fognet_run_batch_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P]),
+    "fognet_run_batch": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut)]),
+    "fognet_replay_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P]),
+    "fognet_rep_stats_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P]),
+    "fognet_reduce_stats_dev": (C.c_int, [P, P, C.c_int32, P, P]),
+    "fognet_job_stats_init": (None, [C.POINTER(JobStats)]),
+    "fognet_job_stats_merge": (None, [C.POINTER(JobStats), C.POINTER(JobStats)]),
+    "fognet_gen_trace_dev": (C.c_int, [P, C.POINTER(GenParams), C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                       P, P, P, P, P, P, P]),
+    "fognet_sync": (C.c_int, [P]),
+}
+
+_lib = None
+
+
+class FognetError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"fognet status {code}: {msg}")
+        self.code = code
+
+
+def load():
+    """Load the in-tree libfognet_hip.so; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run `make` (or __graft_entry__.build()) first; "
+                              "there is no CPU fallback")
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def status_string(code: int) -> str:
+    return load().fognet_status_string(code).decode()

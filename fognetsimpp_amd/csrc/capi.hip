@@ -1,0 +1,371 @@
+// capi.hip — host implementation of the libfognet_hip C ABI (include/fognet_hip.h).
+// Pure host C++ around the gfx950 kernels; there is no CPU compute path: every
+// decision is evaluated on the device, and the library refuses to create a
+// context without a gfx950 GPU.
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "internal.h"
+
+struct fognet_ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;  // private stream for the host-buffer entry points
+  fognet::RingEntry* ring = nullptr;
+  size_t ring_bytes = 0;
+  // scratch for fognet_decide
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  std::string err;
+};
+
+namespace {
+
+int fail(fognet_ctx* c, int rc, const std::string& msg) {
+  if (c) c->err = msg;
+  return rc;
+}
+
+int hip_fail(fognet_ctx* c, hipError_t e, const char* what) {
+  return fail(c, FOGNET_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int ensure(fognet_ctx* c, void** p, size_t* have, size_t want, const char* what) {
+  if (*have >= want) return FOGNET_OK;
+  if (*p) {
+    (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+  }
+  hipError_t e = hipMalloc(p, want);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(c, e == hipErrorOutOfMemory ? FOGNET_ERR_OOM : FOGNET_ERR_DEVICE,
+                std::string("hipMalloc ") + what + ": " + hipGetErrorString(e));
+  }
+  *have = want;
+  return FOGNET_OK;
+}
+
+int set_device(fognet_ctx* c) {
+  hipError_t e = hipSetDevice(c->device);
+  return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "hipSetDevice");
+}
+
+// Validates a batch descriptor; fills the kernel argument block except pointers to outputs.
+int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
+  if (!in) return fail(c, FOGNET_ERR_ARG, "null batch");
+  if (in->R < 0 || in->T < 0 || in->N < 0) return fail(c, FOGNET_ERR_ARG, "negative R/T/N");
+  if (in->N == 0) return fail(c, FOGNET_ERR_NO_NODES, "N == 0 (BrokerBaseApp3.cc:268 reads brokers[0])");
+  if (in->N > fognet::kWave * fognet::kMaxNodesPerLane)
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "N > 256 not supported by the register-resident replay kernel");
+  if (in->policy != FOGNET_POLICY_REF_V3) return fail(c, FOGNET_ERR_UNSUPPORTED, "unknown policy");
+  if (in->node_stride != 0 && in->node_stride != in->N)
+    return fail(c, FOGNET_ERR_ARG, "node_stride must be 0 or N");
+  int q = in->ring_capacity ? in->ring_capacity : 1024;
+  if (q < 2 || (q & (q - 1)) != 0 || q > (1 << 20)) return fail(c, FOGNET_ERR_ARG, "ring_capacity must be a power of two in [2, 2^20]");
+  int qlog = 0;
+  while ((1 << qlog) < q) ++qlog;
+  if (in->R > 0 && in->T > 0 && (!in->arrive_tick || !in->req_mips))
+    return fail(c, FOGNET_ERR_ARG, "null trace arrays");
+  if (in->R > 0 && (!in->mips || !in->dl_tick || !in->ul_tick || !in->init_adv_tick))
+    return fail(c, FOGNET_ERR_ARG, "null node parameter arrays");
+  memset(a, 0, sizeof *a);
+  a->R = in->R;
+  a->T = in->T;
+  a->N = in->N;
+  a->node_stride = in->node_stride;
+  a->q_log2 = qlog;
+  // busy (a sum of at most Q pending service times) must stay below 2^32 s
+  a->max_s = (uint32_t)(0xFFFFFFFFull / (uint64_t)q);
+  a->arrive = in->arrive_tick;
+  a->req = in->req_mips;
+  a->mips = in->mips;
+  a->dl = in->dl_tick;
+  a->ul = in->ul_tick;
+  a->init = in->init_adv_tick;
+  return FOGNET_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fognet_abi_version(void) { return FOGNET_ABI_VERSION; }
+
+const char* fognet_status_string(int s) {
+  switch (s) {
+    case FOGNET_OK: return "ok";
+    case FOGNET_ERR_ARG: return "invalid argument";
+    case FOGNET_ERR_NO_NODES: return "no fog nodes registered";
+    case FOGNET_ERR_DIV0: return "advertised MIPS of node 0 is zero";
+    case FOGNET_ERR_STATE: return "self-message already scheduled";
+    case FOGNET_ERR_DEVICE: return "HIP device error";
+    case FOGNET_ERR_OOM: return "out of device memory";
+    case FOGNET_ERR_CAPACITY: return "pending-task ring capacity exceeded";
+    case FOGNET_ERR_UNSUPPORTED: return "unsupported configuration";
+  }
+  return "unknown status";
+}
+
+int fognet_create(fognet_ctx** out, int hip_device) {
+  if (!out) return FOGNET_ERR_ARG;
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return FOGNET_ERR_DEVICE;
+  if (hip_device < 0 || hip_device >= n) return FOGNET_ERR_ARG;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, hip_device) != hipSuccess) return FOGNET_ERR_DEVICE;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return FOGNET_ERR_DEVICE;
+  fognet_ctx* c = new (std::nothrow) fognet_ctx();
+  if (!c) return FOGNET_ERR_OOM;
+  c->device = hip_device;
+  if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return FOGNET_ERR_DEVICE;
+  }
+  *out = c;
+  return FOGNET_OK;
+}
+
+void fognet_destroy(fognet_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->ring) (void)hipFree(c->ring);
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* fognet_last_error(const fognet_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int fognet_sync(fognet_ctx* c) {
+  if (!c) return FOGNET_ERR_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipError_t e = hipDeviceSynchronize();
+  return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "hipDeviceSynchronize");
+}
+
+int fognet_decide_batch_dev(fognet_ctx* c, int policy, int64_t m, int32_t n, const double* adv_busy,
+                            const int32_t* adv_mips, const int32_t* req, int32_t* out_node, int32_t* out_status,
+                            void* stream) {
+  if (!c) return FOGNET_ERR_ARG;
+  if (policy != FOGNET_POLICY_REF_V3) return fail(c, FOGNET_ERR_UNSUPPORTED, "unknown policy");
+  if (m < 0) return fail(c, FOGNET_ERR_ARG, "m < 0");
+  if (m > 0 && (!out_node || (n > 0 && (!adv_busy || !adv_mips || !req))))
+    return fail(c, FOGNET_ERR_ARG, "null pointer");
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipError_t e = fognet::launch_decide(m, n, adv_busy, adv_mips, req, out_node, out_status, (hipStream_t)stream);
+  return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "decide launch");
+}
+
+int fognet_decide(fognet_ctx* c, int policy, int32_t n, const double* adv_busy, const int32_t* adv_mips,
+                  int32_t req_mips, int32_t* out_node) {
+  if (!c || !out_node) return FOGNET_ERR_ARG;
+  if (n <= 0) return fail(c, FOGNET_ERR_NO_NODES, "n <= 0 (BrokerBaseApp3.cc:268 reads brokers[0])");
+  if (!adv_busy || !adv_mips) return fail(c, FOGNET_ERR_ARG, "null view");
+  int rc = set_device(c);
+  if (rc) return rc;
+  const size_t nb = (size_t)n * sizeof(double), nm = (size_t)n * sizeof(int32_t);
+  const size_t off_m = (nb + 255) & ~(size_t)255, off_r = (off_m + nm + 255) & ~(size_t)255;
+  const size_t off_o = off_r + 256, total = off_o + 256;
+  rc = ensure(c, &c->scratch, &c->scratch_bytes, total, "decide scratch");
+  if (rc) return rc;
+  char* s = (char*)c->scratch;
+  hipError_t e;
+  if ((e = hipMemcpyAsync(s, adv_busy, nb, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(s + off_m, adv_mips, nm, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(s + off_r, &req_mips, sizeof(int32_t), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return hip_fail(c, e, "decide copy-in");
+  e = fognet::launch_decide(1, n, (const double*)s, (const int32_t*)(s + off_m), (const int32_t*)(s + off_r),
+                            (int32_t*)(s + off_o), (int32_t*)(s + off_o + 4), c->stream);
+  if (e != hipSuccess) return hip_fail(c, e, "decide launch");
+  int32_t res[2] = {-1, FOGNET_ERR_DEVICE};
+  if ((e = hipMemcpyAsync(res, s + off_o, sizeof res, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+    return hip_fail(c, e, "decide copy-out");
+  if (res[1] != FOGNET_OK) return fail(c, res[1], fognet_status_string(res[1]));
+  *out_node = res[0];
+  return FOGNET_OK;
+}
+
+static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out, void* stream, int which) {
+  if (!c || !out) return FOGNET_ERR_ARG;
+  fognet::ReplayArgs a;
+  int rc = prepare(c, in, &a);
+  if (rc) return rc;
+  if (!out->stats) return fail(c, FOGNET_ERR_ARG, "stats output is required (per-replication status)");
+  if (!out->node || !out->status || !out->start_tick || !out->done_tick)
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "per-task outputs are required (stats-only mode not implemented)");
+  if (a.R == 0) return FOGNET_OK;
+  rc = set_device(c);
+  if (rc) return rc;
+  a.out_node = out->node;
+  a.out_status = out->status;
+  a.out_start = out->start_tick;
+  a.out_done = out->done_tick;
+  a.out_stats = out->stats;
+  hipError_t e = hipSuccess;
+  if (which & 1) {
+    const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
+    rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ring_bytes, "ring workspace");
+    if (rc) return rc;
+    a.ring = c->ring;
+    e = fognet::launch_replay(a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(c, e, "replay launch");
+  }
+  if (which & 2) {
+    e = fognet::launch_rep_stats(a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(c, e, "stats launch");
+  }
+  return FOGNET_OK;
+}
+
+int fognet_replay_dev(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out, void* stream) {
+  return stage(c, in, out, stream, 1);
+}
+
+int fognet_rep_stats_dev(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out, void* stream) {
+  return stage(c, in, out, stream, 2);
+}
+
+int fognet_run_batch_dev(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out, void* stream) {
+  return stage(c, in, out, stream, 3);
+}
+
+int fognet_run_batch(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out) {
+  if (!c || !in || !out) return FOGNET_ERR_ARG;
+  fognet::ReplayArgs chk;
+  int rc = prepare(c, in, &chk);
+  if (rc) return rc;
+  rc = set_device(c);
+  if (rc) return rc;
+  const size_t R = (size_t)in->R, T = (size_t)in->T, N = (size_t)in->N;
+  const size_t NR = in->node_stride ? R : 1;
+  const size_t sizes[] = {R * T * 8, R * T * 4, NR * N * 4, NR * N * 8, NR * N * 8, NR * N * 8,
+                          R * T * 4, R * T * 1, R * T * 8, R * T * 8, R * sizeof(fognet_rep_stats)};
+  const int nbuf = (int)(sizeof sizes / sizeof sizes[0]);
+  void* d[11] = {};
+  auto cleanup = [&]() {
+    for (int i = 0; i < nbuf; ++i)
+      if (d[i]) (void)hipFree(d[i]);
+  };
+  for (int i = 0; i < nbuf; ++i) {
+    hipError_t e = hipMalloc(&d[i], sizes[i] ? sizes[i] : 8);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_fail(c, e, "hipMalloc batch");
+    }
+  }
+  const void* hsrc[6] = {in->arrive_tick, in->req_mips, in->mips, in->dl_tick, in->ul_tick, in->init_adv_tick};
+  for (int i = 0; i < 6; ++i) {
+    if (!sizes[i]) continue;
+    hipError_t e = hipMemcpyAsync(d[i], hsrc[i], sizes[i], hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_fail(c, e, "copy-in");
+    }
+  }
+  fognet_batch_in din = *in;
+  din.arrive_tick = (const int64_t*)d[0];
+  din.req_mips = (const int32_t*)d[1];
+  din.mips = (const int32_t*)d[2];
+  din.dl_tick = (const int64_t*)d[3];
+  din.ul_tick = (const int64_t*)d[4];
+  din.init_adv_tick = (const int64_t*)d[5];
+  fognet_batch_out dout = {(int32_t*)d[6], (uint8_t*)d[7], (int64_t*)d[8], (int64_t*)d[9], (fognet_rep_stats*)d[10]};
+  rc = fognet_run_batch_dev(c, &din, &dout, c->stream);
+  if (rc) {
+    cleanup();
+    return rc;
+  }
+  void* hdst[5] = {out->node, out->status, out->start_tick, out->done_tick, out->stats};
+  for (int i = 0; i < 5; ++i) {
+    if (!hdst[i] || !sizes[6 + i]) continue;
+    hipError_t e = hipMemcpyAsync(hdst[i], d[6 + i], sizes[6 + i], hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_fail(c, e, "copy-out");
+    }
+  }
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    cleanup();
+    return hip_fail(c, e, "batch sync");
+  }
+  cleanup();
+  if (out->stats)
+    for (size_t r = 0; r < R; ++r)
+      if (out->stats[r].status != FOGNET_OK) {
+        char buf[96];
+        snprintf(buf, sizeof buf, "replication %zu: %s", r, fognet_status_string(out->stats[r].status));
+        return fail(c, out->stats[r].status, buf);
+      }
+  return FOGNET_OK;
+}
+
+int fognet_reduce_stats_dev(fognet_ctx* c, const fognet_rep_stats* stats, int32_t R, fognet_job_stats* out,
+                            void* stream) {
+  if (!c || !out || (R > 0 && !stats) || R < 0) return FOGNET_ERR_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipError_t e = fognet::launch_reduce_stats(stats, R, out, (hipStream_t)stream);
+  return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "reduce launch");
+}
+
+void fognet_job_stats_init(fognet_job_stats* s) {
+  if (!s) return;
+  memset(s, 0, sizeof *s);
+  s->queue_min_ticks = s->resp_min_ticks = INT64_MAX;
+  s->queue_max_ticks = s->resp_max_ticks = s->last_tick = INT64_MIN;
+}
+
+static void add192_host(uint64_t* a, const uint64_t* b) {
+  unsigned __int128 s = (unsigned __int128)a[0] + b[0];
+  a[0] = (uint64_t)s;
+  s = (unsigned __int128)a[1] + b[1] + (uint64_t)(s >> 64);
+  a[1] = (uint64_t)s;
+  a[2] = a[2] + b[2] + (uint64_t)(s >> 64);
+}
+
+void fognet_job_stats_merge(fognet_job_stats* a, const fognet_job_stats* b) {
+  if (!a || !b) return;
+  a->n_reps += b->n_reps;
+  a->n_failed += b->n_failed;
+  a->n_tasks += b->n_tasks;
+  a->n_queued += b->n_queued;
+  a->n_started += b->n_started;
+  a->events += b->events;
+  if (b->last_tick > a->last_tick) a->last_tick = b->last_tick;
+  if (b->queue_min_ticks < a->queue_min_ticks) a->queue_min_ticks = b->queue_min_ticks;
+  if (b->queue_max_ticks > a->queue_max_ticks) a->queue_max_ticks = b->queue_max_ticks;
+  if (b->resp_min_ticks < a->resp_min_ticks) a->resp_min_ticks = b->resp_min_ticks;
+  if (b->resp_max_ticks > a->resp_max_ticks) a->resp_max_ticks = b->resp_max_ticks;
+  if (b->max_pending > a->max_pending) a->max_pending = b->max_pending;
+  add192_host(a->queue_sum, b->queue_sum);
+  add192_host(a->queue_sq, b->queue_sq);
+  add192_host(a->resp_sum, b->resp_sum);
+  add192_host(a->resp_sq, b->resp_sq);
+}
+
+int fognet_gen_trace_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t r0, int32_t R, int32_t T, int32_t N,
+                         int64_t* arrive_tick, int32_t* req_mips, int32_t* mips, int64_t* dl_tick, int64_t* ul_tick,
+                         int64_t* init_adv_tick, void* stream) {
+  if (!c || !p) return FOGNET_ERR_ARG;
+  if (R < 0 || T < 0 || N <= 0 || r0 < 0) return fail(c, FOGNET_ERR_ARG, "bad sizes");
+  if (p->req_lo < 0 || p->req_hi < p->req_lo) return fail(c, FOGNET_ERR_ARG, "bad req range");
+  if (R > 0 && (!p->mean_gap_ticks || !p->lat_scale || !mips || !dl_tick || !ul_tick || !init_adv_tick ||
+                (T > 0 && (!arrive_tick || !req_mips))))
+    return fail(c, FOGNET_ERR_ARG, "null pointer");
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipError_t e = fognet::launch_gen_trace(*p, r0, R, T, N, arrive_tick, req_mips, mips, dl_tick, ul_tick,
+                                          init_adv_tick, (hipStream_t)stream);
+  return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "tracegen launch");
+}
+
+}  // extern "C"

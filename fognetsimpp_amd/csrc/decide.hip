@@ -1,0 +1,92 @@
+// decide.hip — M independent broker decisions, BrokerBaseApp3.cc:265-281,
+// evaluated with the reference's exact arithmetic:
+//   tskTime = req / brokers[0].MIPS           (int / int, then double)
+//   tempp   = busy[0] + tskTime
+//   for j in 0..n-1: if busy[j] + tskTime < tempp: tempp = ..., k = j   (strict '<')
+// The sequential scan returns the first index attaining the minimum of
+// c_j = busy_j + tskTime among non-NaN c_j, or 0 when c_0 is NaN (no
+// comparison against a NaN tempp is ever true).  One wavefront per query; the
+// lanes scan strided candidates and a (value, index) reduction keeps the
+// earliest index on ties, which reproduces the sequential result exactly.
+#include "internal.h"
+
+namespace fognet {
+
+namespace {
+
+constexpr int kDecideThreads = 256;  // 4 queries per workgroup
+
+struct Cand {
+  double c;
+  int32_t j;
+};
+
+// a precedes b in the scan's outcome
+__device__ __forceinline__ bool better(const Cand& a, const Cand& b) {
+  if (a.j < 0) return false;
+  if (b.j < 0) return true;
+  return a.c < b.c || (a.c == b.c && a.j < b.j);
+}
+
+__global__ __launch_bounds__(kDecideThreads) void decide_kernel(int64_t m, int32_t n, const double* busy,
+                                                                 const int32_t* mips, const int32_t* req,
+                                                                 int32_t* node, int32_t* status) {
+  const int64_t q = (int64_t)blockIdx.x * (kDecideThreads / kWave) + threadIdx.x / kWave;
+  const int lane = threadIdx.x % kWave;
+  if (q >= m) return;  // whole wave exits together
+  int32_t rc = FOGNET_OK;
+  int32_t out = -1;
+  if (n <= 0) {
+    rc = FOGNET_ERR_NO_NODES;
+  } else {
+    const double* b = busy + q * (int64_t)n;
+    const int32_t m0 = mips[q * (int64_t)n];
+    const int32_t rq = req[q];
+    if (m0 == 0) {
+      rc = FOGNET_ERR_DIV0;
+    } else if (m0 == -1 && rq == INT32_MIN) {
+      rc = FOGNET_ERR_ARG;  // INT_MIN / -1 overflows in the reference
+    } else {
+      const double tsk = (double)(rq / m0);
+      const double c0 = b[0] + tsk;
+      if (c0 != c0) {
+        out = 0;  // tempp is NaN: no candidate can replace node 0
+      } else {
+        Cand best = {0.0, -1};
+        for (int32_t j = lane; j < n; j += kWave) {
+          const double c = b[j] + tsk;
+          if (c == c) {
+            const Cand cj = {c, j};
+            if (better(cj, best)) best = cj;
+          }
+        }
+        // wave reduction, butterfly over xor distances
+        for (int off = 32; off > 0; off >>= 1) {
+          Cand o;
+          o.c = __shfl_xor(best.c, off);
+          o.j = __shfl_xor(best.j, off);
+          if (better(o, best)) best = o;
+        }
+        out = best.j;  // node 0 is a non-NaN candidate, so best.j >= 0
+      }
+    }
+  }
+  if (lane == 0) {
+    node[q] = out;
+    if (status) status[q] = rc;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_decide(int64_t m, int32_t n, const double* busy, const int32_t* mips, const int32_t* req,
+                         int32_t* node, int32_t* status, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  const int per = kDecideThreads / kWave;
+  const int64_t blocks = (m + per - 1) / per;
+  hipLaunchKernelGGL(decide_kernel, dim3((unsigned)blocks), dim3(kDecideThreads), 0, s, m, n, busy, mips, req,
+                     node, status);
+  return hipGetLastError();
+}
+
+}  // namespace fognet

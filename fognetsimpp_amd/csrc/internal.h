@@ -1,0 +1,150 @@
+// internal.h — device helpers and kernel entry points shared by the
+// libfognet_hip translation units.  gfx950 (CDNA4, wave64) only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fognet_hip.h"
+
+namespace fognet {
+
+constexpr int kWave = 64;
+constexpr int64_t kTicksPerSecond = FOGNET_TICKS_PER_SECOND;
+constexpr int kMaxNodesPerLane = 4;  // N <= 256 in the register-resident replay kernel
+
+// ---------------------------------------------------------------- lane moves
+
+__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, int lane) {
+  const uint32_t lo = readlane_u32((uint32_t)(uint64_t)v, lane);
+  const uint32_t hi = readlane_u32((uint32_t)((uint64_t)v >> 32), lane);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// DPP move of a 32-bit value (bound_ctrl: out-of-row sources read 0; every
+// pattern used below stays inside a row of 16 lanes).
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xF, 0xF, true);
+}
+
+template <int kCtrl>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const uint32_t lo = dpp_u32<kCtrl>((uint32_t)v);
+  const uint32_t hi = dpp_u32<kCtrl>((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return b < a ? b : a; }
+
+// Minimum of a u64 over the 64 lanes; result is wave-uniform.  Must be called
+// with every lane active.  Four in-row DPP butterflies (quad_perm [1,0,3,2],
+// [2,3,0,1], row_half_mirror, row_mirror) leave each row of 16 holding its
+// minimum; the four row minima are then combined on the scalar side.
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  v = umin64(v, dpp_u64<0xB1>(v));
+  v = umin64(v, dpp_u64<0x4E>(v));
+  v = umin64(v, dpp_u64<0x141>(v));
+  v = umin64(v, dpp_u64<0x140>(v));
+  const uint64_t r0 = (uint64_t)readlane_i64((int64_t)v, 0);
+  const uint64_t r1 = (uint64_t)readlane_i64((int64_t)v, 16);
+  const uint64_t r2 = (uint64_t)readlane_i64((int64_t)v, 32);
+  const uint64_t r3 = (uint64_t)readlane_i64((int64_t)v, 48);
+  return umin64(umin64(r0, r1), umin64(r2, r3));
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const U4 n = {(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,
+                  (uint32_t)p0};
+    c = n;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// -ln(u), u in (0, 1], using only IEEE +,-,*,/ so the host restatement
+// (tests/tracegen.py::neg_log_unit) reproduces it bit for bit.
+__device__ __forceinline__ double neg_log_unit(double u) {
+#pragma clang fp contract(off)
+  const uint64_t bits = (uint64_t)__double_as_longlong(u);
+  int64_t e = (int64_t)((bits >> 52) & 0x7FF) - 1023;
+  double m = __longlong_as_double((long long)((bits & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull));
+  if (m > 1.4142135623730951) {
+    m = m * 0.5;
+    e = e + 1;
+  }
+  const double f = (m - 1.0) / (m + 1.0);
+  const double f2 = f * f;
+  double acc = 1.0 / 21.0;
+  acc = acc * f2 + (1.0 / 19.0);
+  acc = acc * f2 + (1.0 / 17.0);
+  acc = acc * f2 + (1.0 / 15.0);
+  acc = acc * f2 + (1.0 / 13.0);
+  acc = acc * f2 + (1.0 / 11.0);
+  acc = acc * f2 + (1.0 / 9.0);
+  acc = acc * f2 + (1.0 / 7.0);
+  acc = acc * f2 + (1.0 / 5.0);
+  acc = acc * f2 + (1.0 / 3.0);
+  acc = acc * f2 + 1.0;
+  const double ln_m = 2.0 * f * acc;
+  const double ln_u = (double)e * 0.6931471805599453 + ln_m;
+  return -ln_u;
+}
+
+// ---------------------------------------------------------------- replay
+
+// Pending-task ring entry: one per task assigned to a node, kept until the
+// advertisement of its completion has been applied to the broker's view.
+struct RingEntry {
+  int64_t a;   // arrival tick at the node (broker decision tick + dl)
+  uint32_t C;  // cumulative service seconds assigned to the node, this task included (mod 2^32)
+  uint32_t S;  // service seconds, requiredMIPS / MIPS (int division)
+};
+static_assert(sizeof(RingEntry) == 16, "ring entry is 16 B");
+
+struct ReplayArgs {
+  int32_t R, T, N, node_stride;
+  int32_t q_log2;  // ring capacity per node = 1 << q_log2
+  uint32_t max_s;  // largest admissible service time (keeps busy < 2^32)
+  const int64_t* arrive;
+  const int32_t* req;
+  const int32_t* mips;
+  const int64_t* dl;
+  const int64_t* ul;
+  const int64_t* init;
+  int32_t* out_node;
+  uint8_t* out_status;
+  int64_t* out_start;
+  int64_t* out_done;
+  fognet_rep_stats* out_stats;
+  RingEntry* ring;  // [R][N][Q]
+};
+
+hipError_t launch_replay(const ReplayArgs& a, hipStream_t s);
+hipError_t launch_rep_stats(const ReplayArgs& a, hipStream_t s);
+hipError_t launch_reduce_stats(const fognet_rep_stats* st, int32_t R, fognet_job_stats* out,
+                               hipStream_t s);
+hipError_t launch_decide(int64_t m, int32_t n, const double* busy, const int32_t* mips,
+                         const int32_t* req, int32_t* node, int32_t* status, hipStream_t s);
+hipError_t launch_gen_trace(const fognet_gen_params& p, int64_t r0, int32_t R, int32_t T, int32_t N,
+                            int64_t* arrive, int32_t* req, int32_t* mips, int64_t* dl, int64_t* ul,
+                            int64_t* init, hipStream_t s);
+
+}  // namespace fognet

@@ -1,0 +1,264 @@
+"""Host-side mirror of FogNetSim++'s offload-decision interface over libfognet_hip.
+
+Device memory, streams and (for multi-GPU) RCCL come from PyTorch; every
+decision, node update and statistic is computed by the gfx950 kernels in
+``csrc/``.  Names follow the reference:
+
+* :class:`BrokerBaseApp3` — the broker's allocation policy plug-in
+  (``simple BrokerBaseApp3 like IUDPApp``, src/mqttapp/BrokerBaseApp3.ned:20);
+  :meth:`BrokerBaseApp3.sendPubAck` is the decision core of
+  ``BrokerBaseApp3::sendPubAck(..., status=false)`` (BrokerBaseApp3.cc:265-281).
+* :class:`Context` + :func:`run_batch` — R independent trace replays of the
+  broker/fog-node loop (BrokerBaseApp3.cc:123-158, ComputeBrokerApp3.cc:205-320).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _abi
+from ._abi import FognetError
+
+_TENSOR_DTYPES = {
+    "arrive": torch.int64, "req": torch.int32, "mips": torch.int32,
+    "dl": torch.int64, "ul": torch.int64, "init": torch.int64,
+}
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream_ptr(device) -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Context:
+    """A fognet_ctx bound to one HIP device (gfx950 required)."""
+
+    def __init__(self, device: int | torch.device = 0):
+        if isinstance(device, torch.device):
+            device = device.index or 0
+        self.device = int(device)
+        self._lib = _abi.load()
+        h = C.c_void_p()
+        rc = self._lib.fognet_create(C.byref(h), self.device)
+        if rc != _abi.FOGNET_OK:
+            raise FognetError(rc, f"fognet_create(device={self.device}) failed: {_abi.status_string(rc)}")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.fognet_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc: int, what: str = ""):
+        if rc != _abi.FOGNET_OK:
+            msg = self._lib.fognet_last_error(self._h).decode()
+            raise FognetError(rc, f"{what}: {msg}" if what else msg)
+
+    def sync(self):
+        self.check(self._lib.fognet_sync(self._h), "sync")
+
+
+class BrokerBaseApp3:
+    """Allocation policy of BrokerBaseApp3 (src/mqttapp/BrokerBaseApp3.cc).
+
+    ``brokers`` is the broker's view of the registered fog nodes in CONNECT
+    order: advertised busy time (double) and MIPS (int) per node
+    (Broker.cc:21-22, updated only by adverts, BrokerBaseApp3.cc:123-130).
+    """
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def sendPubAck(self, adv_busy, adv_mips, MIPSRequired: int) -> int:  # noqa: N802,N803 (reference names)
+        """Index of the node the task is offloaded to (BrokerBaseApp3.cc:267-281).
+
+        Raises FognetError(FOGNET_ERR_NO_NODES) for an empty view (the reference
+        dereferences brokers[0], UB) and FognetError(FOGNET_ERR_DIV0) when node 0
+        has not advertised yet (MIPS 0: SIGFPE in the reference).
+        """
+        busy = np.ascontiguousarray(adv_busy, dtype=np.float64)
+        mips = np.ascontiguousarray(adv_mips, dtype=np.int32)
+        if busy.shape != mips.shape or busy.ndim != 1:
+            raise FognetError(_abi.FOGNET_ERR_ARG, "adv_busy/adv_mips must be 1-D and equal length")
+        out = C.c_int32(-1)
+        lib = self.ctx._lib
+        rc = lib.fognet_decide(self.ctx.handle, _abi.FOGNET_POLICY_REF_V3, len(busy),
+                               busy.ctypes.data_as(C.c_void_p), mips.ctypes.data_as(C.c_void_p),
+                               int(MIPSRequired), C.byref(out))
+        self.ctx.check(rc, "sendPubAck")
+        return out.value
+
+    def sendPubAck_batch(self, adv_busy: torch.Tensor, adv_mips: torch.Tensor, req: torch.Tensor):  # noqa: N802
+        """M independent decisions on device tensors [M, n]; returns (node, status) int32 [M]."""
+        m, n = adv_busy.shape
+        node = torch.empty(m, dtype=torch.int32, device=adv_busy.device)
+        status = torch.empty(m, dtype=torch.int32, device=adv_busy.device)
+        rc = self.ctx._lib.fognet_decide_batch_dev(
+            self.ctx.handle, _abi.FOGNET_POLICY_REF_V3, m, n,
+            _ptr(adv_busy.contiguous()), _ptr(adv_mips.contiguous()), _ptr(req.contiguous()),
+            _ptr(node), _ptr(status), _stream_ptr(adv_busy.device))
+        self.ctx.check(rc, "decide_batch")
+        return node, status
+
+
+@dataclass
+class BatchResult:
+    node: torch.Tensor        # [R, T] int32
+    status: torch.Tensor      # [R, T] uint8 (5 started / 4 queued)
+    start_tick: torch.Tensor  # [R, T] int64
+    done_tick: torch.Tensor   # [R, T] int64
+    stats: torch.Tensor       # [R * sizeof(fognet_rep_stats)] uint8 (device)
+
+    def rep_stats(self) -> np.ndarray:
+        return self.stats.cpu().numpy().view(_abi.REP_STATS_DTYPE)
+
+
+def allocate_outputs(R: int, T: int, device) -> BatchResult:
+    return BatchResult(
+        node=torch.empty((R, T), dtype=torch.int32, device=device),
+        status=torch.empty((R, T), dtype=torch.uint8, device=device),
+        start_tick=torch.empty((R, T), dtype=torch.int64, device=device),
+        done_tick=torch.empty((R, T), dtype=torch.int64, device=device),
+        stats=torch.zeros(R * _abi.REP_STATS_DTYPE.itemsize, dtype=torch.uint8, device=device),
+    )
+
+
+def as_device_trace(trace: dict, device) -> dict:
+    """numpy/torch trace dict -> contiguous device tensors of the ABI dtypes."""
+    out = {}
+    for k, dt in _TENSOR_DTYPES.items():
+        v = trace[k]
+        t = v if isinstance(v, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(v))
+        out[k] = t.to(device=device, dtype=dt).contiguous()
+    if out["arrive"].dim() == 1:
+        out["arrive"] = out["arrive"].unsqueeze(0)
+        out["req"] = out["req"].unsqueeze(0)
+    return out
+
+
+def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_capacity: int = 0,
+              stream=None, stage: str = "all") -> BatchResult:
+    """Enqueue R trace replays (fognet_run_batch_dev) on the current stream.
+
+    ``trace``: device tensors arrive/req [R, T], node params mips/dl/ul/init
+    [R, N] (per replication) or [N] (shared).  ``stage``: "all", "replay"
+    (fognet_replay_dev) or "stats" (fognet_rep_stats_dev).
+    """
+    arrive, req = trace["arrive"], trace["req"]
+    R, T = arrive.shape
+    mips = trace["mips"]
+    N = mips.shape[-1]
+    stride = N if mips.dim() == 2 else 0
+    if out is None:
+        out = allocate_outputs(R, T, arrive.device)
+    bi = _abi.BatchIn(R, T, N, _abi.FOGNET_POLICY_REF_V3, stride, ring_capacity,
+                      _ptr(arrive), _ptr(req), _ptr(mips), _ptr(trace["dl"]), _ptr(trace["ul"]),
+                      _ptr(trace["init"]))
+    bo = _abi.BatchOut(_ptr(out.node), _ptr(out.status), _ptr(out.start_tick), _ptr(out.done_tick),
+                       _ptr(out.stats))
+    s = C.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(arrive.device)
+    fn = {"all": ctx._lib.fognet_run_batch_dev, "replay": ctx._lib.fognet_replay_dev,
+          "stats": ctx._lib.fognet_rep_stats_dev}[stage]
+    ctx.check(fn(ctx.handle, C.byref(bi), C.byref(bo), s), f"run_batch[{stage}]")
+    return out
+
+
+def reduce_stats(ctx: Context, stats: torch.Tensor, R: int) -> np.ndarray:
+    """Exact job-level reduction on the device; returns a JOB_STATS_DTYPE record."""
+    out = torch.zeros(_abi.JOB_STATS_DTYPE.itemsize, dtype=torch.uint8, device=stats.device)
+    ctx.check(ctx._lib.fognet_reduce_stats_dev(ctx.handle, _ptr(stats), R, _ptr(out), _stream_ptr(stats.device)),
+              "reduce_stats")
+    return out.cpu().numpy().view(_abi.JOB_STATS_DTYPE)[0]
+
+
+def merge_job_stats(records) -> np.ndarray:
+    """Exact host merge of job records (e.g. one per GPU after an all-gather)."""
+    lib = _abi.load()
+    acc = _abi.JobStats()
+    lib.fognet_job_stats_init(C.byref(acc))
+    for rec in records:
+        b = _abi.JobStats.from_buffer_copy(np.ascontiguousarray(rec).tobytes())
+        lib.fognet_job_stats_merge(C.byref(acc), C.byref(b))
+    return np.frombuffer(bytes(acc), dtype=_abi.JOB_STATS_DTYPE)[0]
+
+
+def _u192(limbs) -> int:
+    return int(limbs[0]) | (int(limbs[1]) << 64) | (int(limbs[2]) << 128)
+
+
+def summarize(job) -> dict:
+    """`.sca`-style fields (count/mean/stddev/sum/sqrsum/min/max, ms) of a job record,
+    mirroring cStdDev's output for queueTime (ComputeBrokerApp3.ned:45-46)."""
+    def block(n, s, q, lo, hi):
+        n = int(n)
+        s, q = _u192(s), _u192(q)
+        if n == 0:
+            return dict(count=0)
+        mean = s / n
+        var = (q - s * s / n) / (n - 1) if n > 1 else 0.0
+        return dict(count=n, mean=mean / 1e9, stddev=max(var, 0.0) ** 0.5 / 1e9, sum=s / 1e9,
+                    sqrsum=q / 1e18, min=int(lo) / 1e9, max=int(hi) / 1e9)
+
+    return {
+        "replications": int(job["n_reps"]), "failed": int(job["n_failed"]),
+        "decisions": int(job["n_tasks"]), "queued": int(job["n_queued"]), "started": int(job["n_started"]),
+        "queueTime_ms": block(job["n_queued"], job["queue_sum"], job["queue_sq"], job["queue_min_ticks"],
+                              job["queue_max_ticks"]),
+        "response_ms": block(job["n_tasks"], job["resp_sum"], job["resp_sq"], job["resp_min_ticks"],
+                             job["resp_max_ticks"]),
+        "max_pending": int(job["max_pending"]),
+    }
+
+
+def generate_trace(ctx: Context, seed: int, R: int, T: int, N: int, mean_gap_ticks, lat_scale,
+                   r0: int = 0, req_lo: int = 1000, req_hi: int = 64000, device=None) -> dict:
+    """Device trace generator (recipe: csrc/tracegen.hip); per-replication
+    ``mean_gap_ticks`` (float64 [R]) and ``lat_scale`` (int64 [R])."""
+    device = device if device is not None else torch.device("cuda", ctx.device)
+    mg = torch.as_tensor(np.asarray(mean_gap_ticks, dtype=np.float64).reshape(R), device=device)
+    ls = torch.as_tensor(np.asarray(lat_scale, dtype=np.int64).reshape(R), device=device)
+    tr = {
+        "arrive": torch.empty((R, T), dtype=torch.int64, device=device),
+        "req": torch.empty((R, T), dtype=torch.int32, device=device),
+        "mips": torch.empty((R, N), dtype=torch.int32, device=device),
+        "dl": torch.empty((R, N), dtype=torch.int64, device=device),
+        "ul": torch.empty((R, N), dtype=torch.int64, device=device),
+        "init": torch.empty((R, N), dtype=torch.int64, device=device),
+    }
+    gp = _abi.GenParams(seed & 0xFFFFFFFF, req_lo, req_hi, 0, _ptr(mg), _ptr(ls))
+    rc = ctx._lib.fognet_gen_trace_dev(ctx.handle, C.byref(gp), r0, R, T, N, _ptr(tr["arrive"]), _ptr(tr["req"]),
+                                       _ptr(tr["mips"]), _ptr(tr["dl"]), _ptr(tr["ul"]), _ptr(tr["init"]),
+                                       _stream_ptr(device))
+    ctx.check(rc, "gen_trace")
+    tr["_keep"] = (mg, ls)
+    return tr
+
+
+def sweep_params(r_global: np.ndarray, N: int, rho=None, lat_scale=None, req_lo=1000, req_hi=64000):
+    """Per-replication (mean_gap_ticks, lat_scale) for the C3 policy sweep:
+    rho = (0.5, 0.8, 0.95)[r % 3], latency x(1, 10, 100)[(r // 3) % 3]
+    unless fixed values are given.  mips pattern 1000*(1 + j % 4)."""
+    r_global = np.asarray(r_global, dtype=np.int64)
+    mips = 1000.0 * (1 + (np.arange(N) % 4))
+    es = 0.5 * (req_lo + req_hi) * float(np.mean(1.0 / mips))
+    rho_r = np.full(r_global.shape, rho, np.float64) if rho is not None else np.array((0.5, 0.8, 0.95))[r_global % 3]
+    sc = (np.full(r_global.shape, lat_scale, np.int64) if lat_scale is not None
+          else np.array((1, 10, 100), np.int64)[(r_global // 3) % 3])
+    mean_gap = es / (N * rho_r) * _abi.TICKS_PER_SECOND
+    return mean_gap, sc

@@ -1,0 +1,183 @@
+/*
+ * fognet_hip.h — C ABI of libfognet_hip, the MI355X (gfx950) engine for
+ * FogNetSim++'s offload-decision hot path.
+ *
+ * Reference interfaces replaced (paths relative to the FogNetSim++ tree):
+ *   - the broker's allocation argmin, BrokerBaseApp3::sendPubAck(status=false),
+ *     src/mqttapp/BrokerBaseApp3.cc:265-304 (decision core :267-281)
+ *       -> fognet_decide / fognet_decide_batch_dev;
+ *   - the fog node's task arrival, ComputeBrokerApp3::processPacket,
+ *     src/mqttapp/ComputeBrokerApp3.cc:269-320, its completion + advertisement,
+ *     ComputeBrokerApp3::releaseResource / advertiseMIPS, :224-256 / :205-222,
+ *     and the broker's view update on each advertisement,
+ *     BrokerBaseApp3.cc:123-130 -> fognet_run_batch[_dev] (R independent
+ *     trace replays of the whole decide -> queue -> complete -> advertise loop);
+ *   - the queueTime statistic (ComputeBrokerApp3.cc:238, ComputeBrokerApp3.ned:45-46)
+ *     -> fognet_rep_stats, reduced on the device (fognet_reduce_stats_dev).
+ *
+ * Conventions
+ *   - Every entry point returns a fognet_status; no exception crosses the ABI.
+ *     fognet_last_error() gives the message of the last failure on a context.
+ *   - The caller owns every buffer.  *_dev entry points take device pointers
+ *     (hipMalloc'd, or torch.cuda tensors) and enqueue on the given hipStream_t
+ *     (NULL = default stream); the others take host pointers and copy.
+ *   - A fognet_ctx is not thread-safe; use one per host thread (OMNeT++'s
+ *     sequential kernel is single-threaded anyway).
+ *   - Deterministic: identical inputs give bit-identical outputs.
+ *   - Time is OMNeT++ 4.6 simtime_t raw int64 at scale 1e-12 s ("ticks").
+ */
+#ifndef FOGNET_HIP_H
+#define FOGNET_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FOGNET_ABI_VERSION 1
+#define FOGNET_TICKS_PER_SECOND 1000000000000LL
+
+typedef int64_t fognet_tick;
+typedef struct fognet_ctx fognet_ctx;
+
+typedef enum fognet_status {
+    FOGNET_OK = 0,
+    FOGNET_ERR_ARG = 1,         /* invalid argument / precondition (see fognet_run_batch)            */
+    FOGNET_ERR_NO_NODES = 2,    /* n == 0: BrokerBaseApp3.cc:268 reads brokers[0] first (UB)           */
+    FOGNET_ERR_DIV0 = 3,        /* advertised MIPS of node 0 is 0: BrokerBaseApp3.cc:268 SIGFPE        */
+    FOGNET_ERR_STATE = 4,       /* selfMsg already scheduled: ComputeBrokerApp3.cc:301 cRuntimeError   */
+    FOGNET_ERR_DEVICE = 5,      /* HIP runtime failure or no gfx950 device                             */
+    FOGNET_ERR_OOM = 6,
+    FOGNET_ERR_CAPACITY = 7,    /* a node had more than ring_capacity tasks pending                    */
+    FOGNET_ERR_UNSUPPORTED = 8  /* configuration not implemented (e.g. N > 256, unknown policy)        */
+} fognet_status;
+
+typedef enum fognet_policy {
+    FOGNET_POLICY_REF_V3 = 1 /* BrokerBaseApp3: argmin(busy_j + req / mips_0), int division,
+                                strict '<' (ties -> lowest index), stale advertised view        */
+} fognet_policy;
+
+/* Per-replication statistics.  Times are kept in exact ticks; 128-bit sums are
+ * split into (lo, hi) uint64 halves so results are bit-reproducible. */
+typedef struct fognet_rep_stats {
+    int64_t n_tasks;          /* decisions made                                                   */
+    int64_t n_queued;         /* node acks with status 4 (= queueTime emissions, :238)             */
+    int64_t n_started;        /* node acks with status 5                                          */
+    int64_t last_tick;        /* latest RELEASERESOURCE tick (makespan)                           */
+    int64_t queue_min_ticks, queue_max_ticks; /* over queued tasks: start - arrival at node        */
+    int64_t resp_min_ticks, resp_max_ticks;   /* over all tasks: done - arrival at broker          */
+    uint64_t queue_sum_lo, queue_sum_hi, queue_sq_lo, queue_sq_hi;
+    uint64_t resp_sum_lo, resp_sum_hi, resp_sq_lo, resp_sq_hi;
+    int64_t events;           /* reference FES events this replay stands for (2N + 4 per task)    */
+    int32_t max_pending;      /* max tasks assigned to one node whose completion advert had not
+                                 reached the broker yet (ring occupancy)                          */
+    int32_t status;           /* fognet_status of this replication                                */
+} fognet_rep_stats;
+
+/* Job-level statistics: the exact sum of any set of fognet_rep_stats.  Sums
+ * are 192-bit unsigned integers (limbs [0] = least significant), so combining
+ * is associative and the result does not depend on how replications were
+ * sharded over GPUs.  Mean/stddev in ms follow as sum / n / 1e9 etc. */
+typedef struct fognet_job_stats {
+    int64_t n_reps, n_failed;
+    int64_t n_tasks, n_queued, n_started;
+    int64_t last_tick;
+    int64_t queue_min_ticks, queue_max_ticks, resp_min_ticks, resp_max_ticks;
+    uint64_t queue_sum[3], queue_sq[3], resp_sum[3], resp_sq[3];
+    int64_t events;
+    int64_t max_pending;
+} fognet_job_stats;
+
+/* R trace replays of T tasks over N fog nodes, SoA, row-major [R][T] / [R|1][N]. */
+typedef struct fognet_batch_in {
+    int32_t R, T, N;
+    int32_t policy;           /* fognet_policy                                                    */
+    int32_t node_stride;      /* 0: node params shared by all replications; N: one row each       */
+    int32_t ring_capacity;    /* per-node pending capacity, power of two (0 = default 1024)      */
+    const int64_t *arrive_tick;   /* [R][T] publish arrival at the broker, nondecreasing          */
+    const int32_t *req_mips;      /* [R][T] MqttMsgPublish.MIPSRequired, >= 0                      */
+    const int32_t *mips;          /* [R|1][N] node MIPS (> 0), CONNECT order = index order         */
+    const int64_t *dl_tick;       /* [R|1][N] broker -> node delivery latency (>= 0)               */
+    const int64_t *ul_tick;       /* [R|1][N] node -> broker delivery latency (>= 0)               */
+    const int64_t *init_adv_tick; /* [R|1][N] arrival of the node's first advert at the broker;
+                                     ul <= init_adv < arrive[0] (all adverts land before task 0)  */
+} fognet_batch_in;
+
+typedef struct fognet_batch_out {
+    int32_t *node;            /* [R][T] chosen node, nullable (stats-only run)                    */
+    uint8_t *status;          /* [R][T] 5 = started on arrival, 4 = queued; nullable              */
+    int64_t *start_tick;      /* [R][T] service start; nullable                                   */
+    int64_t *done_tick;       /* [R][T] completion (RELEASERESOURCE) tick; nullable               */
+    fognet_rep_stats *stats;  /* [R]; nullable                                                    */
+} fognet_batch_out;
+
+/* Synthetic trace recipe, generated on the device.
+ * Replication r uses Philox4x32-10 key (seed, r); see DESIGN.md §Trace generator. */
+typedef struct fognet_gen_params {
+    uint32_t seed;
+    int32_t req_lo, req_hi;       /* req ~ U_int[req_lo, req_hi]                                  */
+    int32_t pad;
+    const double *mean_gap_ticks; /* [R] exponential inter-arrival mean per replication (device)  */
+    const int64_t *lat_scale;     /* [R] latency multiplier per replication (device)              */
+} fognet_gen_params;
+
+int fognet_abi_version(void);
+const char *fognet_status_string(int status);
+
+/* Context: binds a HIP device (gfx950 required), owns the replay workspace. */
+int fognet_create(fognet_ctx **out, int hip_device);
+void fognet_destroy(fognet_ctx *ctx);
+const char *fognet_last_error(const fognet_ctx *ctx);
+
+/* Scalar drop-in for BrokerBaseApp3.cc:267-281 (the OMNeT++ adapter's call):
+ * host arrays of the broker's advertised view; evaluated on the device. */
+int fognet_decide(fognet_ctx *ctx, int policy, int32_t n, const double *adv_busy,
+                  const int32_t *adv_mips, int32_t req_mips, int32_t *out_node);
+
+/* M independent decisions, device pointers: adv_busy/adv_mips [M][n], req [M],
+ * out_node [M], out_status [M] (fognet_status per query, nullable). */
+int fognet_decide_batch_dev(fognet_ctx *ctx, int policy, int64_t m, int32_t n,
+                            const double *adv_busy, const int32_t *adv_mips, const int32_t *req,
+                            int32_t *out_node, int32_t *out_status, void *hip_stream);
+
+/* Batched replay engine.  *_dev: every pointer in in/out is a device pointer
+ * (the structs themselves are host memory).  Returns FOGNET_OK once enqueued;
+ * per-replication failures are reported in stats[r].status. */
+int fognet_run_batch_dev(fognet_ctx *ctx, const fognet_batch_in *in, fognet_batch_out *out,
+                         void *hip_stream);
+/* The two stages fognet_run_batch_dev enqueues, exposed so callers can time or
+ * overlap them: the replay kernel (decisions, node queues, adverts; fills
+ * node/status/start/done and stats[r].{status,n_tasks,max_pending,events}) and
+ * the statistics pass over its outputs (the remaining stats fields). */
+int fognet_replay_dev(fognet_ctx *ctx, const fognet_batch_in *in, fognet_batch_out *out, void *hip_stream);
+int fognet_rep_stats_dev(fognet_ctx *ctx, const fognet_batch_in *in, fognet_batch_out *out, void *hip_stream);
+/* Host-buffer variant: copies in, replays, copies out, synchronises.  Returns
+ * the first non-OK replication status, if any. */
+int fognet_run_batch(fognet_ctx *ctx, const fognet_batch_in *in, fognet_batch_out *out);
+
+/* Exact reduction of R per-replication stats (device pointers) into one job
+ * record (device pointer).  Replications with status != OK count in n_failed
+ * and contribute nothing else. */
+int fognet_reduce_stats_dev(fognet_ctx *ctx, const fognet_rep_stats *stats, int32_t R,
+                            fognet_job_stats *out, void *hip_stream);
+/* Host-side exact merge (used to combine per-GPU records after an all-gather):
+ * *acc = *acc (+) *other.  fognet_job_stats_init() sets the identity. */
+void fognet_job_stats_init(fognet_job_stats *s);
+void fognet_job_stats_merge(fognet_job_stats *acc, const fognet_job_stats *other);
+
+/* Device trace generator: fills arrive/req [R][T] and node params [R][N]
+ * (replications r0 .. r0+R-1 of the recipe; r0 lets GPUs shard one job). */
+int fognet_gen_trace_dev(fognet_ctx *ctx, const fognet_gen_params *p, int64_t r0, int32_t R,
+                         int32_t T, int32_t N, int64_t *arrive_tick, int32_t *req_mips,
+                         int32_t *mips, int64_t *dl_tick, int64_t *ul_tick, int64_t *init_adv_tick,
+                         void *hip_stream);
+
+/* Synchronise the context's device. */
+int fognet_sync(fognet_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FOGNET_HIP_H */

@@ -1,0 +1,481 @@
+/*
+ * fognet_oracle.c — TEST INFRASTRUCTURE ONLY (see fognet_oracle.h).
+ *
+ * A literal discrete-event restatement of the FogNetSim++ v3 offload path:
+ * every reference handler on the path is one function below, and events are
+ * dispatched from a future-event set ordered exactly like the OMNeT++ 4.6
+ * sequential kernel orders it: (arrival tick, scheduling priority = 0,
+ * insertion sequence).  Time is OMNeT++'s raw int64 simtime_t at the default
+ * scale of 1e-12 s ("ticks").
+ *
+ * Trace-replay model: the user side and INET are
+ * replaced by a pre-generated trace of publish arrivals at the broker and by
+ * fixed per-node link latencies.  Trace publishes and each node's initial
+ * ADVERTISEMIPS self-message are inserted into the FES before the run starts
+ * (nodes first, then publishes in trace order); everything else is inserted
+ * when the reference code would call scheduleAt()/sendTo().
+ */
+#include "fognet_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define TICKS_PER_SECOND 1000000000000LL /* simtime scale 1e-12 (no simtime-scale in any ini) */
+
+enum { EV_PUBLISH = 0, EV_ADVERT = 1, EV_TASK = 2, EV_SELF = 3 };
+enum { KIND_ADVERTISEMIPS = 1, KIND_RELEASERESOURCE = 2 }; /* ComputeBrokerApp3.h selfMsg kinds */
+
+typedef struct {
+    int64_t tick;
+    uint64_t seq;
+    int32_t type;
+    int32_t node;
+    int64_t task;
+    int32_t mips;    /* EV_ADVERT payload: FognetMsgAdvertiseMIPS.MIPS     */
+    uint32_t gen;    /* EV_SELF: selfMsg generation (cancelEvent support)  */
+    double busy;     /* EV_ADVERT payload: FognetMsgAdvertiseMIPS.busyTime */
+} ev_t;
+
+typedef struct {
+    ev_t *a;
+    int64_t n, cap;
+} heap_t;
+
+static int ev_less(const ev_t *x, const ev_t *y) {
+    if (x->tick != y->tick) return x->tick < y->tick;
+    return x->seq < y->seq;
+}
+
+static int heap_push(heap_t *h, const ev_t *e) {
+    if (h->n == h->cap) {
+        int64_t nc = h->cap ? h->cap * 2 : 256;
+        ev_t *na = (ev_t *)realloc(h->a, (size_t)nc * sizeof(ev_t));
+        if (!na) return ORC_ERR_OOM;
+        h->a = na;
+        h->cap = nc;
+    }
+    int64_t i = h->n++;
+    while (i > 0) {
+        int64_t p = (i - 1) >> 1;
+        if (!ev_less(e, &h->a[p])) break;
+        h->a[i] = h->a[p];
+        i = p;
+    }
+    h->a[i] = *e;
+    return ORC_OK;
+}
+
+static void heap_pop(heap_t *h, ev_t *out) {
+    *out = h->a[0];
+    ev_t last = h->a[--h->n];
+    int64_t i = 0;
+    for (;;) {
+        int64_t c = 2 * i + 1;
+        if (c >= h->n) break;
+        if (c + 1 < h->n && ev_less(&h->a[c + 1], &h->a[c])) c++;
+        if (!ev_less(&h->a[c], &last)) break;
+        h->a[i] = h->a[c];
+        i = c;
+    }
+    if (h->n > 0) h->a[i] = last;
+}
+
+/* Request record as the node keeps it (Request.cc:34-48; queueStartTime :25). */
+typedef struct {
+    int64_t task;
+    double required_time; /* tskTime, seconds (integer-valued) */
+    int64_t qstart_tick;  /* queueStartTime (ComputeBrokerApp3.cc:306) */
+} req_t;
+
+/* One fog node: ComputeBrokerApp3 members (ComputeBrokerApp3.h). */
+typedef struct {
+    int32_t MIPS;
+    double busyTime;       /* ComputeBrokerApp3.cc:46 */
+    int resourceStatus;    /* false = idle */
+    req_t currentTask;
+    int self_scheduled;    /* selfMsg->isScheduled() */
+    int self_kind;         /* selfMsg->getKind()     */
+    uint32_t self_gen;
+    req_t *q;              /* FIFO `requests` (push_back / erase(begin)) */
+    int64_t qh, qn, qcap;
+    int64_t pending;       /* assigned by the broker, advert of its completion not yet at broker */
+} node_t;
+
+typedef struct {
+    const orc_rep_in *in;
+    orc_rep_out *out;
+    heap_t fes;
+    uint64_t seq;
+    int64_t now;
+    /* broker: BrokerBaseApp3 `brokers` vector (Broker.cc:21-22) */
+    double *adv_busy;
+    int32_t *adv_mips;
+    node_t *nodes;
+    orc_rep_stats st;
+} sim_t;
+
+static void acc128(uint64_t *lo, uint64_t *hi, uint64_t v_lo, uint64_t v_hi) {
+    uint64_t o = *lo;
+    *lo += v_lo;
+    *hi += v_hi + (*lo < o);
+}
+
+static void acc_moment(uint64_t *sum_lo, uint64_t *sum_hi, uint64_t *sq_lo, uint64_t *sq_hi, int64_t v) {
+    /* v >= 0 for queue/response times */
+    unsigned __int128 sq = (unsigned __int128)(uint64_t)v * (uint64_t)v;
+    acc128(sum_lo, sum_hi, (uint64_t)v, 0);
+    acc128(sq_lo, sq_hi, (uint64_t)sq, (uint64_t)(sq >> 64));
+}
+
+static int schedule(sim_t *s, ev_t *e) {
+    e->seq = s->seq++;
+    return heap_push(&s->fes, e);
+}
+
+/* cSimpleModule::scheduleAt for a node's selfMsg. */
+static int node_schedule_self(sim_t *s, int32_t k, int64_t tick, int kind) {
+    node_t *nd = &s->nodes[k];
+    if (nd->self_scheduled) return ORC_ERR_STATE; /* "scheduleAt(): message already scheduled" */
+    nd->self_scheduled = 1;
+    nd->self_kind = kind;
+    ev_t e;
+    memset(&e, 0, sizeof e);
+    e.tick = tick;
+    e.type = EV_SELF;
+    e.node = k;
+    e.gen = nd->self_gen;
+    return schedule(s, &e);
+}
+
+/* cSimpleModule::cancelEvent(selfMsg): lazily invalidates the pending event. */
+static void node_cancel_self(sim_t *s, int32_t k) {
+    node_t *nd = &s->nodes[k];
+    if (nd->self_scheduled) {
+        nd->self_scheduled = 0;
+        nd->self_gen++;
+    }
+}
+
+/* ComputeBrokerApp3::advertiseMIPS, ComputeBrokerApp3.cc:205-222: the advert carries
+ * {MIPS, busyTime} and is delivered to the broker one uplink latency later. */
+static int node_advertise(sim_t *s, int32_t k, int64_t completed_task) {
+    node_t *nd = &s->nodes[k];
+    ev_t e;
+    memset(&e, 0, sizeof e);
+    e.tick = s->now + s->in->ul_tick[k];
+    e.type = EV_ADVERT;
+    e.node = k;
+    e.task = completed_task;
+    e.mips = nd->MIPS;
+    e.busy = nd->busyTime;
+    return schedule(s, &e);
+}
+
+/* ComputeBrokerApp3::releaseResource, ComputeBrokerApp3.cc:224-256. */
+static int node_release(sim_t *s, int32_t k) {
+    node_t *nd = &s->nodes[k];
+    int64_t t = nd->currentTask.task;
+    /* ack status 6 to the broker (:228-233) -- relay only, no decision effect */
+    nd->busyTime = nd->busyTime - nd->currentTask.required_time; /* :232 */
+    nd->resourceStatus = 0;                                      /* :234 */
+    if (s->out->done_tick) s->out->done_tick[t] = s->now;
+    {
+        int64_t resp = s->now - s->in->arrive_tick[t];
+        acc_moment(&s->st.resp_sum_lo, &s->st.resp_sum_hi, &s->st.resp_sq_lo, &s->st.resp_sq_hi, resp);
+        if (resp < s->st.resp_min_ticks) s->st.resp_min_ticks = resp;
+        if (resp > s->st.resp_max_ticks) s->st.resp_max_ticks = resp;
+        if (s->now > s->st.last_tick) s->st.last_tick = s->now;
+    }
+    if (nd->qn > 0) { /* :236-252 */
+        nd->resourceStatus = 1;
+        req_t *h = &nd->q[nd->qh];
+        /* emit(queueTimeSignal, (simTime() - queueStartTime) * 1000) (:238), kept in exact ticks */
+        int64_t qt = s->now - h->qstart_tick;
+        acc_moment(&s->st.queue_sum_lo, &s->st.queue_sum_hi, &s->st.queue_sq_lo, &s->st.queue_sq_hi, qt);
+        if (qt < s->st.queue_min_ticks) s->st.queue_min_ticks = qt;
+        if (qt > s->st.queue_max_ticks) s->st.queue_max_ticks = qt;
+        nd->currentTask = *h; /* :240-244 */
+        nd->qh = (nd->qh + 1) % nd->qcap; /* requests.erase(begin) (:246) */
+        nd->qn--;
+        if (s->out->start_tick) s->out->start_tick[nd->currentTask.task] = s->now;
+        node_cancel_self(s, k); /* :248-249 */
+        int64_t d = (int64_t)nd->currentTask.required_time * TICKS_PER_SECOND;
+        int rc = node_schedule_self(s, k, s->now + d, KIND_RELEASERESOURCE); /* :250 */
+        if (rc) return rc;
+    }
+    return node_advertise(s, k, t); /* :254 */
+}
+
+/* ComputeBrokerApp3::processPacket, FognetMsgTask branch, ComputeBrokerApp3.cc:269-320. */
+static int node_task(sim_t *s, int32_t k, int64_t t) {
+    node_t *nd = &s->nodes[k];
+    int32_t req = s->in->req_mips[t];
+    if (nd->MIPS == 0) return ORC_ERR_DIV0;
+    double tskTime = (double)(req / nd->MIPS); /* :276 int / int */
+    nd->busyTime = nd->busyTime + tskTime;     /* :279 */
+    if (nd->resourceStatus == 0) {             /* :282 */
+        nd->resourceStatus = 1;
+        if (s->out->status) s->out->status[t] = 5; /* "task assigned" (:285-289) */
+        nd->currentTask.task = t;
+        nd->currentTask.required_time = tskTime; /* :292-296 */
+        nd->currentTask.qstart_tick = s->now;
+        if (s->out->start_tick) s->out->start_tick[t] = s->now;
+        s->st.n_started++;
+        int64_t d = (int64_t)tskTime * TICKS_PER_SECOND;
+        return node_schedule_self(s, k, s->now + d, KIND_RELEASERESOURCE); /* :299-301, no cancelEvent */
+    }
+    /* busy: FIFO enqueue (:305-309), ack status 4 "task queued" (:310-313) */
+    if (nd->qn == nd->qcap) {
+        int64_t nc = nd->qcap ? nd->qcap * 2 : 16;
+        req_t *nq = (req_t *)malloc((size_t)nc * sizeof(req_t));
+        if (!nq) return ORC_ERR_OOM;
+        for (int64_t i = 0; i < nd->qn; i++) nq[i] = nd->q[(nd->qh + i) % nd->qcap];
+        free(nd->q);
+        nd->q = nq;
+        nd->qh = 0;
+        nd->qcap = nc;
+    }
+    req_t *r = &nd->q[(nd->qh + nd->qn) % nd->qcap];
+    r->task = t;
+    r->required_time = tskTime;
+    r->qstart_tick = s->now;
+    nd->qn++;
+    if (s->out->status) s->out->status[t] = 4;
+    s->st.n_queued++;
+    return ORC_OK;
+}
+
+int orc_decide_v3(int32_t n, const double *adv_busy, const int32_t *adv_mips, int32_t req, int32_t *out_node) {
+    /* BrokerBaseApp3::sendPubAck, status==false branch, BrokerBaseApp3.cc:265-281 */
+    if (n <= 0) return ORC_ERR_NO_NODES;    /* :268 dereferences brokers[0] first */
+    if (adv_mips[0] == 0) return ORC_ERR_DIV0; /* :268 int division by brokers[0]->getMips() */
+    int32_t currentGoodBroker = 0;             /* :267 */
+    double tskTime = (double)(req / adv_mips[0]); /* :268 (int/int, then to double) */
+    double tempp = adv_busy[0] + tskTime;         /* :270 */
+    if (n > 1) {                                  /* :271 */
+        for (int32_t j = 0; j < n; j++) {         /* :272 */
+            if (adv_busy[j] + (double)(req / adv_mips[0]) < tempp) { /* :273 strict '<' */
+                tempp = adv_busy[j] + (double)(req / adv_mips[0]);   /* :275 */
+                currentGoodBroker = j;                               /* :277 */
+            }
+        }
+    }
+    *out_node = currentGoodBroker;
+    return ORC_OK;
+}
+
+/* BrokerBaseApp3::handleMessageWhenUp, MqttMsgPublish branch (:138-158) + sendPubAck(false). */
+static int broker_publish(sim_t *s, int64_t t) {
+    /* QoS==1 in every trace publish; the status-4 pubAck to the user (:145-150) and the
+     * `delay` emit (:143) do not influence the decision. */
+    int32_t k;
+    int rc = orc_decide_v3(s->in->n_nodes, s->adv_busy, s->adv_mips, s->in->req_mips[t], &k);
+    if (rc) return rc;
+    if (s->out->node) s->out->node[t] = k;
+    s->st.n_tasks++;
+    node_t *nd = &s->nodes[k];
+    nd->pending++;
+    if (nd->pending > s->st.max_pending) s->st.max_pending = (int32_t)nd->pending;
+    /* socket.sendTo(tsk, brokers[k]) (:302): delivered one downlink latency later */
+    ev_t e;
+    memset(&e, 0, sizeof e);
+    e.tick = s->now + s->in->dl_tick[k];
+    e.type = EV_TASK;
+    e.node = k;
+    e.task = t;
+    return schedule(s, &e);
+}
+
+/* BrokerBaseApp3::handleMessageWhenUp, FognetMsgAdvertiseMIPS branch (:123-130). */
+static void broker_advert(sim_t *s, const ev_t *e) {
+    s->adv_mips[e->node] = e->mips;  /* setMips   (:127) */
+    s->adv_busy[e->node] = e->busy;  /* setBusyTime (:128) */
+}
+
+static int dispatch(sim_t *s, const ev_t *e) {
+    s->now = e->tick;
+    s->st.events++;
+    switch (e->type) {
+    case EV_PUBLISH:
+        return broker_publish(s, e->task);
+    case EV_ADVERT:
+        broker_advert(s, e);
+        if (e->task >= 0) s->nodes[e->node].pending--; /* completion adverts only */
+        return ORC_OK;
+    case EV_TASK:
+        return node_task(s, e->node, e->task);
+    case EV_SELF: {
+        node_t *nd = &s->nodes[e->node];
+        if (e->gen != nd->self_gen || !nd->self_scheduled) return ORC_OK; /* cancelled */
+        nd->self_scheduled = 0;
+        /* ComputeBrokerApp3::handleMessageWhenUp self-message switch (:65-90) */
+        if (nd->self_kind == KIND_ADVERTISEMIPS) {
+            /* initial advert: advertiseMIPS() with task = -1 marker */
+            ev_t a;
+            memset(&a, 0, sizeof a);
+            a.tick = s->now + s->in->ul_tick[e->node];
+            a.type = EV_ADVERT;
+            a.node = e->node;
+            a.task = -1;
+            a.mips = nd->MIPS;
+            a.busy = nd->busyTime;
+            return schedule(s, &a);
+        }
+        return node_release(s, e->node);
+    }
+    }
+    return ORC_ERR_ARG;
+}
+
+int orc_run_rep(const orc_rep_in *in, orc_rep_out *out) {
+    sim_t s;
+    memset(&s, 0, sizeof s);
+    s.in = in;
+    s.out = out;
+    int32_t N = in->n_nodes;
+    int64_t T = in->n_tasks;
+    s.st.queue_min_ticks = INT64_MAX;
+    s.st.resp_min_ticks = INT64_MAX;
+    s.st.queue_max_ticks = INT64_MIN;
+    s.st.resp_max_ticks = INT64_MIN;
+    s.st.last_tick = INT64_MIN;
+    int rc = ORC_OK;
+    if (out->node)
+        for (int64_t t = 0; t < T; t++) out->node[t] = -1;
+    if (N <= 0) {
+        rc = ORC_ERR_NO_NODES;
+        goto done;
+    }
+    s.adv_busy = (double *)calloc((size_t)N, sizeof(double));
+    s.adv_mips = (int32_t *)calloc((size_t)N, sizeof(int32_t));
+    s.nodes = (node_t *)calloc((size_t)N, sizeof(node_t));
+    if (!s.adv_busy || !s.adv_mips || !s.nodes) {
+        rc = ORC_ERR_OOM;
+        goto done;
+    }
+    for (int32_t k = 0; k < N; k++) s.nodes[k].MIPS = in->mips[k];
+
+    /* Pre-inserted events: each node's initial ADVERTISEMIPS self-message (sent one
+     * uplink latency before it reaches the broker), then every trace publish. */
+    for (int32_t k = 0; k < N; k++) {
+        rc = node_schedule_self(&s, k, in->init_adv_tick[k] - in->ul_tick[k], KIND_ADVERTISEMIPS);
+        if (rc) goto done;
+    }
+    int sorted = 1;
+    for (int64_t t = 1; t < T; t++)
+        if (in->arrive_tick[t] < in->arrive_tick[t - 1]) {
+            sorted = 0;
+            break;
+        }
+    if (sorted) {
+        /* Same FES order as inserting every publish up front: publish t carries
+         * sequence number N + t, below every dynamically scheduled event. */
+        uint64_t base = s.seq;
+        s.seq += (uint64_t)T;
+        int64_t next = 0;
+        while (next < T || s.fes.n > 0) {
+            int take_trace = 0;
+            if (next < T) {
+                if (s.fes.n == 0) take_trace = 1;
+                else {
+                    ev_t tr;
+                    tr.tick = in->arrive_tick[next];
+                    tr.seq = base + (uint64_t)next;
+                    take_trace = ev_less(&tr, &s.fes.a[0]);
+                }
+            }
+            ev_t e;
+            if (take_trace) {
+                memset(&e, 0, sizeof e);
+                e.tick = in->arrive_tick[next];
+                e.seq = base + (uint64_t)next;
+                e.type = EV_PUBLISH;
+                e.task = next++;
+            } else {
+                heap_pop(&s.fes, &e);
+            }
+            rc = dispatch(&s, &e);
+            if (rc) goto done;
+        }
+    } else {
+        for (int64_t t = 0; t < T; t++) {
+            ev_t e;
+            memset(&e, 0, sizeof e);
+            e.tick = in->arrive_tick[t];
+            e.type = EV_PUBLISH;
+            e.task = t;
+            rc = schedule(&s, &e);
+            if (rc) goto done;
+        }
+        while (s.fes.n > 0) {
+            ev_t e;
+            heap_pop(&s.fes, &e);
+            rc = dispatch(&s, &e);
+            if (rc) goto done;
+        }
+    }
+    if (out->final_view_busy)
+        for (int32_t k = 0; k < N; k++) out->final_view_busy[k] = s.adv_busy[k];
+done:
+    s.st.status = rc;
+    if (out->stats) *out->stats = s.st;
+    if (s.nodes)
+        for (int32_t k = 0; k < N; k++) free(s.nodes[k].q);
+    free(s.nodes);
+    free(s.adv_busy);
+    free(s.adv_mips);
+    free(s.fes.a);
+    return rc;
+}
+
+/* ---------------------------------------------------------------- batch driver */
+
+typedef struct {
+    int32_t R, N, node_stride;
+    int64_t T;
+    const int64_t *arrive_tick;
+    const int32_t *req_mips, *mips;
+    const int64_t *dl, *ul, *init_adv;
+    int32_t *node;
+    uint8_t *status;
+    int64_t *start_tick, *done_tick;
+    orc_rep_stats *stats;
+    int64_t next; /* work counter */
+    pthread_mutex_t mu;
+} batch_t;
+
+static void *batch_worker(void *arg) {
+    batch_t *b = (batch_t *)arg;
+    for (;;) {
+        pthread_mutex_lock(&b->mu);
+        int64_t r = b->next++;
+        pthread_mutex_unlock(&b->mu);
+        if (r >= b->R) break;
+        size_t to = (size_t)r * (size_t)b->T, no = (size_t)r * (size_t)b->node_stride;
+        orc_rep_in in = {b->N, b->T, b->arrive_tick + to, b->req_mips + to, b->mips + no,
+                         b->dl + no, b->ul + no, b->init_adv + no};
+        orc_rep_out out = {b->node ? b->node + to : 0, b->status ? b->status + to : 0,
+                           b->start_tick ? b->start_tick + to : 0, b->done_tick ? b->done_tick + to : 0,
+                           0, b->stats ? b->stats + r : 0};
+        orc_run_rep(&in, &out);
+    }
+    return 0;
+}
+
+int orc_run_batch(int32_t R, int64_t T, int32_t N, int32_t node_stride,
+                  const int64_t *arrive_tick, const int32_t *req_mips,
+                  const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                  int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                  orc_rep_stats *stats, int threads) {
+    batch_t b = {R, N, node_stride, T, arrive_tick, req_mips, mips, dl, ul, init_adv,
+                 node, status, start_tick, done_tick, stats, 0};
+    pthread_mutex_init(&b.mu, 0);
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    for (int i = 0; i < threads; i++) pthread_create(&th[i], 0, batch_worker, &b);
+    for (int i = 0; i < threads; i++) pthread_join(th[i], 0);
+    pthread_mutex_destroy(&b.mu);
+    return ORC_OK;
+}

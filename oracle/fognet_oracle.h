@@ -1,0 +1,84 @@
+/*
+ * fognet_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of FogNetSim++'s offload-decision hot path, written event by
+ * event after the reference handlers (BrokerBaseApp3 + ComputeBrokerApp3,
+ * OMNeT++ 4.6 sequential kernel semantics).  It is the parity checker for the
+ * HIP engine in fognetsimpp_amd/ and the `cpu_baseline` leg of bench.py.
+ * Nothing in the product path may link, load or call this code.
+ *
+ * Parity status: the reference cannot be built or run in this image (it needs
+ * OMNeT++ 4.6 + INET 3.3; stand-in headers are not allowed) and it ships no
+ * tests and no result files for the v3 modules.  This restatement is therefore
+ * pinned only by hand-traced known-answer vectors derived from the reference
+ * source (tests/golden/kat_*.json) — formally "parity unpinned" against an
+ * executable reference.  See DESIGN.md §Oracle.
+ */
+#ifndef FOGNET_ORACLE_H
+#define FOGNET_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes mirror include/fognet_hip.h */
+enum {
+    ORC_OK = 0,
+    ORC_ERR_ARG = 1,
+    ORC_ERR_NO_NODES = 2, /* BrokerBaseApp3.cc:268 reads brokers[0] before the size check (UB) */
+    ORC_ERR_DIV0 = 3,     /* BrokerBaseApp3.cc:268 / ComputeBrokerApp3.cc:276 int division by MIPS 0 (SIGFPE) */
+    ORC_ERR_STATE = 4,    /* ComputeBrokerApp3.cc:301 scheduleAt() on a pending selfMsg (cRuntimeError) */
+    ORC_ERR_OOM = 6
+};
+
+/* One replication: a pre-generated trace replayed through the broker/node handlers. */
+typedef struct {
+    int32_t n_nodes;
+    int64_t n_tasks;
+    const int64_t *arrive_tick;   /* [T] publish arrival tick at the broker            */
+    const int32_t *req_mips;      /* [T] MqttMsgPublish.MIPSRequired (int)             */
+    const int32_t *mips;          /* [N] ComputeBrokerApp3 par("MIPS") (int)           */
+    const int64_t *dl_tick;       /* [N] broker -> node delivery latency, ticks        */
+    const int64_t *ul_tick;       /* [N] node -> broker delivery latency, ticks        */
+    const int64_t *init_adv_tick; /* [N] arrival tick of node's first advertisement    */
+} orc_rep_in;
+
+typedef struct {
+    int64_t n_tasks, n_queued, n_started;
+    int64_t last_tick;
+    int64_t queue_min_ticks, queue_max_ticks, resp_min_ticks, resp_max_ticks;
+    /* exact 128-bit accumulators (two's complement halves) */
+    uint64_t queue_sum_lo, queue_sum_hi, queue_sq_lo, queue_sq_hi;
+    uint64_t resp_sum_lo, resp_sum_hi, resp_sq_lo, resp_sq_hi;
+    int64_t events;               /* FES events processed (diagnostic) */
+    int32_t max_pending;          /* max tasks assigned-but-not-advertised on one node */
+    int32_t status;
+} orc_rep_stats;
+
+typedef struct {
+    int32_t *node;       /* [T] chosen node index, -1 if never decided (nullable) */
+    uint8_t *status;     /* [T] 5 task assigned (idle) / 4 task queued            */
+    int64_t *start_tick; /* [T] service start tick                                */
+    int64_t *done_tick;  /* [T] RELEASERESOURCE tick                              */
+    double *final_view_busy; /* [N] broker view busyTime after the last event (nullable) */
+    orc_rep_stats *stats;
+} orc_rep_out;
+
+int orc_run_rep(const orc_rep_in *in, orc_rep_out *out);
+
+/* Scalar decision core, BrokerBaseApp3.cc:267-281. */
+int orc_decide_v3(int32_t n, const double *adv_busy, const int32_t *adv_mips, int32_t req, int32_t *out_node);
+
+/* Batch of R replications sharing T and N; node params have stride node_stride
+ * (0 = shared).  Runs on `threads` pthreads, one replication per thread at a time. */
+int orc_run_batch(int32_t R, int64_t T, int32_t N, int32_t node_stride,
+                  const int64_t *arrive_tick, const int32_t *req_mips,
+                  const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                  int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                  orc_rep_stats *stats, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,32 @@
+"""Loaders for the hand-traced fixtures in tests/golden/ (test infrastructure)."""
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _f(x):
+    return float(x) if not isinstance(x, str) else float(x.replace("inf", "inf"))
+
+
+def decide_cases():
+    d = json.load(open(os.path.join(GOLDEN, "kat_decide.json")))
+    out = []
+    for c in d["cases"]:
+        busy = np.array([_f(x) for x in c["busy"]], dtype=np.float64)
+        mips = np.array(c["mips"], dtype=np.int32)
+        out.append((c["name"], busy, mips, int(c["req"]), c.get("node"), c.get("error")))
+    return out
+
+
+def replay_cases():
+    d = json.load(open(os.path.join(GOLDEN, "kat_replay.json")))
+    out = []
+    for c in d["cases"]:
+        tr = dict(arrive=np.array(c["arrive"], np.int64), req=np.array(c["req"], np.int32),
+                  mips=np.array(c["mips"], np.int32), dl=np.array(c["dl"], np.int64),
+                  ul=np.array(c["ul"], np.int64), init=np.array(c["init"], np.int64))
+        out.append((c["name"], tr, c["expect"]))
+    return out

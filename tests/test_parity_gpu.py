@@ -1,0 +1,282 @@
+"""Parity of the gfx950 engine (through the C ABI) with the CPU restatement and
+the hand-traced known answers.  Integer/index outputs must be bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+import fognetsimpp_amd as fa
+import golden_io
+import oracle_lib as ol
+import tracegen as tg
+from fognetsimpp_amd import _abi
+from test_oracle import c1_trace, check_fifo_invariants
+
+pytestmark = pytest.mark.gpu
+TPS = 10**12
+
+
+def run_gpu(ctx, tr, ring_capacity=0):
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(tr, dev)
+    out = fa.run_batch(ctx, d, ring_capacity=ring_capacity)
+    torch.cuda.synchronize()
+    return dict(node=out.node.cpu().numpy(), status=out.status.cpu().numpy(),
+                start=out.start_tick.cpu().numpy(), done=out.done_tick.cpu().numpy(),
+                stats=out.rep_stats(), raw=out)
+
+
+def assert_parity(tr, g, o):
+    st_g, st_o = g["stats"], o["stats"]
+    np.testing.assert_array_equal(st_g["status"], st_o["status"])
+    for k in ("node", "status", "start", "done"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+    for f in ("n_tasks", "n_queued", "n_started", "last_tick", "queue_min_ticks", "queue_max_ticks",
+              "resp_min_ticks", "resp_max_ticks", "queue_sum_lo", "queue_sum_hi", "queue_sq_lo", "queue_sq_hi",
+              "resp_sum_lo", "resp_sum_hi", "resp_sq_lo", "resp_sq_hi", "events", "max_pending"):
+        np.testing.assert_array_equal(st_g[f], st_o[f], err_msg=f)
+
+
+# ------------------------------------------------------------------ decision core
+
+@pytest.mark.parametrize("case", golden_io.decide_cases(), ids=lambda c: c[0])
+def test_sendPubAck_known_answers(ctx, case):
+    name, busy, mips, req, node, err = case
+    broker = fa.BrokerBaseApp3(ctx)
+    if err is not None:
+        with pytest.raises(fa.FognetError) as e:
+            broker.sendPubAck(busy, mips, req)
+        assert e.value.code == err
+    else:
+        assert broker.sendPubAck(busy, mips, req) == node
+
+
+def test_decide_batch_matches_oracle(ctx):
+    rng = np.random.default_rng(5)
+    for n in (1, 3, 64, 65, 256, 1000):
+        m = 2000
+        busy = rng.integers(0, 6, size=(m, n)).astype(np.float64) + rng.choice([0.0, 0.5, 1e-16], size=(m, n))
+        busy[rng.random((m, n)) < 0.01] = np.nan
+        mips = rng.integers(1, 3000, size=(m, n)).astype(np.int32)
+        mips[rng.random(m) < 0.05, 0] = 0
+        req = rng.integers(-5000, 70000, size=m).astype(np.int32)
+        dev = torch.device("cuda", ctx.device)
+        node, status = fa.BrokerBaseApp3(ctx).sendPubAck_batch(
+            torch.from_numpy(busy).to(dev), torch.from_numpy(mips).to(dev), torch.from_numpy(req).to(dev))
+        node, status = node.cpu().numpy(), status.cpu().numpy()
+        for q in range(m):
+            rc, k = ol.decide_v3(busy[q], mips[q], int(req[q]))
+            assert status[q] == rc, (n, q)
+            if rc == 0:
+                assert node[q] == k, (n, q)
+
+
+# ------------------------------------------------------------------ replay engine
+
+@pytest.mark.parametrize("case", golden_io.replay_cases(), ids=lambda c: c[0])
+def test_replay_known_answers(ctx, case):
+    name, tr, exp = case
+    g = run_gpu(ctx, tr)
+    assert g["stats"]["status"][0] == 0
+    np.testing.assert_array_equal(g["node"][0], exp["node"])
+    np.testing.assert_array_equal(g["status"][0], exp["status"])
+    np.testing.assert_array_equal(g["start"][0], exp["start"])
+    np.testing.assert_array_equal(g["done"][0], exp["done"])
+    assert g["stats"]["n_queued"][0] == exp["n_queued"]
+    assert g["stats"]["n_started"][0] == exp["n_started"]
+
+
+def test_c1_example_run(ctx):
+    tr = c1_trace()
+    g = run_gpu(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"])
+    assert_parity(tr, g, o)
+    assert (g["node"] == 0).all()
+
+
+def test_c2_trace_replay_bit_exact(ctx):
+    """Config C2: 1 replication x 10,000 tasks x 64 nodes (BASELINE.json configs[1])."""
+    tr = tg.make_batch(0x5EED0001, 1, 64, 10000)
+    g = run_gpu(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"])
+    assert_parity(tr, g, o)
+
+
+@pytest.mark.parametrize("N", [1, 5, 63, 64, 100, 128, 200, 256])
+def test_node_counts(ctx, N):
+    tr = tg.make_batch(1000 + N, 3, N, 1500, rho=0.9)
+    g = run_gpu(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=3)
+    assert_parity(tr, g, o)
+
+
+def test_policy_sweep_sample(ctx):
+    """C3 recipe (rho x latency-scale sweep) at reduced T for the oracle."""
+    tr = tg.make_batch(0x5EED0003, 18, 256, 4000, sweep=True)
+    g = run_gpu(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8)
+    assert_parity(tr, g, o)
+
+
+def tie_heavy(seed, R, N, T):
+    """Coarse ticks so arrivals, completions and adverts collide: latencies and
+    gaps are small multiples of a base, service times often 0, and some
+    downlinks are >= whole seconds so the arrival-first rule is exercised."""
+    rng = np.random.default_rng(seed)
+    base = 10**11
+    mips = rng.choice([1000, 2000, 500], size=(R, N)).astype(np.int32)
+    dl = rng.choice([0, base, 2 * base, 10 * base, 20 * base, 30 * base], size=(R, N)).astype(np.int64)
+    ul = rng.choice([0, base, 3 * base], size=(R, N)).astype(np.int64)
+    init = ul + rng.integers(0, 3, size=(R, N)) * base
+    start = init.max(axis=1, keepdims=True) + base
+    gaps = rng.choice([0, 0, base, 5 * base, 10 * base], size=(R, T)).astype(np.int64)
+    arrive = start + np.cumsum(gaps, axis=1)
+    req = rng.choice([0, 400, 999, 1000, 1500, 2000, 3000], size=(R, T)).astype(np.int32)
+    return dict(arrive=arrive, req=req, mips=mips, dl=dl, ul=ul, init=init)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_tie_heavy(ctx, seed):
+    tr = tie_heavy(seed, 8, 1 + 37 * seed, 2000)
+    g = run_gpu(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8)
+    assert_parity(tr, g, o)
+
+
+def test_shared_node_params_and_empty_trace(ctx):
+    tr = tg.make_replication(3, 0, 32, 700)
+    batch = dict(arrive=np.stack([tr["arrive"]] * 2), req=np.stack([tr["req"], tr["req"][::-1].copy()]),
+                 mips=tr["mips"], dl=tr["dl"], ul=tr["ul"], init=tr["init"])
+    g = run_gpu(ctx, batch)
+    o = ol.run_batch(batch["arrive"], batch["req"], batch["mips"], batch["dl"], batch["ul"], batch["init"])
+    assert_parity(batch, g, o)
+    empty = dict(batch, arrive=np.zeros((2, 0), np.int64), req=np.zeros((2, 0), np.int32))
+    g = run_gpu(ctx, empty)
+    assert (g["stats"]["status"] == 0).all() and (g["stats"]["n_tasks"] == 0).all()
+
+
+def test_ring_capacity_exceeded(ctx):
+    tr = tg.make_batch(11, 1, 4, 2000, rho=3.0)  # overload: queues grow without bound
+    g = run_gpu(ctx, tr, ring_capacity=16)
+    assert g["stats"]["status"][0] == _abi.FOGNET_ERR_CAPACITY
+    g = run_gpu(ctx, tr, ring_capacity=4096)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"])
+    assert_parity(tr, g, o)
+
+
+@pytest.mark.parametrize("bad", ["unsorted", "neg_req", "mips0", "late_advert", "early_advert_send", "huge_service"])
+def test_precondition_errors(ctx, bad):
+    tr = tg.make_batch(5, 2, 16, 300)
+    tr = {k: v.copy() for k, v in tr.items()}
+    if bad == "unsorted":
+        tr["arrive"][1, 100] = tr["arrive"][1, 99] - 1
+    elif bad == "neg_req":
+        tr["req"][1, 5] = -1
+    elif bad == "mips0":
+        tr["mips"][1, 3] = 0
+    elif bad == "late_advert":
+        tr["init"][1, 7] = tr["arrive"][1, 0]
+    elif bad == "early_advert_send":
+        tr["init"][1, 7] = tr["ul"][1, 7] - 1
+    elif bad == "huge_service":
+        tr["mips"][1, :] = 1
+        tr["req"][1, :] = 2**31 - 1
+    g = run_gpu(ctx, tr)
+    assert g["stats"]["status"][0] == 0
+    assert g["stats"]["status"][1] == _abi.FOGNET_ERR_ARG
+
+
+def test_unsupported_sizes(ctx):
+    tr = tg.make_batch(5, 1, 257, 10)
+    with pytest.raises(fa.FognetError) as e:
+        run_gpu(ctx, tr)
+    assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED
+
+
+# ------------------------------------------------------------------ generator + stats
+
+def test_device_tracegen_matches_host_recipe(ctx):
+    R, T, N = 12, 3000, 256
+    mg, sc = fa.sweep_params(np.arange(R), N)
+    d = fa.generate_trace(ctx, 0x5EED0003, R, T, N, mg, sc)
+    torch.cuda.synchronize()
+    for r in range(R):
+        h = tg.make_replication(0x5EED0003, r, N, T, rho=(0.5, 0.8, 0.95)[r % 3], lat_scale=int(sc[r]),
+                                mean_gap_ticks=float(mg[r]))
+        for k in ("arrive", "req", "mips", "dl", "ul", "init"):
+            np.testing.assert_array_equal(d[k][r].cpu().numpy(), h[k], err_msg=f"{k} r={r}")
+
+
+def test_device_tracegen_sharding_offset(ctx):
+    N, T = 64, 500
+    mg, sc = fa.sweep_params(np.arange(8), N)
+    full = fa.generate_trace(ctx, 9, 8, T, N, mg, sc)
+    part = fa.generate_trace(ctx, 9, 3, T, N, mg[5:], sc[5:], r0=5)
+    torch.cuda.synchronize()
+    for k in ("arrive", "req", "dl"):
+        assert torch.equal(full[k][5:], part[k])
+
+
+def job_from_reps(st):
+    """Exact host reduction of rep stats (test-side), for comparison with the device."""
+    ok = st[st["status"] == 0]
+    def u128(lo, hi):
+        return sum(int(a) | (int(b) << 64) for a, b in zip(lo, hi))
+    return dict(n_reps=len(st), n_failed=int((st["status"] != 0).sum()), n_tasks=int(ok["n_tasks"].sum()),
+                n_queued=int(ok["n_queued"].sum()), queue_sum=u128(ok["queue_sum_lo"], ok["queue_sum_hi"]),
+                queue_sq=u128(ok["queue_sq_lo"], ok["queue_sq_hi"]), resp_sq=u128(ok["resp_sq_lo"], ok["resp_sq_hi"]),
+                resp_max=int(ok["resp_max_ticks"].max()), max_pending=int(ok["max_pending"].max()))
+
+
+def test_reduce_stats_exact(ctx):
+    tr = tg.make_batch(21, 20, 64, 2000, sweep=True)
+    tr["mips"][3, 0] = 0  # one failed replication
+    g = run_gpu(ctx, tr)
+    job = fa.reduce_stats(ctx, g["raw"].stats, 20)
+    ref = job_from_reps(g["stats"])
+    u192 = lambda a: int(a[0]) | (int(a[1]) << 64) | (int(a[2]) << 128)
+    assert int(job["n_reps"]) == 20 and int(job["n_failed"]) == 1 == ref["n_failed"]
+    assert int(job["n_tasks"]) == ref["n_tasks"] and int(job["n_queued"]) == ref["n_queued"]
+    assert u192(job["queue_sum"]) == ref["queue_sum"] and u192(job["queue_sq"]) == ref["queue_sq"]
+    assert u192(job["resp_sq"]) == ref["resp_sq"]
+    assert int(job["resp_max_ticks"]) == ref["resp_max"] and int(job["max_pending"]) == ref["max_pending"]
+    halves = [fa.reduce_stats(ctx, g["raw"].stats[: 7 * _abi.REP_STATS_DTYPE.itemsize], 7),
+              fa.reduce_stats(ctx, g["raw"].stats[7 * _abi.REP_STATS_DTYPE.itemsize:], 13)]
+    assert fa.merge_job_stats(halves).tobytes() == job.tobytes()
+
+
+def test_full_size_sweep_properties(ctx):
+    """C3 shape at reduced R: R=256 x T=100k x N=256, checked through
+    size-independent properties on the device (FIFO recurrence per node,
+    service times, statuses) plus one replication against the oracle."""
+    R, T, N = 256, 100_000, 256
+    dev = torch.device("cuda", ctx.device)
+    mg, sc = fa.sweep_params(np.arange(R), N)
+    d = fa.generate_trace(ctx, 0x5EED0003, R, T, N, mg, sc)
+    out = fa.run_batch(ctx, d)
+    torch.cuda.synchronize()
+    st = out.rep_stats()
+    assert (st["status"] == 0).all() and (st["n_tasks"] == T).all()
+    node = out.node.long()
+    mips = torch.gather(d["mips"].long(), 1, node)
+    dl = torch.gather(d["dl"], 1, node)
+    S = d["req"].long() // mips
+    a = d["arrive"] + dl
+    assert torch.equal(out.done_tick - out.start_tick, S * TPS)
+    assert bool((out.start_tick >= a).all())
+    assert bool(((out.status == 5) <= (out.start_tick == a)).all())
+    # per node FIFO: start = max(a, previous done on the same node)
+    key = node * T + torch.arange(T, device=dev).unsqueeze(0)
+    order = torch.argsort(key, dim=1)
+    n_s, a_s = torch.gather(node, 1, order), torch.gather(a, 1, order)
+    s_s, d_s = torch.gather(out.start_tick, 1, order), torch.gather(out.done_tick, 1, order)
+    prev = torch.cat([torch.full((R, 1), -2**62, device=dev, dtype=torch.int64), d_s[:, :-1]], 1)
+    same = torch.cat([torch.zeros((R, 1), device=dev, dtype=torch.bool), n_s[:, 1:] == n_s[:, :-1]], 1)
+    prev = torch.where(same, prev, torch.full_like(prev, -2**62))
+    assert torch.equal(s_s, torch.maximum(a_s, prev))
+    # one full replication bit-exact against the oracle
+    r = 1
+    h = {k: d[k][r].cpu().numpy() for k in ("arrive", "req", "mips", "dl", "ul", "init")}
+    o = ol.run_batch(h["arrive"], h["req"], h["mips"], h["dl"], h["ul"], h["init"])
+    np.testing.assert_array_equal(out.node[r].cpu().numpy(), o["node"][0])
+    np.testing.assert_array_equal(out.done_tick[r].cpu().numpy(), o["done"][0])
+    assert st[r].tobytes() == o["stats"][0].tobytes()
