@@ -64,7 +64,7 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   if (in->node_stride != 0 && in->node_stride != in->N)
     return fail(c, FOGNET_ERR_ARG, "node_stride must be 0 or N");
   int q = in->ring_capacity ? in->ring_capacity : 1024;
-  if (q < 2 || (q & (q - 1)) != 0 || q > (1 << 20)) return fail(c, FOGNET_ERR_ARG, "ring_capacity must be a power of two in [2, 2^20]");
+  if (q < 2 || (q & (q - 1)) != 0 || q > (1 << 15)) return fail(c, FOGNET_ERR_ARG, "ring_capacity must be a power of two in [2, 2^15]");
   int qlog = 0;
   while ((1 << qlog) < q) ++qlog;
   if (in->R > 0 && in->T > 0 && (!in->arrive_tick || !in->req_mips))

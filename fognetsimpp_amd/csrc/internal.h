@@ -9,6 +9,8 @@
 
 namespace fognet {
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 constexpr int kWave = 64;
 constexpr int64_t kTicksPerSecond = FOGNET_TICKS_PER_SECOND;
 constexpr int kMaxNodesPerLane = 4;  // N <= 256 in the register-resident replay kernel

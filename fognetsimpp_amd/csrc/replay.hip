@@ -34,16 +34,26 @@ struct Slot {
   int64_t nxt;       // tick at which the head's completion advert reaches the broker
   int64_t hd_done;   // head (oldest pending) task: completion tick
   uint32_t hd_C, hd_S;
-  int64_t nh_a;      // entry head+1 (cached; valid when >= 2 tasks pending)
-  uint32_t nh_C, nh_S;
+  u32x4 nh;          // entry head+1 as loaded {a lo, a hi, C, S} (valid when >= 2 pending)
   int64_t tl_a;      // tail (newest) task
   int64_t tl_done;
   uint32_t tl_C, tl_S;
-  uint32_t n_push;   // tasks ever assigned to this node
-  uint32_t n_head;   // completion adverts applied
+  uint32_t cnt;      // ring counters mod 2^16: tasks ever assigned (bits 0-15),
+                     // completion adverts applied (bits 16-31); capacity <= 2^15
 };
 
+__device__ __forceinline__ uint32_t n_push(const Slot& st) { return st.cnt & 0xFFFFu; }
+__device__ __forceinline__ uint32_t n_head(const Slot& st) { return st.cnt >> 16; }
+__device__ __forceinline__ uint32_t pending(const Slot& st) { return (n_push(st) - n_head(st)) & 0xFFFFu; }
+
 constexpr uint64_t kNoKey = ~0ull;
+
+__device__ __forceinline__ int64_t nh_a(u32x4 v) { return (int64_t)(((uint64_t)v.y << 32) | v.x); }
+
+// one dwordx4 load of a ring entry, kept as a single 4-register value
+__device__ __forceinline__ u32x4 load_entry(const RingEntry* ring, uint32_t i) {
+  return *reinterpret_cast<const u32x4*>(ring + i);
+}
 constexpr int64_t kNever = INT64_MAX;
 
 // arrival at tick `a` happens before the completion at `done` of a task with
@@ -58,7 +68,7 @@ __device__ __forceinline__ void apply_advert(Slot& st, int k, int64_t dl, int64_
   // Cumulative service of the tasks that reached the node before the head's
   // completion: scan back from the newest assignment.
   uint32_t c_arrived = st.hd_C;  // the head itself always arrived before it completed
-  const uint32_t pend0 = st.n_push - st.n_head;  // >= 1 whenever an advert is due
+  const uint32_t pend0 = pending(st);  // >= 1 whenever an advert is due
   if (arrives_before(st.tl_a, st.hd_done, dl, st.hd_S)) {
     c_arrived = st.tl_C;
   } else {
@@ -67,10 +77,10 @@ __device__ __forceinline__ void apply_advert(Slot& st, int k, int64_t dl, int64_
       int64_t a;
       uint32_t C;
       if (d == 1u) {
-        a = st.nh_a;
-        C = st.nh_C;
+        a = nh_a(st.nh);
+        C = st.nh.z;
       } else {
-        const RingEntry e = ring[(st.n_head + d) & qmask];
+        const RingEntry e = ring[(n_head(st) + d) & qmask];
         a = e.a;
         C = e.C;
       }
@@ -84,52 +94,50 @@ __device__ __forceinline__ void apply_advert(Slot& st, int k, int64_t dl, int64_
   st.vkey = ((uint64_t)busy << 16) | (uint32_t)k;
 
   // advance the head
-  st.n_head += 1u;
-  const uint32_t pend = st.n_push - st.n_head;
+  st.cnt += 0x10000u;
+  const uint32_t pend = pending(st);
   if (pend == 0u) {
     st.nxt = kNever;
     return;
   }
-  const int64_t start = st.nh_a > st.hd_done ? st.nh_a : st.hd_done;
-  st.hd_done = start + (int64_t)st.nh_S * kTicksPerSecond;
-  st.hd_C = st.nh_C;
-  st.hd_S = st.nh_S;
+  const int64_t na = nh_a(st.nh);
+  const int64_t start = na > st.hd_done ? na : st.hd_done;
+  st.hd_done = start + (int64_t)st.nh.w * kTicksPerSecond;
+  st.hd_C = st.nh.z;
+  st.hd_S = st.nh.w;
   st.nxt = st.hd_done + ul;
-  if (pend >= 2u) {
-    if (pend == 2u) {  // head+1 is the tail
-      st.nh_a = st.tl_a;
-      st.nh_C = st.tl_C;
-      st.nh_S = st.tl_S;
-    } else {  // prefetch; first use is at this node's next advert
-      const RingEntry e = ring[(st.n_head + 1u) & qmask];
-      st.nh_a = e.a;
-      st.nh_C = e.C;
-      st.nh_S = e.S;
-    }
-  }
+  // st.nh (entry head+1) is refreshed by the caller with a load issued by
+  // every lane in uniform control flow (refresh_nh).
 }
 
-struct PushOut {
-  uint32_t ns;  // node | status << 16
-  int64_t start, done;
-  uint32_t pend;
-  uint32_t err;
-};
+// Refresh the head+1 cache of every lane's node in one slot.  The ring holds
+// every pending entry (the tail included), and a lane whose head did not move
+// simply reloads the same entry; with fewer than two entries pending the
+// value is unused.  Issued by all lanes outside any divergent branch, the
+// load targets the loop-carried registers directly, so it is waited for at
+// the node's next advert instead of here (a load inside a divergent branch
+// would be copied into them at the merge, forcing an immediate vmcnt wait).
+__device__ __forceinline__ void refresh_nh(Slot& st, const RingEntry* ring, uint32_t qmask) {
+  st.nh = load_entry(ring, (n_head(st) + 1u) & qmask);
+}
 
-// Assign a publish decided at tick t with requirement rq to node k (lane-local).
-__device__ __forceinline__ PushOut push_task(Slot& st, int k, int64_t t, int32_t rq, int64_t dl,
-                                             int64_t ul, int32_t mips, RingEntry* ring,
-                                             uint32_t qmask, uint32_t max_s) {
-  PushOut o;
+// Assign publish o_idx, decided at tick t with requirement rq, to node k
+// (lane-local).  Returns (fognet_status << 24) | tasks pending on k after the push.
+__device__ __forceinline__ uint32_t push_task(Slot& st, int k, int64_t t, int32_t rq, int64_t dl, int64_t ul,
+                                              int32_t mips, RingEntry* ring, uint32_t qmask,
+                                              const ReplayArgs& A, size_t o_idx) {
+  const uint32_t max_s = A.max_s;
+  struct {
+    uint32_t err;
+  } o;
   o.err = FOGNET_OK;
   const uint32_t S = (uint32_t)rq / (uint32_t)mips;  // double tskTime = requiredMIPS / MIPS (:276)
   const int64_t dur = (int64_t)S * kTicksPerSecond;
   if (S > max_s || t > kNever - dl) o.err = FOGNET_ERR_ARG;
   const int64_t a = t + dl;
-  const bool has = st.n_push != 0u;
   uint32_t status;
   int64_t start;
-  if (!has || st.tl_done < a) {
+  if (st.tl_done < a) {  // tl_done starts at INT64_MIN: first task of the node
     status = 5u;  // idle: "task assigned" (:282-301)
     start = a;
   } else if (st.tl_done > a) {
@@ -142,7 +150,7 @@ __device__ __forceinline__ PushOut push_task(Slot& st, int k, int64_t t, int32_t
   if (start > kNever - dur) o.err = FOGNET_ERR_ARG;
   const int64_t done = start + dur;
   if (done > kNever - ul) o.err = FOGNET_ERR_ARG;
-  const uint32_t pend = st.n_push - st.n_head;
+  const uint32_t pend = pending(st);
   if (pend > qmask) o.err = FOGNET_ERR_CAPACITY;
   const uint32_t C = st.tl_C + S;
   if (o.err == FOGNET_OK) {
@@ -150,28 +158,28 @@ __device__ __forceinline__ PushOut push_task(Slot& st, int k, int64_t t, int32_t
     e.a = a;
     e.C = C;
     e.S = S;
-    ring[st.n_push & qmask] = e;
+    ring[n_push(st) & qmask] = e;
     if (pend == 0u) {
       st.hd_done = done;
       st.hd_C = C;
       st.hd_S = S;
       st.nxt = done + ul;
-    } else if (pend == 1u) {
-      st.nh_a = a;
-      st.nh_C = C;
-      st.nh_S = S;
     }
+    // pend == 1: the new entry is head+1; the caller's refresh_nh reads it
+    // back (same lane, same address: the load observes the store)
     st.tl_a = a;
     st.tl_C = C;
     st.tl_S = S;
     st.tl_done = done;
-    st.n_push += 1u;
+    st.cnt = (st.cnt & 0xFFFF0000u) | ((st.cnt + 1u) & 0xFFFFu);
+    // per-task outputs, stored by the owner lane (consecutive tasks write
+    // consecutive addresses; the partial lines merge in L2)
+    A.out_node[o_idx] = k;
+    A.out_status[o_idx] = (uint8_t)status;
+    A.out_start[o_idx] = start;
+    A.out_done[o_idx] = done;
   }
-  o.ns = (uint32_t)k | (status << 16);
-  o.start = start;
-  o.done = done;
-  o.pend = pend + 1u;
-  return o;
+  return (o.err << 24) | (pend + 1u);
 }
 
 template <int NPL>
@@ -183,7 +191,9 @@ __device__ __forceinline__ uint64_t view_min(const Slot (&st)[NPL]) {
 }
 
 template <int NPL>
-__global__ __launch_bounds__(64) void replay_kernel(ReplayArgs A) {
+// 4 waves per SIMD (<= 128 VGPRs): 16 replications resident per CU, so the
+// 4096-replication sweep runs in a single wave of workgroups on 256 CUs.
+__global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
   __shared__ int64_t s_dl[NPL * kWave];
@@ -220,15 +230,12 @@ __global__ __launch_bounds__(64) void replay_kernel(ReplayArgs A) {
     st[s].hd_done = 0;
     st[s].hd_C = 0u;
     st[s].hd_S = 0u;
-    st[s].nh_a = 0;
-    st[s].nh_C = 0u;
-    st[s].nh_S = 0u;
+    st[s].nh = u32x4{0u, 0u, 0u, 0u};
     st[s].tl_a = 0;
-    st[s].tl_done = 0;
+    st[s].tl_done = INT64_MIN;
     st[s].tl_C = 0u;
     st[s].tl_S = 0u;
-    st[s].n_push = 0u;
-    st[s].n_head = 0u;
+    st[s].cnt = 0u;
   }
   __syncthreads();
 
@@ -236,6 +243,13 @@ __global__ __launch_bounds__(64) void replay_kernel(ReplayArgs A) {
   if (N <= 0) err = FOGNET_ERR_NO_NODES;
 
   RingEntry* const ring_r = A.ring + (size_t)r * (size_t)N * ((size_t)qmask + 1u);
+  // ring of this lane's node in slot s (lanes past N alias node 0: in bounds,
+  // never used); recomputed at each use rather than held in 2 VGPRs per slot
+  const int q_log2 = A.q_log2;
+  auto ring_s = [&](int s) -> RingEntry* {
+    const int k = s * kWave + lane;
+    return ring_r + ((size_t)(k < N ? k : 0) << q_log2);
+  };
   uint64_t best = view_min<NPL>(st);
   bool dirty = false;
   int64_t prev_t = INT64_MIN;
@@ -257,8 +271,6 @@ __global__ __launch_bounds__(64) void replay_kernel(ReplayArgs A) {
     }
     prev_t = readlane_i64(ca, cnt - 1);
 
-    uint32_t o_ns = 0u;
-    int64_t o_start = 0, o_done = 0;
     int j = 0;
     for (; j < cnt; ++j) {
       const int64_t t = readlane_i64(ca, j);
@@ -273,8 +285,9 @@ __global__ __launch_bounds__(64) void replay_kernel(ReplayArgs A) {
           dirty = true;
           if (due) {
             const int k = s * kWave + lane;
-            apply_advert(st[s], k, s_dl[k], s_ul[k], ring_r + (size_t)k * (qmask + 1u), qmask);
+            apply_advert(st[s], k, s_dl[k], s_ul[k], ring_s(s), qmask);
           }
+          refresh_nh(st[s], ring_s(s), qmask);
         }
       }
       // 2) argmin over the advertised view (ties -> lowest index)
@@ -285,42 +298,26 @@ __global__ __launch_bounds__(64) void replay_kernel(ReplayArgs A) {
       const int k = (int)(best & 0xFFFFull);
       const int ks = k / kWave, kl = k % kWave;
       // 3) the chosen node receives the task
-      PushOut po;
-      po.ns = 0u;
-      po.start = po.done = 0;
-      po.pend = 0u;
-      po.err = 0u;
+      uint32_t po = 0u;
 #pragma unroll
       for (int s = 0; s < NPL; ++s) {
-        if (s == ks && lane == kl) {
-          po = push_task(st[s], k, t, rq, s_dl[k], s_ul[k], s_mips[k],
-                         ring_r + (size_t)k * (qmask + 1u), qmask, A.max_s);
+        if (s == ks) {  // wave-uniform
+          if (lane == kl) {
+            po = push_task(st[s], k, t, rq, s_dl[k], s_ul[k], s_mips[k], ring_s(s), qmask, A,
+                           tbase + c0 + j);
+          }
+          refresh_nh(st[s], ring_s(s), qmask);
         }
       }
-      const uint32_t perr = readlane_u32(po.err, kl);
-      if (perr != 0u) {
-        err = perr;
+      const uint32_t pr = readlane_u32(po, kl);
+      if ((pr >> 24) != 0u) {
+        err = pr >> 24;
         break;
       }
-      const uint32_t ns = readlane_u32(po.ns, kl);
-      const int64_t pstart = readlane_i64(po.start, kl);
-      const int64_t pdone = readlane_i64(po.done, kl);
-      const uint32_t pend = readlane_u32(po.pend, kl);
+      const uint32_t pend = pr & 0xFFFFFFu;
       max_pend = pend > max_pend ? pend : max_pend;
-      if (lane == j) {
-        o_ns = ns;
-        o_start = pstart;
-        o_done = pdone;
-      }
     }
     n_done += j;
-    if (lane < j) {
-      const size_t o = tbase + c0 + lane;
-      if (A.out_node) A.out_node[o] = (int32_t)(o_ns & 0xFFFFu);
-      if (A.out_status) A.out_status[o] = (uint8_t)(o_ns >> 16);
-      if (A.out_start) A.out_start[o] = o_start;
-      if (A.out_done) A.out_done[o] = o_done;
-    }
   }
 
   if (lane == 0 && A.out_stats) {

@@ -106,11 +106,12 @@ typedef struct fognet_batch_in {
 } fognet_batch_in;
 
 typedef struct fognet_batch_out {
-    int32_t *node;            /* [R][T] chosen node, nullable (stats-only run)                    */
-    uint8_t *status;          /* [R][T] 5 = started on arrival, 4 = queued; nullable              */
-    int64_t *start_tick;      /* [R][T] service start; nullable                                   */
-    int64_t *done_tick;       /* [R][T] completion (RELEASERESOURCE) tick; nullable               */
-    fognet_rep_stats *stats;  /* [R]; nullable                                                    */
+    int32_t *node;            /* [R][T] chosen node                                               */
+    uint8_t *status;          /* [R][T] 5 = started on arrival, 4 = queued                        */
+    int64_t *start_tick;      /* [R][T] service start                                             */
+    int64_t *done_tick;       /* [R][T] completion (RELEASERESOURCE) tick                         */
+    fognet_rep_stats *stats;  /* [R] (all five arrays are required; a stats-only mode that skips
+                                 the per-task arrays is not implemented yet: ERR_UNSUPPORTED)    */
 } fognet_batch_out;
 
 /* Synthetic trace recipe, generated on the device.
