@@ -1,0 +1,47 @@
+"""Multi-GPU plumbing for the replay engine.
+
+Replications are independent, so a job is sharded by contiguous blocks of
+the global replication index; each rank generates and replays its own block
+(trace keys depend on the global index only, so results do not depend on the
+number of GPUs).  The only collective is one all-gather of the per-rank
+``fognet_job_stats`` record, merged with exact integer arithmetic
+(``fognet_job_stats_merge``), so the job statistics are bit-identical for any
+sharding.  Works with the ``nccl`` (RCCL) backend on device tensors and with
+``gloo`` on CPU tensors.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _abi
+from .engine import merge_job_stats
+
+
+def shard(r_total: int, world: int, rank: int) -> tuple[int, int]:
+    """(first global replication, count) of ``rank``'s contiguous block;
+    the first ``r_total % world`` ranks take one extra replication."""
+    if world <= 0 or not 0 <= rank < world or r_total < 0:
+        raise ValueError("bad shard request")
+    q, rem = divmod(r_total, world)
+    r0 = rank * q + min(rank, rem)
+    return r0, q + (1 if rank < rem else 0)
+
+
+def job_record_tensor(job, device) -> torch.Tensor:
+    """A job record (JOB_STATS_DTYPE) as a uint8 tensor for collectives."""
+    raw = np.frombuffer(np.ascontiguousarray(job).tobytes(), dtype=np.uint8).copy()
+    return torch.from_numpy(raw).to(device)
+
+
+def allgather_job_stats(job_bytes: torch.Tensor, group=None) -> np.ndarray:
+    """All-gather each rank's job record (uint8 tensor of one JOB_STATS_DTYPE)
+    and return the exact merge over ranks (rank order; the merge is
+    associative, so any order gives the same record)."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    parts = [torch.empty_like(job_bytes) for _ in range(world)]
+    dist.all_gather(parts, job_bytes.contiguous(), group=group)
+    recs = [p.cpu().numpy().view(_abi.JOB_STATS_DTYPE)[0] for p in parts]
+    return merge_job_stats(recs)

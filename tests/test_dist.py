@@ -1,0 +1,99 @@
+"""Multi-rank path on CPU (gloo, world size 2): sharding covers every
+replication once, and the all-gathered job record merged with the product's
+exact merge equals the single-process record."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from fognetsimpp_amd import _abi
+from fognetsimpp_amd.dist import allgather_job_stats, job_record_tensor, shard
+from fognetsimpp_amd.engine import merge_job_stats
+
+
+def job_from_rep_stats(st):
+    """Test-side exact rep -> job record (what reduce_kernel computes on the device)."""
+    rec = np.zeros(1, dtype=_abi.JOB_STATS_DTYPE)[0]
+    rec["n_reps"] = len(st)
+    ok = st[st["status"] == 0]
+    rec["n_failed"] = len(st) - len(ok)
+    for f in ("n_tasks", "n_queued", "n_started", "events"):
+        rec[f] = int(ok[f].sum())
+    big = np.iinfo(np.int64)
+    rec["last_tick"] = int(ok["last_tick"].max()) if len(ok) else big.min
+    rec["queue_min_ticks"] = int(ok["queue_min_ticks"].min()) if len(ok) else big.max
+    rec["resp_min_ticks"] = int(ok["resp_min_ticks"].min()) if len(ok) else big.max
+    rec["queue_max_ticks"] = int(ok["queue_max_ticks"].max()) if len(ok) else big.min
+    rec["resp_max_ticks"] = int(ok["resp_max_ticks"].max()) if len(ok) else big.min
+    rec["max_pending"] = int(ok["max_pending"].max()) if len(ok) else 0
+    for name, lo, hi in (("queue_sum", "queue_sum_lo", "queue_sum_hi"), ("queue_sq", "queue_sq_lo", "queue_sq_hi"),
+                         ("resp_sum", "resp_sum_lo", "resp_sum_hi"), ("resp_sq", "resp_sq_lo", "resp_sq_hi")):
+        tot = sum(int(a) | (int(b) << 64) for a, b in zip(ok[lo], ok[hi]))
+        rec[name] = [(tot >> (64 * i)) & (2**64 - 1) for i in range(3)]
+    return rec
+
+
+def test_shard_partitions():
+    for total in (0, 1, 7, 4096, 1_000_000):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for rank in range(world):
+                r0, n = shard(total, world, rank)
+                seen.extend(range(r0, r0 + n))
+            assert seen == list(range(total))
+
+
+def _worker(rank, world, port, reps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle_lib as ol
+    import tracegen as tg
+    r0, n = shard(reps, world, rank)
+    recs = []
+    for r in range(r0, r0 + n):
+        rp = tg.make_replication(77, r, 16, 400, rho=(0.5, 0.9)[r % 2])
+        recs.append(ol.run_batch(rp["arrive"], rp["req"], rp["mips"], rp["dl"], rp["ul"], rp["init"])["stats"])
+    st = np.concatenate(recs).view(_abi.REP_STATS_DTYPE) if recs else np.zeros(0, _abi.REP_STATS_DTYPE)
+    merged = allgather_job_stats(job_record_tensor(job_from_rep_stats(st), torch.device("cpu")))
+    if rank == 0:
+        q.put(merged.tobytes())
+    dist.destroy_process_group()
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_job_stats_match_single_process():
+    import oracle_lib as ol
+    import tracegen as tg
+    reps = 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, reps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=110)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    sts = []
+    for r in range(reps):
+        rp = tg.make_replication(77, r, 16, 400, rho=(0.5, 0.9)[r % 2])
+        sts.append(ol.run_batch(rp["arrive"], rp["req"], rp["mips"], rp["dl"], rp["ul"], rp["init"])["stats"])
+    st = np.concatenate(sts).view(_abi.REP_STATS_DTYPE)
+    single = job_from_rep_stats(st)
+    assert got == merge_job_stats([single]).tobytes()
+    # and the merge is associative: per-replication records merged one by one
+    one_by_one = merge_job_stats([job_from_rep_stats(st[i:i + 1]) for i in range(reps)])
+    assert one_by_one.tobytes() == got
