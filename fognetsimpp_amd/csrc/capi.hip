@@ -78,7 +78,9 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   a->node_stride = in->node_stride;
   a->q_log2 = qlog;
   // busy (a sum of at most Q pending service times) must stay below 2^32 s
-  a->max_s = (uint32_t)(0xFFFFFFFFull / (uint64_t)q);
+  // and a service time fits 24 bits (the replay kernel packs it with a stamp)
+  const uint64_t by_ring = 0xFFFFFFFFull / (uint64_t)q;
+  a->max_s = (uint32_t)(by_ring < 0xFFFFFFull ? by_ring : 0xFFFFFFull);
   a->arrive = in->arrive_tick;
   a->req = in->req_mips;
   a->mips = in->mips;

@@ -33,7 +33,8 @@ struct Slot {
   uint64_t vkey;     // broker view of the node: (advertised busy seconds << 16) | node index
   int64_t nxt;       // tick at which the head's completion advert reaches the broker
   int64_t hd_done;   // head (oldest pending) task: completion tick
-  uint32_t hd_C, hd_S;
+  uint32_t hd_C;
+  uint32_t hd_S;      // head service seconds (bits 0-23) | nh prefetch stamp (bits 24-31)
   u32x4 nh;          // entry head+1 as loaded {a lo, a hi, C, S} (valid when >= 2 pending)
   int64_t tl_a;      // tail (newest) task
   int64_t tl_done;
@@ -42,19 +43,63 @@ struct Slot {
                      // completion adverts applied (bits 16-31); capacity <= 2^15
 };
 
+// ---- head+1 prefetch, outside the compiler's wait-count tracking
+//
+// The head+1 entry of a node is needed at that node's next advert, typically
+// many publishes later.  A compiler-visible load cannot express that: its
+// loop-carried destination gets a conservative `s_waitcnt vmcnt(0)` at the
+// first read in the next loop iteration (loads and stores share the in-order
+// vmcnt counter, and the count between issue and use is data dependent).  So
+// the prefetch is an inline-asm load into the tied loop-carried registers,
+// and reads are preceded by an explicit wait (nh_read_*) whose count follows
+// from the publishes decided since the issue: each publish issues >= 5 vector
+// memory operations (one ring store, four output stores), so a load issued
+// >= kPrefetchAge publishes ago is older than the kPrefetchOps youngest and has
+// completed once vmcnt <= kPrefetchOps.  Vector-memory loads return in issue
+// order on gfx950, so a newer prefetch into the same registers wins.
+constexpr uint32_t kPrefetchAge = 8;
+constexpr int kPrefetchOps = 40;  // 5 * kPrefetchAge, <= 63 (vmcnt field)
+
+__device__ __forceinline__ void prefetch_entry(u32x4& nh, const RingEntry* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(nh) : "v"(p) : "memory");
+}
+
+// Wave-level wait, then copy nh into fresh registers in the same asm
+// statement, so no compiler-generated instruction ever reads nh: the
+// registers are only named by these asm statements (an input operand is read
+// in place; a tied "+v" operand would be copied around the asm).
+#define FOGNET_NH_READ(CNT)                                                                          \
+  __device__ __forceinline__ u32x4 nh_read_##CNT(const u32x4& nh) {                                  \
+    uint32_t x, y, z, w;                                                                             \
+    asm volatile("s_waitcnt vmcnt(" #CNT ")\n\tv_mov_b32 %0, %4\n\tv_mov_b32 %1, %5\n\t"             \
+                 "v_mov_b32 %2, %6\n\tv_mov_b32 %3, %7"                                              \
+                 : "=&v"(x), "=&v"(y), "=&v"(z), "=&v"(w)                                            \
+                 : "v"(nh.x), "v"(nh.y), "v"(nh.z), "v"(nh.w));                                      \
+    return u32x4{x, y, z, w};                                                                        \
+  }
+FOGNET_NH_READ(0)
+FOGNET_NH_READ(40)
+#undef FOGNET_NH_READ
+static_assert(kPrefetchOps == 40, "nh_read_40 encodes the count");
+
 __device__ __forceinline__ uint32_t n_push(const Slot& st) { return st.cnt & 0xFFFFu; }
 __device__ __forceinline__ uint32_t n_head(const Slot& st) { return st.cnt >> 16; }
 __device__ __forceinline__ uint32_t pending(const Slot& st) { return (n_push(st) - n_head(st)) & 0xFFFFu; }
 
+__device__ __forceinline__ uint32_t head_S(const Slot& st) { return st.hd_S & 0xFFFFFFu; }
+// 8-bit issue stamp of the node's pending prefetch; a wrapped stamp can only
+// make an old prefetch look recent (a full wait), never the reverse.
+__device__ __forceinline__ void stamp_prefetch(Slot& st, uint32_t tix) {
+  st.hd_S = (st.hd_S & 0xFFFFFFu) | (tix << 24);
+}
+__device__ __forceinline__ uint32_t prefetch_age(const Slot& st, uint32_t tix) {
+  return (tix - (st.hd_S >> 24)) & 0xFFu;
+}
+
 constexpr uint64_t kNoKey = ~0ull;
+constexpr int64_t kNever = INT64_MAX;
 
 __device__ __forceinline__ int64_t nh_a(u32x4 v) { return (int64_t)(((uint64_t)v.y << 32) | v.x); }
-
-// one dwordx4 load of a ring entry, kept as a single 4-register value
-__device__ __forceinline__ u32x4 load_entry(const RingEntry* ring, uint32_t i) {
-  return *reinterpret_cast<const u32x4*>(ring + i);
-}
-constexpr int64_t kNever = INT64_MAX;
 
 // arrival at tick `a` happens before the completion at `done` of a task with
 // service S on a node with downlink latency dl (FES insertion-order rule).
@@ -62,14 +107,15 @@ __device__ __forceinline__ bool arrives_before(int64_t a, int64_t done, int64_t 
   return a < done || (a == done && dl >= (int64_t)S * kTicksPerSecond);
 }
 
-// Apply the advert of the head completion of node k (lane-local).
-__device__ __forceinline__ void apply_advert(Slot& st, int k, int64_t dl, int64_t ul,
-                                             const RingEntry* ring, uint32_t qmask) {
+// Apply the advert of the head completion of node k (lane-local).  nhw is
+// st.nh read after the wait (nh_read_*).  tix: index of the publish being decided.
+__device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, int64_t dl, int64_t ul,
+                                             const RingEntry* ring, uint32_t qmask, uint32_t tix) {
   // Cumulative service of the tasks that reached the node before the head's
   // completion: scan back from the newest assignment.
   uint32_t c_arrived = st.hd_C;  // the head itself always arrived before it completed
   const uint32_t pend0 = pending(st);  // >= 1 whenever an advert is due
-  if (arrives_before(st.tl_a, st.hd_done, dl, st.hd_S)) {
+  if (arrives_before(st.tl_a, st.hd_done, dl, head_S(st))) {
     c_arrived = st.tl_C;
   } else {
     // entries head+d, d = pend0-2 .. 1 (the tail, d = pend0-1, did not qualify)
@@ -77,14 +123,14 @@ __device__ __forceinline__ void apply_advert(Slot& st, int k, int64_t dl, int64_
       int64_t a;
       uint32_t C;
       if (d == 1u) {
-        a = nh_a(st.nh);
-        C = st.nh.z;
+        a = nh_a(nhw);
+        C = nhw.z;
       } else {
         const RingEntry e = ring[(n_head(st) + d) & qmask];
         a = e.a;
         C = e.C;
       }
-      if (arrives_before(a, st.hd_done, dl, st.hd_S)) {
+      if (arrives_before(a, st.hd_done, dl, head_S(st))) {
         c_arrived = C;
         break;
       }
@@ -100,32 +146,34 @@ __device__ __forceinline__ void apply_advert(Slot& st, int k, int64_t dl, int64_
     st.nxt = kNever;
     return;
   }
-  const int64_t na = nh_a(st.nh);
+  const int64_t na = nh_a(nhw);
   const int64_t start = na > st.hd_done ? na : st.hd_done;
-  st.hd_done = start + (int64_t)st.nh.w * kTicksPerSecond;
-  st.hd_C = st.nh.z;
-  st.hd_S = st.nh.w;
+  st.hd_done = start + (int64_t)nhw.w * kTicksPerSecond;
+  st.hd_C = nhw.z;
+  st.hd_S = (st.hd_S & 0xFF000000u) | nhw.w;
   st.nxt = st.hd_done + ul;
-  // st.nh (entry head+1) is refreshed by the caller with a load issued by
-  // every lane in uniform control flow (refresh_nh).
+  if (pend >= 2u) {  // the ring holds every pending entry, the tail included
+    prefetch_entry(st.nh, ring + ((n_head(st) + 1u) & qmask));
+    stamp_prefetch(st, tix);
+  }
 }
 
-// Refresh the head+1 cache of every lane's node in one slot.  The ring holds
-// every pending entry (the tail included), and a lane whose head did not move
-// simply reloads the same entry; with fewer than two entries pending the
-// value is unused.  Issued by all lanes outside any divergent branch, the
-// load targets the loop-carried registers directly, so it is waited for at
-// the node's next advert instead of here (a load inside a divergent branch
-// would be copied into them at the merge, forcing an immediate vmcnt wait).
-__device__ __forceinline__ void refresh_nh(Slot& st, const RingEntry* ring, uint32_t qmask) {
-  st.nh = load_entry(ring, (n_head(st) + 1u) & qmask);
+// Reload nh of every lane in a slot from its node's current head+1 ring entry,
+// issued by all lanes in uniform control flow (an asm load inside a divergent
+// branch is given a temporary that the compiler copies back before the data
+// lands).  For a lane whose head+1 did not change this is a duplicate of the
+// same address: the register already holds, or will receive, the same value,
+// so its stamp is left alone.  The ring store of a just-pushed entry precedes
+// this load in the same lane, which therefore observes it.
+__device__ __forceinline__ void refill_slot(Slot& st, const RingEntry* ring, uint32_t qmask) {
+  prefetch_entry(st.nh, ring + ((n_head(st) + 1u) & qmask));
 }
 
 // Assign publish o_idx, decided at tick t with requirement rq, to node k
 // (lane-local).  Returns (fognet_status << 24) | tasks pending on k after the push.
 __device__ __forceinline__ uint32_t push_task(Slot& st, int k, int64_t t, int32_t rq, int64_t dl, int64_t ul,
                                               int32_t mips, RingEntry* ring, uint32_t qmask,
-                                              const ReplayArgs& A, size_t o_idx) {
+                                              const ReplayArgs& A, size_t o_idx, uint32_t tix) {
   const uint32_t max_s = A.max_s;
   struct {
     uint32_t err;
@@ -158,15 +206,18 @@ __device__ __forceinline__ uint32_t push_task(Slot& st, int k, int64_t t, int32_
     e.a = a;
     e.C = C;
     e.S = S;
-    ring[n_push(st) & qmask] = e;
+    RingEntry* slot = ring + (n_push(st) & qmask);
+    *slot = e;
     if (pend == 0u) {
       st.hd_done = done;
       st.hd_C = C;
-      st.hd_S = S;
+      st.hd_S = (st.hd_S & 0xFF000000u) | S;
       st.nxt = done + ul;
+    } else if (pend == 1u) {
+      // the new entry is head+1: the caller reloads nh for the whole slot
+      // (refill_slot), in uniform control flow
+      stamp_prefetch(st, tix);
     }
-    // pend == 1: the new entry is head+1; the caller's refresh_nh reads it
-    // back (same lane, same address: the load observes the store)
     st.tl_a = a;
     st.tl_C = C;
     st.tl_S = S;
@@ -275,6 +326,7 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
     for (; j < cnt; ++j) {
       const int64_t t = readlane_i64(ca, j);
       const int32_t rq = (int32_t)readlane_u32((uint32_t)cr, j);
+      const uint32_t tix = (uint32_t)(c0 + j);
 
       // 1) completion adverts that reached the broker strictly before t
 #pragma unroll
@@ -283,11 +335,17 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
           const bool due = st[s].nxt < t;
           if (!ballot(due)) break;
           dirty = true;
+          // the due nodes read their prefetched head+1 entry
+          u32x4 nhw;
+          if (ballot(due && prefetch_age(st[s], tix) < kPrefetchAge)) {
+            nhw = nh_read_0(st[s].nh);
+          } else {
+            nhw = nh_read_40(st[s].nh);
+          }
           if (due) {
             const int k = s * kWave + lane;
-            apply_advert(st[s], k, s_dl[k], s_ul[k], ring_s(s), qmask);
+            apply_advert(st[s], nhw, k, s_dl[k], s_ul[k], ring_s(s), qmask, tix);
           }
-          refresh_nh(st[s], ring_s(s), qmask);
         }
       }
       // 2) argmin over the advertised view (ties -> lowest index)
@@ -301,12 +359,9 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
       uint32_t po = 0u;
 #pragma unroll
       for (int s = 0; s < NPL; ++s) {
-        if (s == ks) {  // wave-uniform
-          if (lane == kl) {
-            po = push_task(st[s], k, t, rq, s_dl[k], s_ul[k], s_mips[k], ring_s(s), qmask, A,
-                           tbase + c0 + j);
-          }
-          refresh_nh(st[s], ring_s(s), qmask);
+        if (s == ks && lane == kl) {
+          po = push_task(st[s], k, t, rq, s_dl[k], s_ul[k], s_mips[k], ring_s(s), qmask, A,
+                         tbase + c0 + j, tix);
         }
       }
       const uint32_t pr = readlane_u32(po, kl);
@@ -316,9 +371,16 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
       }
       const uint32_t pend = pr & 0xFFFFFFu;
       max_pend = pend > max_pend ? pend : max_pend;
+      if (pend == 2u) {  // the new entry became head+1 of node k
+#pragma unroll
+        for (int s = 0; s < NPL; ++s)
+          if (s == ks) refill_slot(st[s], ring_s(s), qmask);
+      }
     }
     n_done += j;
   }
+  // drain the inline-asm prefetches before the wave retires
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   if (lane == 0 && A.out_stats) {
     fognet_rep_stats* S = A.out_stats + r;

@@ -1,0 +1,66 @@
+"""Audit the replay kernel ISA: the registers that receive inline-asm prefetch
+loads must be referenced only by inline asm (the prefetch loads and the
+wait+copy reads).  Usage: python tools/check_nh_regs.py build/asm/replay-...-gfx950.s"""
+import re
+import sys
+
+
+def regs_of(s):
+    out = set()
+    for m in re.finditer(r"v\[(\d+):(\d+)\]", s):
+        out |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+    for m in re.finditer(r"\bv(\d+)\b", s):
+        out.add(int(m.group(1)))
+    return out
+
+
+def audit(path, kernel_prefix="_ZN6fognet12_GLOBAL__N_113replay_kernelILi"):
+    text = open(path).read().split("\n")
+    bad_total = 0
+    for npl in (1, 2, 4):
+        name = f"{kernel_prefix}{npl}EEEvNS_10ReplayArgsE"
+        starts = [i for i, ln in enumerate(text) if ln.startswith(f"{name}:")]
+        if not starts:
+            continue
+        s = starts[0]
+        body = []
+        for ln in text[s + 1:]:
+            if ln.startswith(".Lfunc_end"):
+                break
+            body.append(ln.strip())
+        nh = set()
+        in_asm = False
+        for ln in body:
+            if ln.startswith(";;#ASMSTART"):
+                in_asm = True
+            elif ln.startswith(";;#ASMEND"):
+                in_asm = False
+            elif in_asm and ln.startswith("global_load_dwordx4"):
+                nh |= regs_of(ln.split(",")[0])
+        # audit region: from the first loop header to the final drain (the
+        # last inline asm); the zero-initialisation precedes the loop and the
+        # statistics epilogue follows the drain
+        lo = next(i for i, ln in enumerate(body) if "Loop Header" in ln)
+        hi = max(i for i, ln in enumerate(body) if ln.startswith(";;#ASMSTART"))
+        bad = []
+        in_asm = False
+        for ln in body[lo:hi]:
+            if ln.startswith(";;#ASMSTART"):
+                in_asm = True
+                continue
+            if ln.startswith(";;#ASMEND"):
+                in_asm = False
+                continue
+            if not ln or ln.startswith(";") or ln.startswith("."):
+                continue
+            if not in_asm and regs_of(ln) & nh:
+                bad.append(ln)
+        print(f"NPL={npl}: prefetch registers {sorted(nh)}; compiler references outside asm: {len(bad)}")
+        for b in bad[:20]:
+            print("   ", b)
+        bad_total += len(bad)
+    return bad_total
+
+
+if __name__ == "__main__":
+    sys.exit(1 if audit(sys.argv[1]) else 0)
