@@ -201,7 +201,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
   int rc = prepare(c, in, &a);
   if (rc) return rc;
   if (!out->stats) return fail(c, FOGNET_ERR_ARG, "stats output is required (per-replication status)");
-  if (!out->node || !out->status || !out->start_tick || !out->done_tick)
+  if (a.T > 0 && (!out->node || !out->status || !out->start_tick || !out->done_tick))
     return fail(c, FOGNET_ERR_UNSUPPORTED, "per-task outputs are required (stats-only mode not implemented)");
   if (a.R == 0) return FOGNET_OK;
   rc = set_device(c);
