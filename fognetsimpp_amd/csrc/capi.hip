@@ -77,10 +77,12 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   a->N = in->N;
   a->node_stride = in->node_stride;
   a->q_log2 = qlog;
-  // busy (a sum of at most Q pending service times) must stay below 2^32 s
-  // and a service time fits 24 bits (the replay kernel packs it with a stamp)
-  const uint64_t by_ring = 0xFFFFFFFFull / (uint64_t)q;
-  a->max_s = (uint32_t)(by_ring < 0xFFFFFFull ? by_ring : 0xFFFFFFull);
+  // busy (a sum of at most Q pending service times) must stay below 2^24 s
+  // (the replay kernel's 32-bit view key is busy << 8 | node), and service
+  // times stay below 2^16 s (18.2 h) so its run scan cannot overflow
+  // (replay.hip, kMaxTick).  Q = 1024: at most 16383 s per task.
+  const uint64_t by_ring = 0xFFFFFFull / (uint64_t)q;
+  a->max_s = (uint32_t)(by_ring < 0xFFFFull ? by_ring : 0xFFFFull);
   a->arrive = in->arrive_tick;
   a->req = in->req_mips;
   a->mips = in->mips;

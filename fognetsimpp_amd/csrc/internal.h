@@ -61,6 +61,17 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
   return umin64(umin64(r0, r1), umin64(r2, r3));
 }
 
+// The same for u32 with native DPP-fed v_min_u32.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  v = min(v, dpp_u32<0xB1>(v));
+  v = min(v, dpp_u32<0x4E>(v));
+  v = min(v, dpp_u32<0x141>(v));
+  v = min(v, dpp_u32<0x140>(v));
+  const uint32_t r0 = readlane_u32(v, 0), r1 = readlane_u32(v, 16);
+  const uint32_t r2 = readlane_u32(v, 32), r3 = readlane_u32(v, 48);
+  return min(min(r0, r1), min(r2, r3));
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 
 struct U4 {

@@ -11,7 +11,7 @@
 //
 // Instead of dispatching the ~4 FES events per task one by one, the kernel
 // walks the broker's publishes in trace order and derives everything else in
-// closed form (DESIGN.md §Replay algorithm):
+// closed form:
 //   * a node is a FIFO single server, so a task's service start/done ticks
 //     follow from the previous task on the same node when it is decided;
 //   * the broker's view of node k changes only when the advert of one of k's
@@ -23,6 +23,13 @@
 //   * same-tick ordering follows OMNeT++'s (tick, insertion order) FES rule:
 //     trace publishes precede dynamic events at their tick, and a task's
 //     arrival precedes a same-tick completion iff dl_k >= S_completing * 1e12.
+//
+// Decision runs.  The broker's view is stale, so consecutive publishes keep
+// going to the same node until an advert changes the argmin (runs of 50-200
+// publishes at the C3 sweep).  The kernel finds, lane-parallel, the earliest
+// advert that could change the decision (run horizon), then pushes the whole
+// run (up to the 64 publishes of a trace chunk, one per lane) with a (max,+)
+// scan over the FIFO recurrence and coalesced ring and output stores.
 #include "internal.h"
 
 namespace fognet {
@@ -30,18 +37,30 @@ namespace fognet {
 namespace {
 
 struct Slot {
-  uint64_t vkey;     // broker view of the node: (advertised busy seconds << 16) | node index
+  uint32_t vkey;     // broker view of the node: (advertised busy seconds << 8) | node index
   int64_t nxt;       // tick at which the head's completion advert reaches the broker
   int64_t hd_done;   // head (oldest pending) task: completion tick
-  uint32_t hd_C;
-  uint32_t hd_S;      // head service seconds (bits 0-23) | nh prefetch stamp (bits 24-31)
-  u32x4 nh;          // entry head+1 as loaded {a lo, a hi, C, S} (valid when >= 2 pending)
-  int64_t tl_a;      // tail (newest) task
-  int64_t tl_done;
-  uint32_t tl_C, tl_S;
+  uint32_t hd_C;     // cumulative service up to and including the head
+  uint32_t hd_S;     // head service seconds (bits 0-23) | nh prefetch stamp (bits 24-31)
+  u32x4 nh;          // entry head+1 {a lo, a hi, C, S}; written only by inline asm
+  int64_t tl_a;      // tail (newest) task: arrival tick at the node
+  // (tail completion tick, cumulative service and service time live in LDS:
+  //  s_tld / s_tlC / s_tlS, read at a uniform address when the node is chosen)
   uint32_t cnt;      // ring counters mod 2^16: tasks ever assigned (bits 0-15),
                      // completion adverts applied (bits 16-31); capacity <= 2^15
 };
+
+constexpr uint32_t kNoKey = ~0u;
+constexpr int64_t kNever = INT64_MAX;
+// Simulated ticks are kept below 2^61 (26.7 days) and service times below
+// 2^16 s, so no intermediate of the run scan can overflow int64.
+constexpr int64_t kMaxTick = (int64_t)1 << 61;
+
+__device__ __forceinline__ uint32_t n_push(const Slot& st) { return st.cnt & 0xFFFFu; }
+__device__ __forceinline__ uint32_t n_head(const Slot& st) { return st.cnt >> 16; }
+__device__ __forceinline__ uint32_t pending(const Slot& st) { return (n_push(st) - n_head(st)) & 0xFFFFu; }
+__device__ __forceinline__ uint32_t head_S(const Slot& st) { return st.hd_S & 0xFFFFFFu; }
+__device__ __forceinline__ int64_t nh_a(u32x4 v) { return (int64_t)(((uint64_t)v.y << 32) | v.x); }
 
 // ---- head+1 prefetch, outside the compiler's wait-count tracking
 //
@@ -50,24 +69,25 @@ struct Slot {
 // loop-carried destination gets a conservative `s_waitcnt vmcnt(0)` at the
 // first read in the next loop iteration (loads and stores share the in-order
 // vmcnt counter, and the count between issue and use is data dependent).  So
-// the prefetch is an inline-asm load into the tied loop-carried registers,
-// and reads are preceded by an explicit wait (nh_read_*) whose count follows
-// from the publishes decided since the issue: each publish issues >= 5 vector
-// memory operations (one ring store, four output stores), so a load issued
-// >= kPrefetchAge publishes ago is older than the kPrefetchOps youngest and has
-// completed once vmcnt <= kPrefetchOps.  Vector-memory loads return in issue
-// order on gfx950, so a newer prefetch into the same registers wins.
-constexpr uint32_t kPrefetchAge = 8;
-constexpr int kPrefetchOps = 40;  // 5 * kPrefetchAge, <= 63 (vmcnt field)
+// the prefetch is an inline-asm load into loop-carried registers that only
+// inline asm ever names (tools/check_nh_regs.py audits the ISA), and reads go
+// through nh_read_*, which waits and copies in one asm statement.
+//
+// The wait count comes from a wave-uniform tally `ops` of vector-memory
+// instructions that are certainly issued (the five stores of every push run,
+// the slot refills).  A node's prefetch is stamped with the tally at issue;
+// once kPrefetchOps tallied instructions were issued after it, it is older
+// than the kPrefetchOps youngest and `s_waitcnt vmcnt(kPrefetchOps)` covers
+// it, otherwise the wait is vmcnt(0).  Untallied instructions only make the
+// real count larger (safe).  The stamp keeps 8 bits; a wrapped stamp can only
+// make an old prefetch look recent.  Vector-memory loads return in issue
+// order on gfx950, so the newest prefetch into a register wins.
+constexpr uint32_t kPrefetchOps = 8;
 
 __device__ __forceinline__ void prefetch_entry(u32x4& nh, const RingEntry* p) {
   asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(nh) : "v"(p) : "memory");
 }
 
-// Wave-level wait, then copy nh into fresh registers in the same asm
-// statement, so no compiler-generated instruction ever reads nh: the
-// registers are only named by these asm statements (an input operand is read
-// in place; a tied "+v" operand would be copied around the asm).
 #define FOGNET_NH_READ(CNT)                                                                          \
   __device__ __forceinline__ u32x4 nh_read_##CNT(const u32x4& nh) {                                  \
     uint32_t x, y, z, w;                                                                             \
@@ -78,28 +98,33 @@ __device__ __forceinline__ void prefetch_entry(u32x4& nh, const RingEntry* p) {
     return u32x4{x, y, z, w};                                                                        \
   }
 FOGNET_NH_READ(0)
-FOGNET_NH_READ(40)
+FOGNET_NH_READ(8)
 #undef FOGNET_NH_READ
-static_assert(kPrefetchOps == 40, "nh_read_40 encodes the count");
+static_assert(kPrefetchOps == 8, "nh_read_8 encodes the count");
 
-__device__ __forceinline__ uint32_t n_push(const Slot& st) { return st.cnt & 0xFFFFu; }
-__device__ __forceinline__ uint32_t n_head(const Slot& st) { return st.cnt >> 16; }
-__device__ __forceinline__ uint32_t pending(const Slot& st) { return (n_push(st) - n_head(st)) & 0xFFFFu; }
-
-__device__ __forceinline__ uint32_t head_S(const Slot& st) { return st.hd_S & 0xFFFFFFu; }
-// 8-bit issue stamp of the node's pending prefetch; a wrapped stamp can only
-// make an old prefetch look recent (a full wait), never the reverse.
-__device__ __forceinline__ void stamp_prefetch(Slot& st, uint32_t tix) {
-  st.hd_S = (st.hd_S & 0xFFFFFFu) | (tix << 24);
+__device__ __forceinline__ void stamp_prefetch(Slot& st, uint32_t ops) {
+  st.hd_S = (st.hd_S & 0xFFFFFFu) | (ops << 24);
 }
-__device__ __forceinline__ uint32_t prefetch_age(const Slot& st, uint32_t tix) {
-  return (tix - (st.hd_S >> 24)) & 0xFFu;
+__device__ __forceinline__ bool prefetch_recent(const Slot& st, uint32_t ops) {
+  return ((ops - (st.hd_S >> 24)) & 0xFFu) < kPrefetchOps;
 }
 
-constexpr uint64_t kNoKey = ~0ull;
-constexpr int64_t kNever = INT64_MAX;
+// Wave-level read of a slot's nh for the lanes in `need`.
+__device__ __forceinline__ u32x4 read_nh(const Slot& st, bool need, uint32_t ops) {
+  if (ballot(need && prefetch_recent(st, ops))) return nh_read_0(st.nh);
+  return nh_read_8(st.nh);
+}
 
-__device__ __forceinline__ int64_t nh_a(u32x4 v) { return (int64_t)(((uint64_t)v.y << 32) | v.x); }
+// Reload nh of every lane in a slot from its node's current head+1 ring entry,
+// issued by all lanes in uniform control flow (an asm load inside a divergent
+// branch gets a temporary that the compiler copies back before the data
+// lands).  For a lane whose head+1 did not change this is a duplicate of the
+// same address, harmless under in-order returns, so its stamp is left alone.
+// Ring stores issued earlier by this wave (any lane) precede it in the same
+// in-order memory pipeline, so it observes them.
+__device__ __forceinline__ void refill_slot(Slot& st, const RingEntry* ring, uint32_t qmask) {
+  prefetch_entry(st.nh, ring + ((n_head(st) + 1u) & qmask));
+}
 
 // arrival at tick `a` happens before the completion at `done` of a task with
 // service S on a node with downlink latency dl (FES insertion-order rule).
@@ -107,39 +132,38 @@ __device__ __forceinline__ bool arrives_before(int64_t a, int64_t done, int64_t 
   return a < done || (a == done && dl >= (int64_t)S * kTicksPerSecond);
 }
 
-// Apply the advert of the head completion of node k (lane-local).  nhw is
-// st.nh read after the wait (nh_read_*).  tix: index of the publish being decided.
-__device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, int64_t dl, int64_t ul,
-                                             const RingEntry* ring, uint32_t qmask, uint32_t tix) {
-  // Cumulative service of the tasks that reached the node before the head's
-  // completion: scan back from the newest assignment.
-  uint32_t c_arrived = st.hd_C;  // the head itself always arrived before it completed
-  const uint32_t pend0 = pending(st);  // >= 1 whenever an advert is due
-  if (arrives_before(st.tl_a, st.hd_done, dl, head_S(st))) {
-    c_arrived = st.tl_C;
-  } else {
-    // entries head+d, d = pend0-2 .. 1 (the tail, d = pend0-1, did not qualify)
-    for (uint32_t d = pend0 - 1u; d-- > 1u;) {
-      int64_t a;
-      uint32_t C;
-      if (d == 1u) {
-        a = nh_a(nhw);
-        C = nhw.z;
-      } else {
-        const RingEntry e = ring[(n_head(st) + d) & qmask];
-        a = e.a;
-        C = e.C;
-      }
-      if (arrives_before(a, st.hd_done, dl, head_S(st))) {
-        c_arrived = C;
-        break;
-      }
+// Cumulative service of the tasks that reached the node before the
+// completion (tick `done`, service S) of pending entry head+d0; scans back
+// from the newest assignment.  c_self: cumulative service of that entry.
+__device__ __forceinline__ uint32_t c_arrived(const Slot& st, const u32x4 nhw, int64_t done, uint32_t S,
+                                              uint32_t d0, uint32_t c_self, int64_t dl, uint32_t tl_C,
+                                              const RingEntry* ring, uint32_t qmask) {
+  if (arrives_before(st.tl_a, done, dl, S)) return tl_C;
+  const uint32_t pend = pending(st);
+  // entries head+d for d = pend-2 .. d0+1 (the tail, d = pend-1, did not qualify)
+  for (uint32_t d = pend - 1u; d-- > d0 + 1u;) {
+    int64_t a;
+    uint32_t C;
+    if (d == 1u) {
+      a = nh_a(nhw);
+      C = nhw.z;
+    } else {
+      const RingEntry e = ring[(n_head(st) + d) & qmask];
+      a = e.a;
+      C = e.C;
     }
+    if (arrives_before(a, done, dl, S)) return C;
   }
-  const uint32_t busy = c_arrived - st.hd_C;  // busyTime after releaseResource (:232, :254)
-  st.vkey = ((uint64_t)busy << 16) | (uint32_t)k;
+  return c_self;  // only the completing task itself
+}
 
-  // advance the head
+// Apply the advert of the head completion of node k (lane-local): the broker
+// view takes busyTime after releaseResource (:232, :254), the head advances
+// and entry head+2 is prefetched.  nhw: st.nh read after its wait.
+__device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, int64_t dl, int64_t ul, uint32_t tl_C,
+                                             const RingEntry* ring, uint32_t qmask, uint32_t ops) {
+  const uint32_t busy = c_arrived(st, nhw, st.hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask) - st.hd_C;
+  st.vkey = (busy << 8) | (uint32_t)k;  // busy < 2^24 (max_s * ring capacity)
   st.cnt += 0x10000u;
   const uint32_t pend = pending(st);
   if (pend == 0u) {
@@ -154,91 +178,43 @@ __device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, i
   st.nxt = st.hd_done + ul;
   if (pend >= 2u) {  // the ring holds every pending entry, the tail included
     prefetch_entry(st.nh, ring + ((n_head(st) + 1u) & qmask));
-    stamp_prefetch(st, tix);
+    stamp_prefetch(st, ops);
   }
 }
 
-// Reload nh of every lane in a slot from its node's current head+1 ring entry,
-// issued by all lanes in uniform control flow (an asm load inside a divergent
-// branch is given a temporary that the compiler copies back before the data
-// lands).  For a lane whose head+1 did not change this is a duplicate of the
-// same address: the register already holds, or will receive, the same value,
-// so its stamp is left alone.  The ring store of a just-pushed entry precedes
-// this load in the same lane, which therefore observes it.
-__device__ __forceinline__ void refill_slot(Slot& st, const RingEntry* ring, uint32_t qmask) {
-  prefetch_entry(st.nh, ring + ((n_head(st) + 1u) & qmask));
-}
-
-// Assign publish o_idx, decided at tick t with requirement rq, to node k
-// (lane-local).  Returns (fognet_status << 24) | tasks pending on k after the push.
-__device__ __forceinline__ uint32_t push_task(Slot& st, int k, int64_t t, int32_t rq, int64_t dl, int64_t ul,
-                                              int32_t mips, RingEntry* ring, uint32_t qmask,
-                                              const ReplayArgs& A, size_t o_idx, uint32_t tix) {
-  const uint32_t max_s = A.max_s;
-  struct {
-    uint32_t err;
-  } o;
-  o.err = FOGNET_OK;
-  const uint32_t S = (uint32_t)rq / (uint32_t)mips;  // double tskTime = requiredMIPS / MIPS (:276)
-  const int64_t dur = (int64_t)S * kTicksPerSecond;
-  if (S > max_s || t > kNever - dl) o.err = FOGNET_ERR_ARG;
-  const int64_t a = t + dl;
-  uint32_t status;
-  int64_t start;
-  if (st.tl_done < a) {  // tl_done starts at INT64_MIN: first task of the node
-    status = 5u;  // idle: "task assigned" (:282-301)
-    start = a;
-  } else if (st.tl_done > a) {
-    status = 4u;  // busy: "task queued" (:304-313), starts when the previous one completes
-    start = st.tl_done;
-  } else {  // completion of the previous task at the same tick
-    status = (dl < (int64_t)st.tl_S * kTicksPerSecond) ? 5u : 4u;
-    start = a;
-  }
-  if (start > kNever - dur) o.err = FOGNET_ERR_ARG;
-  const int64_t done = start + dur;
-  if (done > kNever - ul) o.err = FOGNET_ERR_ARG;
+// Earliest tick at which an advert of node j (not the current argmin) could
+// change the decision whose key is best, for a window whose last publish is
+// at t_last.  The first two pending completions are evaluated exactly; a
+// third one's arrival is unknown without another ring read, so when its two
+// predecessors do not change the decision the horizon stops at the second.
+// No push reaches j during the run, so the values do not depend on it.
+__device__ __forceinline__ int64_t horizon(const Slot& st, const u32x4 nhw, int j, uint32_t best, int64_t t_last, uint32_t tl_C,
+                                           int64_t dl, int64_t ul, const RingEntry* ring, uint32_t qmask) {
   const uint32_t pend = pending(st);
-  if (pend > qmask) o.err = FOGNET_ERR_CAPACITY;
-  const uint32_t C = st.tl_C + S;
-  if (o.err == FOGNET_OK) {
-    RingEntry e;
-    e.a = a;
-    e.C = C;
-    e.S = S;
-    RingEntry* slot = ring + (n_push(st) & qmask);
-    *slot = e;
-    if (pend == 0u) {
-      st.hd_done = done;
-      st.hd_C = C;
-      st.hd_S = (st.hd_S & 0xFF000000u) | S;
-      st.nxt = done + ul;
-    } else if (pend == 1u) {
-      // the new entry is head+1: the caller reloads nh for the whole slot
-      // (refill_slot), in uniform control flow
-      stamp_prefetch(st, tix);
-    }
-    st.tl_a = a;
-    st.tl_C = C;
-    st.tl_S = S;
-    st.tl_done = done;
-    st.cnt = (st.cnt & 0xFFFF0000u) | ((st.cnt + 1u) & 0xFFFFu);
-    // per-task outputs, stored by the owner lane (consecutive tasks write
-    // consecutive addresses; the partial lines merge in L2)
-    A.out_node[o_idx] = k;
-    A.out_status[o_idx] = (uint8_t)status;
-    A.out_start[o_idx] = start;
-    A.out_done[o_idx] = done;
-  }
-  return (o.err << 24) | (pend + 1u);
+  const uint32_t v1 = c_arrived(st, nhw, st.hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask) - st.hd_C;
+  if (((v1 << 8) | (uint32_t)j) < best) return st.nxt;
+  if (pend < 2u) return kNever;
+  const int64_t na = nh_a(nhw);
+  const int64_t done2 = (na > st.hd_done ? na : st.hd_done) + (int64_t)nhw.w * kTicksPerSecond;
+  const int64_t x2 = done2 + ul;
+  if (x2 >= t_last) return kNever;
+  const uint32_t v2 = c_arrived(st, nhw, done2, nhw.w, 1u, nhw.z, dl, tl_C, ring, qmask) - nhw.z;
+  if (((v2 << 8) | (uint32_t)j) < best) return x2;
+  return pend == 2u ? kNever : x2;
 }
 
 template <int NPL>
-__device__ __forceinline__ uint64_t view_min(const Slot (&st)[NPL]) {
-  uint64_t m = st[0].vkey;
+__device__ __forceinline__ uint32_t view_min(const Slot (&st)[NPL]) {
+  uint32_t m = st[0].vkey;
 #pragma unroll
-  for (int s = 1; s < NPL; ++s) m = umin64(m, st[s].vkey);
-  return wave_min_u64(m);
+  for (int s = 1; s < NPL; ++s) m = min(m, st[s].vkey);
+  return wave_min_u32(m);
+}
+
+__device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int off) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)(uint64_t)v, off);
+  const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)((uint64_t)v >> 32), off);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 template <int NPL>
@@ -250,6 +226,9 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
   __shared__ int64_t s_dl[NPL * kWave];
   __shared__ int64_t s_ul[NPL * kWave];
   __shared__ int32_t s_mips[NPL * kWave];
+  __shared__ int64_t s_tld[NPL * kWave];   // tail completion tick (INT64_MIN: node never used)
+  __shared__ uint32_t s_tlC[NPL * kWave];  // tail cumulative service (mod 2^32)
+  __shared__ uint32_t s_tlS[NPL * kWave];  // tail service seconds
 
   const int T = A.T, N = A.N;
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
@@ -270,22 +249,22 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
       d = A.dl[nbase + k];
       u = A.ul[nbase + k];
       const int64_t ia = A.init[nbase + k];
-      bad |= (m <= 0) | (d < 0) | (u < 0) | (ia < u) | (ia >= arrive0);
+      bad |= (m <= 0) | (d < 0) | (u < 0) | (d > kMaxTick) | (u > kMaxTick) | (ia < u) | (ia >= arrive0);
     }
     s_dl[k] = d;
     s_ul[k] = u;
     s_mips[k] = m;
     // every node's first advert {MIPS, busyTime = 0.0} has reached the broker
-    st[s].vkey = k < N ? (uint64_t)k : kNoKey;
+    st[s].vkey = k < N ? (uint32_t)k : kNoKey;
     st[s].nxt = kNever;
     st[s].hd_done = 0;
     st[s].hd_C = 0u;
     st[s].hd_S = 0u;
     st[s].nh = u32x4{0u, 0u, 0u, 0u};
     st[s].tl_a = 0;
-    st[s].tl_done = INT64_MIN;
-    st[s].tl_C = 0u;
-    st[s].tl_S = 0u;
+    s_tld[k] = INT64_MIN;
+    s_tlC[k] = 0u;
+    s_tlS[k] = 0u;
     st[s].cnt = 0u;
   }
   __syncthreads();
@@ -294,17 +273,17 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
   if (N <= 0) err = FOGNET_ERR_NO_NODES;
 
   RingEntry* const ring_r = A.ring + (size_t)r * (size_t)N * ((size_t)qmask + 1u);
-  // ring of this lane's node in slot s (lanes past N alias node 0: in bounds,
-  // never used); recomputed at each use rather than held in 2 VGPRs per slot
   const int q_log2 = A.q_log2;
+  // ring of this lane's node in slot s (lanes past N alias node 0: in bounds, never used)
   auto ring_s = [&](int s) -> RingEntry* {
     const int k = s * kWave + lane;
     return ring_r + ((size_t)(k < N ? k : 0) << q_log2);
   };
-  uint64_t best = view_min<NPL>(st);
+  uint32_t best = view_min<NPL>(st);
   bool dirty = false;
   int64_t prev_t = INT64_MIN;
   uint32_t max_pend = 0u;
+  uint32_t ops = 0u;  // tally of issued vector-memory instructions (see kPrefetchOps)
   int64_t n_done = 0;
 
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
@@ -312,39 +291,31 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
     const bool live = lane < cnt;
     const int64_t ca = live ? A.arrive[tbase + c0 + lane] : kNever;
     const int32_t cr = live ? A.req[tbase + c0 + lane] : 0;
-    // trace preconditions: nondecreasing ticks, requirement >= 0
-    const int64_t up = (int64_t)(((uint64_t)(uint32_t)__shfl_up((int)((uint64_t)ca >> 32), 1) << 32) |
-                                 (uint32_t)__shfl_up((int)(uint32_t)(uint64_t)ca, 1));
+    // trace preconditions: nondecreasing ticks, requirement >= 0, ticks < 2^61
+    const int64_t up = shfl_up_i64(ca, 1);
     const int64_t prv = lane == 0 ? prev_t : up;
-    if (ballot(live && (ca < prv || cr < 0))) {
+    if (ballot(live && (ca < prv || cr < 0 || ca > kMaxTick))) {
       err = FOGNET_ERR_ARG;
       break;
     }
     prev_t = readlane_i64(ca, cnt - 1);
+    const int64_t t_last = prev_t;
 
-    int j = 0;
-    for (; j < cnt; ++j) {
-      const int64_t t = readlane_i64(ca, j);
-      const int32_t rq = (int32_t)readlane_u32((uint32_t)cr, j);
-      const uint32_t tix = (uint32_t)(c0 + j);
+    int jp = 0;
+    while (jp < cnt) {
+      const int64_t t_p = readlane_i64(ca, jp);
 
-      // 1) completion adverts that reached the broker strictly before t
+      // 1) completion adverts that reached the broker strictly before t_p
 #pragma unroll
       for (int s = 0; s < NPL; ++s) {
         for (;;) {
-          const bool due = st[s].nxt < t;
+          const bool due = st[s].nxt < t_p;
           if (!ballot(due)) break;
           dirty = true;
-          // the due nodes read their prefetched head+1 entry
-          u32x4 nhw;
-          if (ballot(due && prefetch_age(st[s], tix) < kPrefetchAge)) {
-            nhw = nh_read_0(st[s].nh);
-          } else {
-            nhw = nh_read_40(st[s].nh);
-          }
+          const u32x4 nhw = read_nh(st[s], due && pending(st[s]) >= 2u, ops);
           if (due) {
             const int k = s * kWave + lane;
-            apply_advert(st[s], nhw, k, s_dl[k], s_ul[k], ring_s(s), qmask, tix);
+            apply_advert(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops);
           }
         }
       }
@@ -353,31 +324,161 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
         best = view_min<NPL>(st);
         dirty = false;
       }
-      const int k = (int)(best & 0xFFFFull);
+      const int k = (int)(best & 0xFFu);
       const int ks = k / kWave, kl = k % kWave;
-      // 3) the chosen node receives the task
-      uint32_t po = 0u;
+
+      // 3) run horizon: earliest advert that could change the decision
+      int64_t e_lane = kNever;
 #pragma unroll
       for (int s = 0; s < NPL; ++s) {
-        if (s == ks && lane == kl) {
-          po = push_task(st[s], k, t, rq, s_dl[k], s_ul[k], s_mips[k], ring_s(s), qmask, A,
-                         tbase + c0 + j, tix);
+        const int j = s * kWave + lane;
+        // only nodes whose key can drop below best (busy >= 0) matter
+        const bool rel = j < N && j != k && (uint32_t)j < best && pending(st[s]) >= 1u && st[s].nxt < t_last;
+        if (ballot(rel)) {
+          const u32x4 nhw = read_nh(st[s], rel && pending(st[s]) >= 2u, ops);
+          if (rel) {
+            const int64_t h = horizon(st[s], nhw, j, best, t_last, s_tlC[j], s_dl[j], s_ul[j], ring_s(s), qmask);
+            e_lane = h < e_lane ? h : e_lane;
+          }
         }
       }
-      const uint32_t pr = readlane_u32(po, kl);
-      if ((pr >> 24) != 0u) {
-        err = pr >> 24;
+      int64_t E = (int64_t)wave_min_u64((uint64_t)e_lane);  // all candidates are >= 0
+
+      // node k: parameters and tail state (uniform)
+      const int64_t dl_k = s_dl[k], ul_k = s_ul[k];
+      const int32_t mips_k = s_mips[k];
+      const uint32_t tlC_k = s_tlC[k], tlS_k = s_tlS[k];
+      const int64_t tld_k = s_tld[k];
+      uint32_t cnt_k = 0u;
+      int64_t nxt_k = 0;
+#pragma unroll
+      for (int s = 0; s < NPL; ++s) {
+        if (s == ks) {
+          cnt_k = readlane_u32(st[s].cnt, kl);
+          nxt_k = readlane_i64(st[s].nxt, kl);
+        }
+      }
+      const uint32_t pend_k = ((cnt_k & 0xFFFFu) - (cnt_k >> 16)) & 0xFFFFu;
+      if (pend_k > 0u) {
+        E = nxt_k < E ? nxt_k : E;  // k's own next advert changes its key
+      } else {
+        // the run's first task becomes k's head: its advert ends the run
+        const uint32_t s_p = (uint32_t)readlane_u32((uint32_t)cr, jp) / (uint32_t)mips_k;
+        const int64_t a_p = t_p + dl_k;
+        const int64_t done_p = (a_p > tld_k ? a_p : tld_k) + (int64_t)(s_p & 0xFFFFu) * kTicksPerSecond;
+        const int64_t x_p = done_p + ul_k;
+        E = x_p < E ? x_p : E;
+      }
+
+      // 4) the run: publishes jp .. jq-1 with tick <= E all go to node k
+      const bool in_run = (lane >= jp && lane < cnt && ca <= E) || lane == jp;
+      const uint64_t run_mask = ballot(in_run);
+      const int L = __popcll(run_mask);
+      const int jq = jp + L;
+
+      // 5) FIFO recurrence over the run: done_m = max(a_m, done_{m-1}) + S_m,
+      //    as an inclusive scan of g_m(x) = max(x + D, A) (D = S_m 1e12,
+      //    A = a_m + D); non-run lanes carry the identity (0, -inf).
+      uint32_t S = 0u;
+      int64_t a = 0, dd = 0;
+      bool lerr = false;
+      if (in_run) {
+        S = (uint32_t)cr / (uint32_t)mips_k;  // double tskTime = requiredMIPS / MIPS (:276)
+        a = ca + dl_k;
+        dd = (int64_t)S * kTicksPerSecond;
+        lerr = S > A.max_s || a > kMaxTick;
+      }
+      int64_t D = in_run ? dd : 0, Ac = in_run ? a + dd : INT64_MIN;
+      uint32_t Cs = S;
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) {
+        const int64_t De = shfl_up_i64(D, off);
+        const int64_t Ae = shfl_up_i64(Ac, off);
+        const uint32_t Ce = (uint32_t)__shfl_up((int)Cs, off);
+        if (lane >= off) {
+          const int64_t aa = Ae + D;
+          Ac = aa > Ac ? aa : Ac;
+          D = De + D;
+          Cs = Ce + Cs;
+        }
+      }
+      const int64_t base_done = tld_k;  // INT64_MIN when k never ran a task
+      const int64_t via = base_done + D;
+      const int64_t done = via > Ac ? via : Ac;
+      // previous task on node k: the run's previous lane, or k's tail
+      const int64_t done_up = shfl_up_i64(done, 1);
+      const uint32_t S_up = (uint32_t)__shfl_up((int)S, 1);
+      const int64_t prev_done = lane == jp ? base_done : done_up;
+      const uint32_t prev_S = lane == jp ? tlS_k : S_up;
+      uint32_t status;
+      if (prev_done < a) {
+        status = 5u;  // idle: "task assigned" (:282-301)
+      } else if (prev_done > a) {
+        status = 4u;  // busy: "task queued" (:304-313)
+      } else {        // completion of the previous task at the same tick
+        status = (dl_k < (int64_t)prev_S * kTicksPerSecond) ? 5u : 4u;
+      }
+      const int64_t start = done - dd;
+      lerr = lerr || (in_run && done > kMaxTick);
+      if (ballot(lerr)) {
+        err = FOGNET_ERR_ARG;
         break;
       }
-      const uint32_t pend = pr & 0xFFFFFFu;
-      max_pend = pend > max_pend ? pend : max_pend;
-      if (pend == 2u) {  // the new entry became head+1 of node k
-#pragma unroll
-        for (int s = 0; s < NPL; ++s)
-          if (s == ks) refill_slot(st[s], ring_s(s), qmask);
+      if (pend_k + (uint32_t)L - 1u > qmask) {
+        err = FOGNET_ERR_CAPACITY;
+        break;
       }
+      // ring entries (consecutive slots of node k's ring) and per-task outputs
+      RingEntry* const ring_k = ring_r + ((size_t)k << q_log2);
+      if (in_run) {
+        RingEntry e;
+        e.a = a;
+        e.C = tlC_k + Cs;
+        e.S = S;
+        ring_k[((cnt_k & 0xFFFFu) + (uint32_t)(lane - jp)) & qmask] = e;
+        const size_t o = tbase + c0 + lane;
+        A.out_node[o] = k;
+        A.out_status[o] = (uint8_t)status;
+        A.out_start[o] = start;
+        A.out_done[o] = done;
+      }
+      ops += 5u;
+
+      // 6) node k's state after the run
+      const int lz = jq - 1;
+      const int64_t a_z = readlane_i64(a, lz), done_z = readlane_i64(done, lz);
+      const uint32_t C_z = readlane_u32(tlC_k + Cs, lz), S_z = readlane_u32(S, lz);
+      const int64_t done_f = readlane_i64(done, jp);
+      const uint32_t C_f = readlane_u32(tlC_k + Cs, jp), S_f = readlane_u32(S, jp);
+#pragma unroll
+      for (int s = 0; s < NPL; ++s) {
+        if (s == ks) {
+          if (lane == kl) {
+            if (pend_k == 0u) {
+              st[s].hd_done = done_f;
+              st[s].hd_C = C_f;
+              st[s].hd_S = (st[s].hd_S & 0xFF000000u) | S_f;
+              st[s].nxt = done_f + ul_k;
+            }
+            st[s].tl_a = a_z;
+            s_tld[k] = done_z;
+            s_tlC[k] = C_z;
+            s_tlS[k] = S_z;
+            st[s].cnt = (cnt_k & 0xFFFF0000u) | ((cnt_k + (uint32_t)L) & 0xFFFFu);
+          }
+          // k's head+1 changed: reload it (whole slot, uniform control flow)
+          if ((pend_k == 0u && L >= 2) || pend_k == 1u) {
+            refill_slot(st[s], ring_s(s), qmask);
+            ops += 1u;
+            if (lane == kl) stamp_prefetch(st[s], ops);  // stamp counts the refill itself
+          }
+        }
+      }
+      const uint32_t pend_after = pend_k + (uint32_t)L;
+      max_pend = pend_after > max_pend ? pend_after : max_pend;
+      n_done += L;
+      jp = jq;
     }
-    n_done += j;
   }
   // drain the inline-asm prefetches before the wave retires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
