@@ -115,15 +115,24 @@ __device__ __forceinline__ u32x4 read_nh(const Slot& st, bool need, uint32_t ops
   return nh_read_8(st.nh);
 }
 
-// Reload nh of every lane in a slot from its node's current head+1 ring entry,
-// issued by all lanes in uniform control flow (an asm load inside a divergent
+// Reload nh of one lane (its node's current head+1 ring entry).  The asm
+// statement is executed in uniform control flow (a load inside a divergent
 // branch gets a temporary that the compiler copies back before the data
-// lands).  For a lane whose head+1 did not change this is a duplicate of the
-// same address, harmless under in-order returns, so its stamp is left alone.
+// lands) and narrows EXEC to that lane itself, so one cache line is fetched.
 // Ring stores issued earlier by this wave (any lane) precede it in the same
 // in-order memory pipeline, so it observes them.
-__device__ __forceinline__ void refill_slot(Slot& st, const RingEntry* ring, uint32_t qmask) {
-  prefetch_entry(st.nh, ring + ((n_head(st) + 1u) & qmask));
+__device__ __forceinline__ void refill_lane(Slot& st, const RingEntry* ring, uint32_t qmask, int lane) {
+  const RingEntry* p = ring + ((n_head(st) + 1u) & qmask);
+  const uint64_t only = 1ull << lane;
+  uint64_t saved;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, %3\n\t"
+      "global_load_dwordx4 %0, %2, off\n\t"
+      "s_mov_b64 exec, %1"
+      : "+v"(st.nh), "=&s"(saved)
+      : "v"(p), "s"(only)
+      : "memory");
 }
 
 // arrival at tick `a` happens before the completion at `done` of a task with
@@ -291,6 +300,7 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
     const bool live = lane < cnt;
     const int64_t ca = live ? A.arrive[tbase + c0 + lane] : kNever;
     const int32_t cr = live ? A.req[tbase + c0 + lane] : 0;
+    ops += 2u;  // the two chunk loads (lane 0 is always live)
     // trace preconditions: nondecreasing ticks, requirement >= 0, ticks < 2^61
     const int64_t up = shfl_up_i64(ca, 1);
     const int64_t prv = lane == 0 ? prev_t : up;
@@ -313,6 +323,9 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
           if (!ballot(due)) break;
           dirty = true;
           const u32x4 nhw = read_nh(st[s], due && pending(st[s]) >= 2u, ops);
+          // apply_advert prefetches head+2 where >= 3 are pending: tally it
+          // first, so the stamp already counts the load itself
+          if (ballot(due && pending(st[s]) >= 3u)) ops += 1u;
           if (due) {
             const int k = s * kWave + lane;
             apply_advert(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops);
@@ -466,9 +479,9 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
             s_tlS[k] = S_z;
             st[s].cnt = (cnt_k & 0xFFFF0000u) | ((cnt_k + (uint32_t)L) & 0xFFFFu);
           }
-          // k's head+1 changed: reload it (whole slot, uniform control flow)
+          // k's head+1 changed: reload it (uniform control flow, one lane)
           if ((pend_k == 0u && L >= 2) || pend_k == 1u) {
-            refill_slot(st[s], ring_s(s), qmask);
+            refill_lane(st[s], ring_s(s), qmask, kl);
             ops += 1u;
             if (lane == kl) stamp_prefetch(st[s], ops);  // stamp counts the refill itself
           }

@@ -1,0 +1,47 @@
+"""Summarise rocprofv3 PMC passes (gpurun_out/pmc/p*/) for one kernel:
+totals per counter, per-dispatch averages, derived per-decision figures and
+HBM traffic (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, + WRITE_SIZE,
+in KiB units from rocprofv3)."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def load(root="gpurun_out/pmc", kernel="replay_kernel"):
+    agg = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
+    for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
+        for row in csv.DictReader(open(f)):
+            if kernel in row["Kernel_Name"]:
+                agg[row["Counter_Name"]] += float(row["Counter_Value"])
+                disp[row["Counter_Name"]].add((f, row["Dispatch_Id"]))
+    return {k: (v, len(disp[k])) for k, v in agg.items()}
+
+
+def main():
+    kernel = sys.argv[1] if len(sys.argv) > 1 else "replay_kernel"
+    decisions = float(sys.argv[2]) if len(sys.argv) > 2 else 4096 * 100000
+    d = load(kernel=kernel)
+    per = {k: v / n for k, (v, n) in d.items()}
+    out = {"kernel": kernel, "per_dispatch": per}
+    if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+        fetch = 2 * per["FETCH_SIZE"] * 1024  # gfx950 reports half of a wide stream
+        write = per["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch"] = fetch + write
+        out["hbm_fetch_bytes_corrected"] = fetch
+        out["hbm_write_bytes"] = write
+        out["hbm_bytes_per_decision"] = (fetch + write) / decisions
+    for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
+        if k in per:
+            out[k + "_per_decision"] = per[k] / decisions
+    if "SQ_WAVE_CYCLES" in per:
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if k in per:
+                out[k + "_frac_of_wave_cycles"] = per[k] / per["SQ_WAVE_CYCLES"]
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
