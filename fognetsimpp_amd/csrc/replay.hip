@@ -123,7 +123,7 @@ __device__ __forceinline__ u32x4 read_nh(const Slot& st, bool need, uint32_t ops
 // in-order memory pipeline, so it observes them.
 __device__ __forceinline__ void refill_lane(Slot& st, const RingEntry* ring, uint32_t qmask, int lane) {
   const RingEntry* p = ring + ((n_head(st) + 1u) & qmask);
-  const uint64_t only = 1ull << lane;
+  const uint64_t only = 1ull << __builtin_amdgcn_readfirstlane(lane);  // lane is wave-uniform
   uint64_t saved;
   asm volatile(
       "s_mov_b64 %1, exec\n\t"
