@@ -30,3 +30,14 @@ clean:
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean asm
+
+# Profile build: replay_kernel writes loop counters into the stats record
+# (tools/replay_counters.py); not used by the product path.
+PROF_LIB := build/prof/libfognet_hip.so
+prof: $(SRCS) $(HDRS)
+	@mkdir -p build/prof
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DFOGNET_REPLAY_PROFILE=1 -Iinclude -shared -o $(PROF_LIB) $(SRCS)
+	@mkdir -p build/prof2
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DFOGNET_REPLAY_PROFILE=2 -Iinclude -shared -o build/prof2/libfognet_hip.so $(SRCS)
+
+.PHONY: prof

@@ -43,6 +43,26 @@ __device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// DPP move that leaves `old` where the source lane is invalid or the row is
+// masked off (bound_ctrl off): shifts with a fill value and the row
+// broadcasts of a wave scan.
+//   row_shr:n 0x110+n (within rows of 16)   wave_shr:1 0x138 (whole wave)
+//   row_bcast:15 0x142 (lane 15 of each row -> next row; rows 1,3: mask 0xA)
+//   row_bcast:31 0x143 (lane 31 -> rows 2,3: mask 0xC)
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp_or_u32(uint32_t old, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, kCtrl, kRowMask, 0xF, false);
+}
+
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ int64_t dpp_or_i64(int64_t old, int64_t v) {
+  const uint32_t lo = dpp_or_u32<kCtrl, kRowMask>((uint32_t)(uint64_t)old, (uint32_t)(uint64_t)v);
+  const uint32_t hi = dpp_or_u32<kCtrl, kRowMask>((uint32_t)((uint64_t)old >> 32), (uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+constexpr int kDppWaveShr1 = 0x138;
+
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return b < a ? b : a; }
 
 // Minimum of a u64 over the 64 lanes; result is wave-uniform.  Must be called

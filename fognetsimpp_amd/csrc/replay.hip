@@ -50,6 +50,25 @@ struct Slot {
                      // completion adverts applied (bits 16-31); capacity <= 2^15
 };
 
+// Profile builds (`make prof`, tools/replay_counters.py) only:
+// FOGNET_REPLAY_PROFILE=1 counts loop events, =2 accumulates s_memtime cycles
+// per loop segment; either is written into the stats record.
+#if FOGNET_REPLAY_PROFILE == 1
+#define PROF(x) x
+#else
+#define PROF(x)
+#endif
+#if FOGNET_REPLAY_PROFILE == 2
+#define TMARK(i)                                            \
+  {                                                         \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
+    p_t[i] += now_ - p_last;                                \
+    p_last = now_;                                          \
+  }
+#else
+#define TMARK(i)
+#endif
+
 constexpr uint32_t kNoKey = ~0u;
 constexpr int64_t kNever = INT64_MAX;
 // Simulated ticks are kept below 2^61 (26.7 days) and service times below
@@ -135,6 +154,12 @@ __device__ __forceinline__ void refill_lane(Slot& st, const RingEntry* ring, uin
       : "memory");
 }
 
+// S seconds in ticks: S * 1e12 = (S * 5^12) << 12, one v_mad_u64_u32 + shift.
+__device__ __forceinline__ int64_t ticks_of(uint32_t s) {
+  static_assert(kTicksPerSecond == 244140625ll << 12, "1e12 ticks per second");
+  return (int64_t)(((uint64_t)s * 244140625u) << 12);
+}
+
 // arrival at tick `a` happens before the completion at `done` of a task with
 // service S on a node with downlink latency dl (FES insertion-order rule).
 __device__ __forceinline__ bool arrives_before(int64_t a, int64_t done, int64_t dl, uint32_t S) {
@@ -146,7 +171,7 @@ __device__ __forceinline__ bool arrives_before(int64_t a, int64_t done, int64_t 
 // from the newest assignment.  c_self: cumulative service of that entry.
 __device__ __forceinline__ uint32_t c_arrived(const Slot& st, const u32x4 nhw, int64_t done, uint32_t S,
                                               uint32_t d0, uint32_t c_self, int64_t dl, uint32_t tl_C,
-                                              const RingEntry* ring, uint32_t qmask) {
+                                              const RingEntry* ring, uint32_t qmask, uint32_t& scan) {
   if (arrives_before(st.tl_a, done, dl, S)) return tl_C;
   const uint32_t pend = pending(st);
   // entries head+d for d = pend-2 .. d0+1 (the tail, d = pend-1, did not qualify)
@@ -157,6 +182,7 @@ __device__ __forceinline__ uint32_t c_arrived(const Slot& st, const u32x4 nhw, i
       a = nh_a(nhw);
       C = nhw.z;
     } else {
+      PROF(scan += 1u;)
       const RingEntry e = ring[(n_head(st) + d) & qmask];
       a = e.a;
       C = e.C;
@@ -170,8 +196,8 @@ __device__ __forceinline__ uint32_t c_arrived(const Slot& st, const u32x4 nhw, i
 // view takes busyTime after releaseResource (:232, :254), the head advances
 // and entry head+2 is prefetched.  nhw: st.nh read after its wait.
 __device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, int64_t dl, int64_t ul, uint32_t tl_C,
-                                             const RingEntry* ring, uint32_t qmask, uint32_t ops) {
-  const uint32_t busy = c_arrived(st, nhw, st.hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask) - st.hd_C;
+                                             const RingEntry* ring, uint32_t qmask, uint32_t ops, uint32_t& scan) {
+  const uint32_t busy = c_arrived(st, nhw, st.hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask, scan) - st.hd_C;
   st.vkey = (busy << 8) | (uint32_t)k;  // busy < 2^24 (max_s * ring capacity)
   st.cnt += 0x10000u;
   const uint32_t pend = pending(st);
@@ -198,18 +224,27 @@ __device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, i
 // predecessors do not change the decision the horizon stops at the second.
 // No push reaches j during the run, so the values do not depend on it.
 __device__ __forceinline__ int64_t horizon(const Slot& st, const u32x4 nhw, int j, uint32_t best, int64_t t_last, uint32_t tl_C,
-                                           int64_t dl, int64_t ul, const RingEntry* ring, uint32_t qmask) {
+                                           int64_t dl, int64_t ul, const RingEntry* ring, uint32_t qmask,
+                                           uint32_t& scan) {
   const uint32_t pend = pending(st);
-  const uint32_t v1 = c_arrived(st, nhw, st.hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask) - st.hd_C;
+  const uint32_t v1 = c_arrived(st, nhw, st.hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask, scan) - st.hd_C;
   if (((v1 << 8) | (uint32_t)j) < best) return st.nxt;
   if (pend < 2u) return kNever;
   const int64_t na = nh_a(nhw);
   const int64_t done2 = (na > st.hd_done ? na : st.hd_done) + (int64_t)nhw.w * kTicksPerSecond;
   const int64_t x2 = done2 + ul;
   if (x2 >= t_last) return kNever;
-  const uint32_t v2 = c_arrived(st, nhw, done2, nhw.w, 1u, nhw.z, dl, tl_C, ring, qmask) - nhw.z;
+  const uint32_t v2 = c_arrived(st, nhw, done2, nhw.w, 1u, nhw.z, dl, tl_C, ring, qmask, scan) - nhw.z;
   if (((v2 << 8) | (uint32_t)j) < best) return x2;
-  return pend == 2u ? kNever : x2;
+  if (pend == 2u) return kNever;
+  if (!arrives_before(st.tl_a, done2, dl, nhw.w)) return x2;
+  // Every pending task reached the node before completion 2, so each later
+  // completion m advertises busy_m = tl_C - C_m = v2 - (C_m - C_2): the value
+  // only falls by the service completed since, and completions are at least
+  // that many seconds apart.  Key (b << 8 | j) < best  <=>  b < thr.
+  const uint32_t thr = (best >> 8) + ((uint32_t)j < (best & 0xFFu) ? 1u : 0u);
+  const uint32_t need = min(v2 - thr + 1u, 1u << 21);  // v2 >= thr here; cap keeps the sum < 2^62
+  return x2 + ticks_of(need);
 }
 
 template <int NPL>
@@ -220,10 +255,14 @@ __device__ __forceinline__ uint32_t view_min(const Slot (&st)[NPL]) {
   return wave_min_u32(m);
 }
 
-__device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int off) {
-  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)(uint64_t)v, off);
-  const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)((uint64_t)v >> 32), off);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
+// One level of the run scan: combine with the element kCtrl names on the left.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void run_scan_level(uint32_t& Cs, int64_t& Ac) {
+  const uint32_t Cl = dpp_or_u32<kCtrl, kRowMask>(0u, Cs);
+  const int64_t Al = dpp_or_i64<kCtrl, kRowMask>(INT64_MIN, Ac);
+  const int64_t aa = (int64_t)((uint64_t)Al + (uint64_t)ticks_of(Cs));  // no signed-overflow UB on rejected lanes
+  Ac = aa > Ac ? aa : Ac;
+  Cs = Cl + Cs;
 }
 
 template <int NPL>
@@ -294,6 +333,16 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
   uint32_t max_pend = 0u;
   uint32_t ops = 0u;  // tally of issued vector-memory instructions (see kPrefetchOps)
   int64_t n_done = 0;
+  uint32_t scan = 0u;  // profile builds: ring entries read by c_arrived (per lane)
+#if FOGNET_REPLAY_PROFILE == 2
+  uint64_t p_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t p_start = __builtin_amdgcn_s_memtime();
+  uint64_t p_last = p_start;
+#endif
+#if FOGNET_REPLAY_PROFILE == 1
+  uint64_t p_iter = 0, p_advit = 0, p_adv = 0, p_end_k = 0, p_end_j = 0, p_end_c = 0, p_hz = 0, p_refill = 0, p_w0 = 0, p_rd = 0,
+           p_chunks = 0, p_pk0 = 0;
+#endif
 
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
@@ -301,9 +350,10 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
     const int64_t ca = live ? A.arrive[tbase + c0 + lane] : kNever;
     const int32_t cr = live ? A.req[tbase + c0 + lane] : 0;
     ops += 2u;  // the two chunk loads (lane 0 is always live)
+    PROF(p_chunks++;)
+    TMARK(0)
     // trace preconditions: nondecreasing ticks, requirement >= 0, ticks < 2^61
-    const int64_t up = shfl_up_i64(ca, 1);
-    const int64_t prv = lane == 0 ? prev_t : up;
+    const int64_t prv = dpp_or_i64<kDppWaveShr1>(prev_t, ca);  // lane 0 gets prev_t
     if (ballot(live && (ca < prv || cr < 0 || ca > kMaxTick))) {
       err = FOGNET_ERR_ARG;
       break;
@@ -314,6 +364,7 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
     int jp = 0;
     while (jp < cnt) {
       const int64_t t_p = readlane_i64(ca, jp);
+      PROF(p_iter++;)
 
       // 1) completion adverts that reached the broker strictly before t_p
 #pragma unroll
@@ -322,21 +373,26 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
           const bool due = st[s].nxt < t_p;
           if (!ballot(due)) break;
           dirty = true;
+          PROF(p_advit++; p_adv += __popcll(ballot(due)); p_rd++;
+               if (ballot(due && pending(st[s]) >= 2u && prefetch_recent(st[s], ops))) p_w0++;
+)
           const u32x4 nhw = read_nh(st[s], due && pending(st[s]) >= 2u, ops);
           // apply_advert prefetches head+2 where >= 3 are pending: tally it
           // first, so the stamp already counts the load itself
           if (ballot(due && pending(st[s]) >= 3u)) ops += 1u;
           if (due) {
             const int k = s * kWave + lane;
-            apply_advert(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops);
+            apply_advert(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops, scan);
           }
         }
       }
+      TMARK(1)
       // 2) argmin over the advertised view (ties -> lowest index)
       if (dirty) {
         best = view_min<NPL>(st);
         dirty = false;
       }
+      TMARK(2)
       const int k = (int)(best & 0xFFu);
       const int ks = k / kWave, kl = k % kWave;
 
@@ -348,14 +404,18 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
         // only nodes whose key can drop below best (busy >= 0) matter
         const bool rel = j < N && j != k && (uint32_t)j < best && pending(st[s]) >= 1u && st[s].nxt < t_last;
         if (ballot(rel)) {
+          PROF(p_hz++; p_rd++; if (ballot(rel && pending(st[s]) >= 2u && prefetch_recent(st[s], ops))) p_w0++;
+)
           const u32x4 nhw = read_nh(st[s], rel && pending(st[s]) >= 2u, ops);
           if (rel) {
-            const int64_t h = horizon(st[s], nhw, j, best, t_last, s_tlC[j], s_dl[j], s_ul[j], ring_s(s), qmask);
+            const int64_t h = horizon(st[s], nhw, j, best, t_last, s_tlC[j], s_dl[j], s_ul[j], ring_s(s), qmask, scan);
             e_lane = h < e_lane ? h : e_lane;
           }
         }
       }
       int64_t E = (int64_t)wave_min_u64((uint64_t)e_lane);  // all candidates are >= 0
+      PROF(const int64_t E_other = E;)
+      TMARK(3)
 
       // node k: parameters and tail state (uniform)
       const int64_t dl_k = s_dl[k], ul_k = s_ul[k];
@@ -390,8 +450,11 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
       const int jq = jp + L;
 
       // 5) FIFO recurrence over the run: done_m = max(a_m, done_{m-1}) + S_m,
-      //    as an inclusive scan of g_m(x) = max(x + D, A) (D = S_m 1e12,
-      //    A = a_m + D); non-run lanes carry the identity (0, -inf).
+      //    as an inclusive scan of g_m(x) = max(x + S_m 1e12, A_m) with
+      //    A_m = a_m + S_m 1e12, composed left to right:
+      //    (Cs_l, A_l) then (Cs_r, A_r) = (Cs_l + Cs_r, max(A_l + Cs_r 1e12, A_r)).
+      //    Non-run lanes carry the identity (0, INT64_MIN); DPP row shifts
+      //    and row broadcasts fill invalid sources with it.
       uint32_t S = 0u;
       int64_t a = 0, dd = 0;
       bool lerr = false;
@@ -401,26 +464,20 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
         dd = (int64_t)S * kTicksPerSecond;
         lerr = S > A.max_s || a > kMaxTick;
       }
-      int64_t D = in_run ? dd : 0, Ac = in_run ? a + dd : INT64_MIN;
+      int64_t Ac = in_run ? a + dd : INT64_MIN;
       uint32_t Cs = S;
-#pragma unroll
-      for (int off = 1; off < kWave; off <<= 1) {
-        const int64_t De = shfl_up_i64(D, off);
-        const int64_t Ae = shfl_up_i64(Ac, off);
-        const uint32_t Ce = (uint32_t)__shfl_up((int)Cs, off);
-        if (lane >= off) {
-          const int64_t aa = Ae + D;
-          Ac = aa > Ac ? aa : Ac;
-          D = De + D;
-          Cs = Ce + Cs;
-        }
-      }
+      run_scan_level<0x111, 0xF>(Cs, Ac);  // row_shr:1
+      run_scan_level<0x112, 0xF>(Cs, Ac);  // row_shr:2
+      run_scan_level<0x114, 0xF>(Cs, Ac);  // row_shr:4
+      run_scan_level<0x118, 0xF>(Cs, Ac);  // row_shr:8
+      run_scan_level<0x142, 0xA>(Cs, Ac);  // row_bcast:15
+      run_scan_level<0x143, 0xC>(Cs, Ac);  // row_bcast:31
       const int64_t base_done = tld_k;  // INT64_MIN when k never ran a task
-      const int64_t via = base_done + D;
+      const int64_t via = base_done + ticks_of(Cs);
       const int64_t done = via > Ac ? via : Ac;
       // previous task on node k: the run's previous lane, or k's tail
-      const int64_t done_up = shfl_up_i64(done, 1);
-      const uint32_t S_up = (uint32_t)__shfl_up((int)S, 1);
+      const int64_t done_up = dpp_or_i64<kDppWaveShr1>(0, done);
+      const uint32_t S_up = dpp_or_u32<kDppWaveShr1>(0u, S);
       const int64_t prev_done = lane == jp ? base_done : done_up;
       const uint32_t prev_S = lane == jp ? tlS_k : S_up;
       uint32_t status;
@@ -441,6 +498,7 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
         err = FOGNET_ERR_CAPACITY;
         break;
       }
+      TMARK(4)
       // ring entries (consecutive slots of node k's ring) and per-task outputs
       RingEntry* const ring_k = ring_r + ((size_t)k << q_log2);
       if (in_run) {
@@ -456,6 +514,7 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
         A.out_done[o] = done;
       }
       ops += 5u;
+      TMARK(5)
 
       // 6) node k's state after the run
       const int lz = jq - 1;
@@ -482,6 +541,7 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
           // k's head+1 changed: reload it (uniform control flow, one lane)
           if ((pend_k == 0u && L >= 2) || pend_k == 1u) {
             refill_lane(st[s], ring_s(s), qmask, kl);
+            PROF(p_refill++;)
             ops += 1u;
             if (lane == kl) stamp_prefetch(st[s], ops);  // stamp counts the refill itself
           }
@@ -490,18 +550,53 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
       const uint32_t pend_after = pend_k + (uint32_t)L;
       max_pend = pend_after > max_pend ? pend_after : max_pend;
       n_done += L;
+      TMARK(6)
+      PROF(p_pk0 += pend_k == 0u; if (jq >= cnt) p_end_c++; else if (E == E_other) p_end_j++; else p_end_k++;)
       jp = jq;
     }
   }
   // drain the inline-asm prefetches before the wave retires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+#if FOGNET_REPLAY_PROFILE == 2
+  TMARK(7)
+#endif
+#if FOGNET_REPLAY_PROFILE == 1
+  uint64_t p_scan = 0;
+  for (int l = 0; l < kWave; ++l) p_scan += readlane_u32(scan, l);
+#endif
   if (lane == 0 && A.out_stats) {
     fognet_rep_stats* S = A.out_stats + r;
     S->n_tasks = n_done;
     S->max_pending = (int32_t)max_pend;
     S->status = (int32_t)err;
     S->events = 2 * (int64_t)N + 4 * n_done;
+#if FOGNET_REPLAY_PROFILE == 2
+    S->n_queued = p_t[0];
+    S->n_started = p_t[1];
+    S->last_tick = p_t[2];
+    S->queue_min_ticks = p_t[3];
+    S->queue_max_ticks = p_t[4];
+    S->resp_min_ticks = p_t[5];
+    S->resp_max_ticks = p_t[6];
+    S->queue_sum_lo = p_t[7];
+    S->queue_sum_hi = p_last - p_start;
+#endif
+#if FOGNET_REPLAY_PROFILE == 1
+    S->n_queued = p_iter;
+    S->n_started = p_advit;
+    S->last_tick = p_adv;
+    S->queue_min_ticks = p_scan;
+    S->queue_max_ticks = p_end_k;
+    S->resp_min_ticks = p_hz;
+    S->resp_max_ticks = p_refill;
+    S->queue_sum_lo = p_w0;
+    S->queue_sum_hi = p_rd;
+    S->queue_sq_lo = p_chunks;
+    S->queue_sq_hi = p_end_j;
+    S->resp_sum_hi = p_end_c;
+    S->resp_sum_lo = p_pk0;
+#endif
   }
 }
 
