@@ -39,10 +39,10 @@ namespace {
 struct Slot {
   uint32_t vkey;     // broker view of the node: (advertised busy seconds << 8) | node index
   int64_t nxt;       // tick at which the head's completion advert reaches the broker
-  int64_t hd_done;   // head (oldest pending) task: completion tick
+  // (head completion tick = nxt - ul: the advert leaves the node at completion)
   uint32_t hd_C;     // cumulative service up to and including the head
   uint32_t hd_S;     // head service seconds (bits 0-23) | nh prefetch stamp (bits 24-31)
-  u32x4 nh;          // entry head+1 {a lo, a hi, C, S}; written only by inline asm
+  // (entry head+1 {a lo, a hi, C, S} lives in reserved VGPRs, see nh_prefetch)
   int64_t tl_a;      // tail (newest) task: arrival tick at the node
   // (tail completion tick, cumulative service and service time live in LDS:
   //  s_tld / s_tlC / s_tlS, read at a uniform address when the node is chosen)
@@ -81,77 +81,148 @@ __device__ __forceinline__ uint32_t pending(const Slot& st) { return (n_push(st)
 __device__ __forceinline__ uint32_t head_S(const Slot& st) { return st.hd_S & 0xFFFFFFu; }
 __device__ __forceinline__ int64_t nh_a(u32x4 v) { return (int64_t)(((uint64_t)v.y << 32) | v.x); }
 
-// ---- head+1 prefetch, outside the compiler's wait-count tracking
+// ---- head+1 prefetch, outside the compiler's register allocation
 //
 // The head+1 entry of a node is needed at that node's next advert, typically
 // many publishes later.  A compiler-visible load cannot express that: its
 // loop-carried destination gets a conservative `s_waitcnt vmcnt(0)` at the
 // first read in the next loop iteration (loads and stores share the in-order
-// vmcnt counter, and the count between issue and use is data dependent).  So
-// the prefetch is an inline-asm load into loop-carried registers that only
-// inline asm ever names (tools/check_nh_regs.py audits the ISA), and reads go
-// through nh_read_*, which waits and copies in one asm statement.
+// vmcnt counter, and the count between issue and use is data dependent), and
+// a value the compiler believes is ready may be copied between registers
+// while the load is still in flight.  So the entries live in VGPRs the
+// compiler never allocates: the kernel caps allocation at kNhBase
+// (amdgpu_num_vgpr; on gfx90a+ the attribute counts half the unified
+// register file, so kNhBase / 2) and slot s of every lane owns v[kNhBase + 4s .. +3].  Only
+// inline asm names them: the prefetch loads, and nh_read, which waits and
+// copies them out in one statement (tools/check_nh_regs.py audits the ISA).
 //
 // The wait count comes from a wave-uniform tally `ops` of vector-memory
-// instructions that are certainly issued (the five stores of every push run,
-// the slot refills).  A node's prefetch is stamped with the tally at issue;
-// once kPrefetchOps tallied instructions were issued after it, it is older
-// than the kPrefetchOps youngest and `s_waitcnt vmcnt(kPrefetchOps)` covers
-// it, otherwise the wait is vmcnt(0).  Untallied instructions only make the
+// instructions that are certainly issued (the chunk loads, the five stores of
+// every push run, slot refills and advert prefetches).  A node's prefetch is
+// stamped with the tally including itself; `ops - stamp` tallied
+// instructions were issued after it, so `s_waitcnt vmcnt(ops - stamp)`
+// (capped at kPrefetchOps) covers it.  Untallied instructions only make the
 // real count larger (safe).  The stamp keeps 8 bits; a wrapped stamp can only
-// make an old prefetch look recent.  Vector-memory loads return in issue
-// order on gfx950, so the newest prefetch into a register wins.
+// make an old prefetch look recent.  Vector-memory operations complete in
+// issue order for vmcnt, so the newest prefetch into a register wins.
 constexpr uint32_t kPrefetchOps = 8;
+constexpr int kNhBase = 112;  // v112..v127: 4 slots x {a lo, a hi, C, S}
+static_assert(kNhBase + 4 * kMaxNodesPerLane == 128, "4 waves/SIMD: 128 VGPRs per lane");
 
-__device__ __forceinline__ void prefetch_entry(u32x4& nh, const RingEntry* p) {
-  asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(nh) : "v"(p) : "memory");
-}
-
-#define FOGNET_NH_READ(CNT)                                                                          \
-  __device__ __forceinline__ u32x4 nh_read_##CNT(const u32x4& nh) {                                  \
-    uint32_t x, y, z, w;                                                                             \
-    asm volatile("s_waitcnt vmcnt(" #CNT ")\n\tv_mov_b32 %0, %4\n\tv_mov_b32 %1, %5\n\t"             \
-                 "v_mov_b32 %2, %6\n\tv_mov_b32 %3, %7"                                              \
-                 : "=&v"(x), "=&v"(y), "=&v"(z), "=&v"(w)                                            \
-                 : "v"(nh.x), "v"(nh.y), "v"(nh.z), "v"(nh.w));                                      \
-    return u32x4{x, y, z, w};                                                                        \
+#define FOGNET_NH_SLOT(S, R0, R1, R2, R3, RR)                                                  \
+  __device__ __forceinline__ void nh_prefetch_##S(const RingEntry* p) {                       \
+    asm volatile("global_load_dwordx4 " RR ", %0, off" : : "v"(p) : "memory", R0, R1, R2, R3); \
+  }                                                                                           \
+  /* one lane's load: EXEC narrowed inside the statement (uniform control flow) */           \
+  __device__ __forceinline__ void nh_refill_##S(const RingEntry* p, uint64_t only) {          \
+    uint64_t saved;                                                                           \
+    asm volatile("s_mov_b64 %0, exec\n\t"                                                     \
+                 "s_mov_b64 exec, %2\n\t"                                                     \
+                 "global_load_dwordx4 " RR ", %1, off\n\t"                                    \
+                 "s_mov_b64 exec, %0"                                                         \
+                 : "=&s"(saved)                                                               \
+                 : "v"(p), "s"(only)                                                          \
+                 : "memory", R0, R1, R2, R3);                                                 \
+  }                                                                                           \
+  /* wait until at most m vector-memory instructions are outstanding (s_waitcnt  */          \
+  /* takes an immediate: branch to the right one; m >= 8 -> vmcnt(8)), then copy */          \
+  __device__ __forceinline__ u32x4 nh_read_##S(uint32_t m) {                                  \
+    uint32_t x, y, z, w;                                                                      \
+    asm volatile(                                                                             \
+      "s_cmp_lt_u32 %4, 8\n\t"                                                                 \
+      "s_cbranch_scc1 1f\n\t"                                                                   \
+      "s_waitcnt vmcnt(8)\n\t"                                                                  \
+      "s_branch 9f\n"                                                                           \
+      "1:\n\t"                                                                                  \
+      "s_cmp_lt_u32 %4, 6\n\t"                                                                  \
+      "s_cbranch_scc1 2f\n\t"                                                                   \
+      "s_cmp_eq_u32 %4, 6\n\t"                                                                  \
+      "s_cbranch_scc1 3f\n\t"                                                                   \
+      "s_waitcnt vmcnt(7)\n\t"                                                                  \
+      "s_branch 9f\n"                                                                           \
+      "3:\n\t"                                                                                  \
+      "s_waitcnt vmcnt(6)\n\t"                                                                  \
+      "s_branch 9f\n"                                                                           \
+      "2:\n\t"                                                                                  \
+      "s_cmp_lt_u32 %4, 4\n\t"                                                                  \
+      "s_cbranch_scc1 4f\n\t"                                                                   \
+      "s_cmp_eq_u32 %4, 4\n\t"                                                                  \
+      "s_cbranch_scc1 5f\n\t"                                                                   \
+      "s_waitcnt vmcnt(5)\n\t"                                                                  \
+      "s_branch 9f\n"                                                                           \
+      "5:\n\t"                                                                                  \
+      "s_waitcnt vmcnt(4)\n\t"                                                                  \
+      "s_branch 9f\n"                                                                           \
+      "4:\n\t"                                                                                  \
+      "s_cmp_lt_u32 %4, 2\n\t"                                                                  \
+      "s_cbranch_scc1 6f\n\t"                                                                   \
+      "s_cmp_eq_u32 %4, 2\n\t"                                                                  \
+      "s_cbranch_scc1 7f\n\t"                                                                   \
+      "s_waitcnt vmcnt(3)\n\t"                                                                  \
+      "s_branch 9f\n"                                                                           \
+      "7:\n\t"                                                                                  \
+      "s_waitcnt vmcnt(2)\n\t"                                                                  \
+      "s_branch 9f\n"                                                                           \
+      "6:\n\t"                                                                                  \
+      "s_cmp_eq_u32 %4, 1\n\t"                                                                  \
+      "s_cbranch_scc0 8f\n\t"                                                                   \
+      "s_waitcnt vmcnt(1)\n\t"                                                                  \
+      "s_branch 9f\n"                                                                           \
+      "8:\n\t"                                                                                  \
+      "s_waitcnt vmcnt(0)\n"                                                                    \
+      "9:\n\t"                                                                                  \
+      "v_mov_b32 %0, " R0 "\n\t"                                                                \
+      "v_mov_b32 %1, " R1 "\n\t"                                                                \
+      "v_mov_b32 %2, " R2 "\n\t"                                                                \
+      "v_mov_b32 %3, " R3                                                                       \
+      : "=&v"(x), "=&v"(y), "=&v"(z), "=&v"(w)                                                  \
+      : "s"(m)                                                                                  \
+      : "scc");                                                                                 \
+    return u32x4{x, y, z, w};                                                                 \
   }
-FOGNET_NH_READ(0)
-FOGNET_NH_READ(8)
-#undef FOGNET_NH_READ
-static_assert(kPrefetchOps == 8, "nh_read_8 encodes the count");
+FOGNET_NH_SLOT(0, "v112", "v113", "v114", "v115", "v[112:115]")
+FOGNET_NH_SLOT(1, "v116", "v117", "v118", "v119", "v[116:119]")
+FOGNET_NH_SLOT(2, "v120", "v121", "v122", "v123", "v[120:123]")
+FOGNET_NH_SLOT(3, "v124", "v125", "v126", "v127", "v[124:127]")
+#undef FOGNET_NH_SLOT
+static_assert(kPrefetchOps == 8, "nh_read waits at most for vmcnt(8)");
+
+template <int S>
+__device__ __forceinline__ void nh_prefetch(const RingEntry* p) {
+  if constexpr (S == 0) nh_prefetch_0(p);
+  else if constexpr (S == 1) nh_prefetch_1(p);
+  else if constexpr (S == 2) nh_prefetch_2(p);
+  else nh_prefetch_3(p);
+}
 
 __device__ __forceinline__ void stamp_prefetch(Slot& st, uint32_t ops) {
   st.hd_S = (st.hd_S & 0xFFFFFFu) | (ops << 24);
 }
-__device__ __forceinline__ bool prefetch_recent(const Slot& st, uint32_t ops) {
-  return ((ops - (st.hd_S >> 24)) & 0xFFu) < kPrefetchOps;
-}
 
-// Wave-level read of a slot's nh for the lanes in `need`.
+// Wave-level read of slot S's head+1 entry for the lanes in `need`: waits
+// until the youngest of their prefetches has landed.
+template <int S>
 __device__ __forceinline__ u32x4 read_nh(const Slot& st, bool need, uint32_t ops) {
-  if (ballot(need && prefetch_recent(st, ops))) return nh_read_0(st.nh);
-  return nh_read_8(st.nh);
+  const uint32_t age = need ? ((ops - (st.hd_S >> 24)) & 0xFFu) : 0xFFu;
+  const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane(wave_min_u32(age));
+  if constexpr (S == 0) return nh_read_0(m);
+  else if constexpr (S == 1) return nh_read_1(m);
+  else if constexpr (S == 2) return nh_read_2(m);
+  else return nh_read_3(m);
 }
 
-// Reload nh of one lane (its node's current head+1 ring entry).  The asm
-// statement is executed in uniform control flow (a load inside a divergent
-// branch gets a temporary that the compiler copies back before the data
-// lands) and narrows EXEC to that lane itself, so one cache line is fetched.
-// Ring stores issued earlier by this wave (any lane) precede it in the same
+// Reload the head+1 entry of node (slot s, lane): one cache line.  Ring
+// stores issued earlier by this wave (any lane) precede it in the same
 // in-order memory pipeline, so it observes them.
-__device__ __forceinline__ void refill_lane(Slot& st, const RingEntry* ring, uint32_t qmask, int lane) {
+__device__ __forceinline__ void refill_nh(int s, const Slot& st, const RingEntry* ring, uint32_t qmask, int lane) {
   const RingEntry* p = ring + ((n_head(st) + 1u) & qmask);
   const uint64_t only = 1ull << __builtin_amdgcn_readfirstlane(lane);  // lane is wave-uniform
-  uint64_t saved;
-  asm volatile(
-      "s_mov_b64 %1, exec\n\t"
-      "s_mov_b64 exec, %3\n\t"
-      "global_load_dwordx4 %0, %2, off\n\t"
-      "s_mov_b64 exec, %1"
-      : "+v"(st.nh), "=&s"(saved)
-      : "v"(p), "s"(only)
-      : "memory");
+  switch (__builtin_amdgcn_readfirstlane(s)) {
+    case 0: nh_refill_0(p, only); break;
+    case 1: nh_refill_1(p, only); break;
+    case 2: nh_refill_2(p, only); break;
+    default: nh_refill_3(p, only); break;
+  }
 }
 
 // S seconds in ticks: S * 1e12 = (S * 5^12) << 12, one v_mad_u64_u32 + shift.
@@ -195,9 +266,11 @@ __device__ __forceinline__ uint32_t c_arrived(const Slot& st, const u32x4 nhw, i
 // Apply the advert of the head completion of node k (lane-local): the broker
 // view takes busyTime after releaseResource (:232, :254), the head advances
 // and entry head+2 is prefetched.  nhw: st.nh read after its wait.
+template <int SL>
 __device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, int64_t dl, int64_t ul, uint32_t tl_C,
                                              const RingEntry* ring, uint32_t qmask, uint32_t ops, uint32_t& scan) {
-  const uint32_t busy = c_arrived(st, nhw, st.hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask, scan) - st.hd_C;
+  const int64_t hd_done = st.nxt - ul;
+  const uint32_t busy = c_arrived(st, nhw, hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask, scan) - st.hd_C;
   st.vkey = (busy << 8) | (uint32_t)k;  // busy < 2^24 (max_s * ring capacity)
   st.cnt += 0x10000u;
   const uint32_t pend = pending(st);
@@ -206,45 +279,69 @@ __device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, i
     return;
   }
   const int64_t na = nh_a(nhw);
-  const int64_t start = na > st.hd_done ? na : st.hd_done;
-  st.hd_done = start + (int64_t)nhw.w * kTicksPerSecond;
+  const int64_t start = na > hd_done ? na : hd_done;
+  const int64_t done = start + (int64_t)nhw.w * kTicksPerSecond;
   st.hd_C = nhw.z;
   st.hd_S = (st.hd_S & 0xFF000000u) | nhw.w;
-  st.nxt = st.hd_done + ul;
+  st.nxt = done + ul;
   if (pend >= 2u) {  // the ring holds every pending entry, the tail included
-    prefetch_entry(st.nh, ring + ((n_head(st) + 1u) & qmask));
+    nh_prefetch<SL>(ring + ((n_head(st) + 1u) & qmask));
     stamp_prefetch(st, ops);
   }
 }
 
-// Earliest tick at which an advert of node j (not the current argmin) could
-// change the decision whose key is best, for a window whose last publish is
-// at t_last.  The first two pending completions are evaluated exactly; a
-// third one's arrival is unknown without another ring read, so when its two
-// predecessors do not change the decision the horizon stops at the second.
-// No push reaches j during the run, so the values do not depend on it.
-__device__ __forceinline__ int64_t horizon(const Slot& st, const u32x4 nhw, int j, uint32_t best, int64_t t_last, uint32_t tl_C,
+// Horizons: a lower bound on the tick at which an advert of node j (not the
+// current argmin, key best) can change the decision.  No push reaches j
+// during the run, so they do not depend on it, and every bound holds for any
+// publish tick (a run may continue into the next trace chunk).
+//
+// Key (b << 8 | j) < best  <=>  b < thr.
+__device__ __forceinline__ uint32_t busy_threshold(int j, uint32_t best) {
+  return (best >> 8) + ((uint32_t)j < (best & 0xFFu) ? 1u : 0u);
+}
+
+// Every pending task of j reached it before its head completes (checked by
+// the caller), so completion m advertises busy_m = tl_C - C_m: the value only
+// falls by the service completed since the head, and completions are at
+// least that many seconds apart.  Needs no ring entry.
+__device__ __forceinline__ int64_t horizon_all_in(const Slot& st, int j, uint32_t best, uint32_t tl_C) {
+  const uint32_t v1 = tl_C - st.hd_C;
+  const uint32_t thr = busy_threshold(j, best);
+  if (v1 < thr) return st.nxt;
+  const uint32_t need = min(v1 - thr + 1u, 1u << 21);  // cap keeps the sum < 2^63
+  return st.nxt + ticks_of(need);
+}
+
+// General case: the first two pending completions are evaluated exactly; past
+// them the closed form above applies once the queue has fully arrived,
+// otherwise the horizon stops at the second.
+__device__ __forceinline__ int64_t horizon(const Slot& st, const u32x4 nhw, int j, uint32_t best, uint32_t tl_C,
                                            int64_t dl, int64_t ul, const RingEntry* ring, uint32_t qmask,
                                            uint32_t& scan) {
   const uint32_t pend = pending(st);
-  const uint32_t v1 = c_arrived(st, nhw, st.hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask, scan) - st.hd_C;
+  const int64_t hd_done = st.nxt - ul;
+  const uint32_t v1 = c_arrived(st, nhw, hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask, scan) - st.hd_C;
   if (((v1 << 8) | (uint32_t)j) < best) return st.nxt;
   if (pend < 2u) return kNever;
   const int64_t na = nh_a(nhw);
-  const int64_t done2 = (na > st.hd_done ? na : st.hd_done) + (int64_t)nhw.w * kTicksPerSecond;
+  const int64_t done2 = (na > hd_done ? na : hd_done) + (int64_t)nhw.w * kTicksPerSecond;
   const int64_t x2 = done2 + ul;
-  if (x2 >= t_last) return kNever;
   const uint32_t v2 = c_arrived(st, nhw, done2, nhw.w, 1u, nhw.z, dl, tl_C, ring, qmask, scan) - nhw.z;
   if (((v2 << 8) | (uint32_t)j) < best) return x2;
   if (pend == 2u) return kNever;
   if (!arrives_before(st.tl_a, done2, dl, nhw.w)) return x2;
-  // Every pending task reached the node before completion 2, so each later
-  // completion m advertises busy_m = tl_C - C_m = v2 - (C_m - C_2): the value
-  // only falls by the service completed since, and completions are at least
-  // that many seconds apart.  Key (b << 8 | j) < best  <=>  b < thr.
-  const uint32_t thr = (best >> 8) + ((uint32_t)j < (best & 0xFFu) ? 1u : 0u);
-  const uint32_t need = min(v2 - thr + 1u, 1u << 21);  // v2 >= thr here; cap keeps the sum < 2^62
+  // fully arrived from completion 2 on: busy_m = v2 - (C_m - C_2), v2 >= thr
+  const uint32_t need = min(v2 - busy_threshold(j, best) + 1u, 1u << 21);
   return x2 + ticks_of(need);
+}
+
+// Compile-time loop over slots (slot-specific inline asm needs a constant).
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
 }
 
 template <int NPL>
@@ -268,7 +365,7 @@ __device__ __forceinline__ void run_scan_level(uint32_t& Cs, int64_t& Ac) {
 template <int NPL>
 // 4 waves per SIMD (<= 128 VGPRs): 16 replications resident per CU, so the
 // 4096-replication sweep runs in a single wave of workgroups on 256 CUs.
-__global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
+__global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))) void replay_kernel(ReplayArgs A) {
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
   __shared__ int64_t s_dl[NPL * kWave];
@@ -305,10 +402,8 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
     // every node's first advert {MIPS, busyTime = 0.0} has reached the broker
     st[s].vkey = k < N ? (uint32_t)k : kNoKey;
     st[s].nxt = kNever;
-    st[s].hd_done = 0;
     st[s].hd_C = 0u;
     st[s].hd_S = 0u;
-    st[s].nh = u32x4{0u, 0u, 0u, 0u};
     st[s].tl_a = 0;
     s_tld[k] = INT64_MIN;
     s_tlC[k] = 0u;
@@ -323,9 +418,17 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
   RingEntry* const ring_r = A.ring + (size_t)r * (size_t)N * ((size_t)qmask + 1u);
   const int q_log2 = A.q_log2;
   // ring of this lane's node in slot s (lanes past N alias node 0: in bounds, never used)
+  // Per-lane addresses are rebuilt at each use from wave-uniform bases and an
+  // opaque lane index: hoisted out of the loops they would pin 64-bit VGPR
+  // pairs for the whole kernel (or spill, and every reload drains vmcnt).
+  auto lane_now = [&]() -> uint32_t {
+    uint32_t l = (uint32_t)lane;
+    asm volatile("" : "+v"(l));
+    return l;
+  };
   auto ring_s = [&](int s) -> RingEntry* {
-    const int k = s * kWave + lane;
-    return ring_r + ((size_t)(k < N ? k : 0) << q_log2);
+    const uint32_t k = (uint32_t)(s * kWave) + lane_now();
+    return ring_r + ((size_t)(k < (uint32_t)N ? k : 0u) << q_log2);
   };
   uint32_t best = view_min<NPL>(st);
   bool dirty = false;
@@ -341,8 +444,13 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
 #endif
 #if FOGNET_REPLAY_PROFILE == 1
   uint64_t p_iter = 0, p_advit = 0, p_adv = 0, p_end_k = 0, p_end_j = 0, p_end_c = 0, p_hz = 0, p_refill = 0, p_w0 = 0, p_rd = 0,
-           p_chunks = 0, p_pk0 = 0;
+           p_chunks = 0, p_pk0 = 0, p_resume = 0;
+  auto young = [&](const Slot& x, bool need) { return ballot(need && ((ops - (x.hd_S >> 24)) & 0xFFu) < 2u) != 0; };
 #endif
+  // A run that consumed the rest of its chunk continues into the next one
+  // while the publishes stay within its horizon E_carry (argmin unchanged).
+  bool carry = false;
+  int64_t E_carry = 0;
 
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
@@ -359,61 +467,77 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
       break;
     }
     prev_t = readlane_i64(ca, cnt - 1);
-    const int64_t t_last = prev_t;
+    const int64_t t_last = prev_t;  // only picks which horizons are evaluated exactly
 
     int jp = 0;
     while (jp < cnt) {
       const int64_t t_p = readlane_i64(ca, jp);
       PROF(p_iter++;)
-
-      // 1) completion adverts that reached the broker strictly before t_p
-#pragma unroll
-      for (int s = 0; s < NPL; ++s) {
-        for (;;) {
-          const bool due = st[s].nxt < t_p;
-          if (!ballot(due)) break;
-          dirty = true;
-          PROF(p_advit++; p_adv += __popcll(ballot(due)); p_rd++;
-               if (ballot(due && pending(st[s]) >= 2u && prefetch_recent(st[s], ops))) p_w0++;
-)
-          const u32x4 nhw = read_nh(st[s], due && pending(st[s]) >= 2u, ops);
-          // apply_advert prefetches head+2 where >= 3 are pending: tally it
-          // first, so the stamp already counts the load itself
-          if (ballot(due && pending(st[s]) >= 3u)) ops += 1u;
-          if (due) {
-            const int k = s * kWave + lane;
-            apply_advert(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops, scan);
+      const bool resume = carry && t_p <= E_carry;
+      carry = false;
+      int64_t E = E_carry;
+      if (!resume) {
+        // 1) completion adverts that reached the broker strictly before t_p
+        static_for<0, NPL>([&](auto sc) {
+          constexpr int s = decltype(sc)::value;
+          for (;;) {
+            const bool due = st[s].nxt < t_p;
+            if (!ballot(due)) break;
+            dirty = true;
+            PROF(p_advit++; p_adv += __popcll(ballot(due)); p_rd++; p_w0 += young(st[s], due && pending(st[s]) >= 2u);)
+            const u32x4 nhw = read_nh<s>(st[s], due && pending(st[s]) >= 2u, ops);
+            // apply_advert prefetches head+2 where >= 3 are pending: tally it
+            // first, so the stamp already counts the load itself
+            if (ballot(due && pending(st[s]) >= 3u)) ops += 1u;
+            if (due) {
+              const int k = s * kWave + lane;
+              apply_advert<s>(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops, scan);
+            }
           }
+        });
+        TMARK(1)
+        // 2) argmin over the advertised view (ties -> lowest index)
+        if (dirty) {
+          best = view_min<NPL>(st);
+          dirty = false;
         }
+        TMARK(2)
+        const int k = (int)(best & 0xFFu);
+
+        // 3) run horizon: earliest advert that could change the decision.
+        //    Only nodes whose key can drop below best (busy >= 0) matter.
+        int64_t e_lane = kNever;
+        static_for<0, NPL>([&](auto sc) {
+          constexpr int s = decltype(sc)::value;
+          const int j = s * kWave + lane;
+          const bool rel = j < N && j != k && (uint32_t)j < best && pending(st[s]) >= 1u;
+          bool deep = false;
+          if (rel) {
+            const uint32_t tlC_j = s_tlC[j];
+            if (arrives_before(st[s].tl_a, st[s].nxt - s_ul[j], s_dl[j], head_S(st[s]))) {
+              const int64_t h = horizon_all_in(st[s], j, best, tlC_j);
+              e_lane = h < e_lane ? h : e_lane;
+            } else if (st[s].nxt < t_last) {
+              deep = true;
+            } else {
+              e_lane = st[s].nxt < e_lane ? st[s].nxt : e_lane;  // beyond this chunk: its first advert
+            }
+          }
+          if (ballot(deep)) {
+            PROF(p_hz++; p_rd++; p_w0 += young(st[s], deep && pending(st[s]) >= 2u);)
+            const u32x4 nhw = read_nh<s>(st[s], deep && pending(st[s]) >= 2u, ops);
+            if (deep) {
+              const int64_t h = horizon(st[s], nhw, j, best, s_tlC[j], s_dl[j], s_ul[j], ring_s(s), qmask, scan);
+              e_lane = h < e_lane ? h : e_lane;
+            }
+          }
+        });
+        E = (int64_t)wave_min_u64((uint64_t)e_lane);  // all candidates are >= 0
+      } else {
+        PROF(p_resume++;)
       }
-      TMARK(1)
-      // 2) argmin over the advertised view (ties -> lowest index)
-      if (dirty) {
-        best = view_min<NPL>(st);
-        dirty = false;
-      }
-      TMARK(2)
       const int k = (int)(best & 0xFFu);
       const int ks = k / kWave, kl = k % kWave;
-
-      // 3) run horizon: earliest advert that could change the decision
-      int64_t e_lane = kNever;
-#pragma unroll
-      for (int s = 0; s < NPL; ++s) {
-        const int j = s * kWave + lane;
-        // only nodes whose key can drop below best (busy >= 0) matter
-        const bool rel = j < N && j != k && (uint32_t)j < best && pending(st[s]) >= 1u && st[s].nxt < t_last;
-        if (ballot(rel)) {
-          PROF(p_hz++; p_rd++; if (ballot(rel && pending(st[s]) >= 2u && prefetch_recent(st[s], ops))) p_w0++;
-)
-          const u32x4 nhw = read_nh(st[s], rel && pending(st[s]) >= 2u, ops);
-          if (rel) {
-            const int64_t h = horizon(st[s], nhw, j, best, t_last, s_tlC[j], s_dl[j], s_ul[j], ring_s(s), qmask, scan);
-            e_lane = h < e_lane ? h : e_lane;
-          }
-        }
-      }
-      int64_t E = (int64_t)wave_min_u64((uint64_t)e_lane);  // all candidates are >= 0
       PROF(const int64_t E_other = E;)
       TMARK(3)
 
@@ -432,7 +556,9 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
         }
       }
       const uint32_t pend_k = ((cnt_k & 0xFFFFu) - (cnt_k >> 16)) & 0xFFFFu;
-      if (pend_k > 0u) {
+      if (resume) {
+        // E_carry already holds k's own bound
+      } else if (pend_k > 0u) {
         E = nxt_k < E ? nxt_k : E;  // k's own next advert changes its key
       } else {
         // the run's first task becomes k's head: its advert ends the run
@@ -507,11 +633,14 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
         e.C = tlC_k + Cs;
         e.S = S;
         ring_k[((cnt_k & 0xFFFFu) + (uint32_t)(lane - jp)) & qmask] = e;
-        const size_t o = tbase + c0 + lane;
-        A.out_node[o] = k;
-        A.out_status[o] = (uint8_t)status;
-        A.out_start[o] = start;
-        A.out_done[o] = done;
+        // chunk bases are wave-uniform (SGPR) and the lane index a 32-bit
+        // offset, so no per-lane 64-bit addresses stay live across the chunk
+        const size_t o = tbase + (size_t)c0;
+        const uint32_t l = lane_now();
+        (A.out_node + o)[l] = k;
+        (A.out_status + o)[l] = (uint8_t)status;
+        (A.out_start + o)[l] = start;
+        (A.out_done + o)[l] = done;
       }
       ops += 5u;
       TMARK(5)
@@ -527,7 +656,6 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
         if (s == ks) {
           if (lane == kl) {
             if (pend_k == 0u) {
-              st[s].hd_done = done_f;
               st[s].hd_C = C_f;
               st[s].hd_S = (st[s].hd_S & 0xFF000000u) | S_f;
               st[s].nxt = done_f + ul_k;
@@ -540,7 +668,7 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
           }
           // k's head+1 changed: reload it (uniform control flow, one lane)
           if ((pend_k == 0u && L >= 2) || pend_k == 1u) {
-            refill_lane(st[s], ring_s(s), qmask, kl);
+            refill_nh(s, st[s], ring_s(s), qmask, kl);
             PROF(p_refill++;)
             ops += 1u;
             if (lane == kl) stamp_prefetch(st[s], ops);  // stamp counts the refill itself
@@ -550,6 +678,10 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
       const uint32_t pend_after = pend_k + (uint32_t)L;
       max_pend = pend_after > max_pend ? pend_after : max_pend;
       n_done += L;
+      if (jq == cnt) {  // the chunk is used up and E still bounds the decision
+        carry = true;
+        E_carry = E;
+      }
       TMARK(6)
       PROF(p_pk0 += pend_k == 0u; if (jq >= cnt) p_end_c++; else if (E == E_other) p_end_j++; else p_end_k++;)
       jp = jq;
@@ -595,6 +727,7 @@ __global__ __launch_bounds__(64, 4) void replay_kernel(ReplayArgs A) {
     S->queue_sq_lo = p_chunks;
     S->queue_sq_hi = p_end_j;
     S->resp_sum_hi = p_end_c;
+    S->resp_sq_lo = p_resume;
     S->resp_sum_lo = p_pk0;
 #endif
   }

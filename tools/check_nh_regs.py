@@ -1,6 +1,7 @@
-"""Audit the replay kernel ISA: the registers that receive inline-asm prefetch
-loads must be referenced only by inline asm (the prefetch loads and the
-wait+copy reads).  Usage: python tools/check_nh_regs.py build/asm/replay-...-gfx950.s"""
+"""Audit the replay kernel ISA: the reserved registers that receive the
+inline-asm prefetch loads (v112..v127, kNhBase in replay.hip) must be
+referenced only by inline asm (the prefetch loads and the wait+copy reads),
+anywhere in the kernel.  Usage: python tools/check_nh_regs.py build/asm/replay-...-gfx950.s"""
 import re
 import sys
 
@@ -37,14 +38,10 @@ def audit(path, kernel_prefix="_ZN6fognet12_GLOBAL__N_113replay_kernelILi"):
                 in_asm = False
             elif in_asm and ln.startswith("global_load_dwordx4"):
                 nh |= regs_of(ln.split(",")[0])
-        # audit region: from the first loop header to the final drain (the
-        # last inline asm); the zero-initialisation precedes the loop and the
-        # statistics epilogue follows the drain
-        lo = next(i for i, ln in enumerate(body) if "Loop Header" in ln)
-        hi = max(i for i, ln in enumerate(body) if ln.startswith(";;#ASMSTART"))
+        assert nh and min(nh) >= 112, f"prefetch destinations outside the reserved range: {sorted(nh)}"
         bad = []
         in_asm = False
-        for ln in body[lo:hi]:
+        for ln in body:
             if ln.startswith(";;#ASMSTART"):
                 in_asm = True
                 continue
