@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--N", type=int, default=256)
     ap.add_argument("--ring", type=int, default=1024)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0003)
-    ap.add_argument("--cpu-reps", type=int, default=256, help="replications in the CPU-baseline sample")
+    ap.add_argument("--cpu-reps", type=int, default=1024, help="replications in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()

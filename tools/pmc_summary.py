@@ -40,7 +40,15 @@ def main():
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
             if k in per:
                 out[k + "_frac_of_wave_cycles"] = per[k] / per["SQ_WAVE_CYCLES"]
-    print(json.dumps(out, indent=1))
+    # the record bench.py reads (profiles/pmc_traffic.json): C3 default config
+    if "hbm_bytes_per_launch" in out:
+        out["config"] = {"R": 4096, "T": 100000, "N": 256, "ring": 1024}
+        out["replay_hbm_bytes_per_launch"] = out["hbm_bytes_per_launch"]
+    txt = json.dumps(out, indent=1)
+    print(txt)
+    if len(sys.argv) > 3:
+        with open(sys.argv[3], "w") as f:
+            f.write(txt + "\n")
 
 
 if __name__ == "__main__":

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from fognetsimpp_amd import _abi  # noqa: E402
 
-MODE = "time" if "--mode=time" in sys.argv else "count"
+MODE = "time" if ("--mode=time" in sys.argv or " ".join(sys.argv).find("--mode time") >= 0) else "count"
 _abi.LIB_PATH = os.path.join(ROOT, "build", "prof2" if MODE == "time" else "prof", "libfognet_hip.so")
 import fognetsimpp_amd as fa  # noqa: E402
 
