@@ -24,7 +24,11 @@ FOGNET_ERR_CAPACITY = 7
 FOGNET_ERR_UNSUPPORTED = 8
 
 FOGNET_POLICY_REF_V3 = 1
+FOGNET_POLICY_EXT_LAT = 16
 TICKS_PER_SECOND = 10**12
+ABI_VERSION = 2
+HIST_METRICS = 2  # 0 queueTime, 1 response
+HIST_BINS = 64
 
 
 class RepStats(C.Structure):
@@ -38,11 +42,13 @@ class RepStats(C.Structure):
         ("resp_sum_lo", C.c_uint64), ("resp_sum_hi", C.c_uint64),
         ("resp_sq_lo", C.c_uint64), ("resp_sq_hi", C.c_uint64),
         ("events", C.c_int64), ("max_pending", C.c_int32), ("status", C.c_int32),
+        ("busy_s", C.c_int64), ("energy_j", C.c_double),
     ]
 
 
 def _np_dtype(struct):
-    m = {C.c_int64: np.int64, C.c_uint64: np.uint64, C.c_int32: np.int32, C.c_uint32: np.uint32}
+    m = {C.c_int64: np.int64, C.c_uint64: np.uint64, C.c_int32: np.int32, C.c_uint32: np.uint32,
+         C.c_double: np.float64}
     fields = []
     for name, t in struct._fields_:
         if hasattr(t, "_length_"):
@@ -67,6 +73,7 @@ class JobStats(C.Structure):
         ("queue_sum", C.c_uint64 * 3), ("queue_sq", C.c_uint64 * 3),
         ("resp_sum", C.c_uint64 * 3), ("resp_sq", C.c_uint64 * 3),
         ("events", C.c_int64), ("max_pending", C.c_int64),
+        ("busy_s", C.c_int64), ("energy_j", C.c_double),
     ]
 
 
@@ -79,12 +86,14 @@ class BatchIn(C.Structure):
         ("node_stride", C.c_int32), ("ring_capacity", C.c_int32),
         ("arrive_tick", C.c_void_p), ("req_mips", C.c_void_p), ("mips", C.c_void_p),
         ("dl_tick", C.c_void_p), ("ul_tick", C.c_void_p), ("init_adv_tick", C.c_void_p),
+        ("p_busy_w", C.c_void_p), ("p_idle_w", C.c_void_p),
     ]
 
 
 class BatchOut(C.Structure):
     _fields_ = [("node", C.c_void_p), ("status", C.c_void_p), ("start_tick", C.c_void_p),
-                ("done_tick", C.c_void_p), ("stats", C.c_void_p)]
+                ("done_tick", C.c_void_p), ("stats", C.c_void_p), ("node_energy_j", C.c_void_p),
+                ("hist", C.c_void_p)]
 
 
 class GenParams(C.Structure):

@@ -60,7 +60,10 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   if (in->N == 0) return fail(c, FOGNET_ERR_NO_NODES, "N == 0 (BrokerBaseApp3.cc:268 reads brokers[0])");
   if (in->N > fognet::kWave * fognet::kMaxNodesPerLane)
     return fail(c, FOGNET_ERR_UNSUPPORTED, "N > 256 not supported by the register-resident replay kernel");
-  if (in->policy != FOGNET_POLICY_REF_V3) return fail(c, FOGNET_ERR_UNSUPPORTED, "unknown policy");
+  if (in->policy != FOGNET_POLICY_REF_V3 && in->policy != FOGNET_POLICY_EXT_LAT)
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "unknown policy");
+  if ((in->p_busy_w == nullptr) != (in->p_idle_w == nullptr))
+    return fail(c, FOGNET_ERR_ARG, "p_busy_w and p_idle_w must both be given or both be null");
   if (in->node_stride != 0 && in->node_stride != in->N)
     return fail(c, FOGNET_ERR_ARG, "node_stride must be 0 or N");
   int q = in->ring_capacity ? in->ring_capacity : 1024;
@@ -89,6 +92,9 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   a->dl = in->dl_tick;
   a->ul = in->ul_tick;
   a->init = in->init_adv_tick;
+  a->policy = in->policy;
+  a->p_busy = in->p_busy_w;
+  a->p_idle = in->p_idle_w;
   return FOGNET_OK;
 }
 
@@ -213,6 +219,9 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
   a.out_start = out->start_tick;
   a.out_done = out->done_tick;
   a.out_stats = out->stats;
+  a.out_energy = out->node_energy_j;
+  a.hist = out->hist;
+  if (a.out_energy && !a.p_busy) return fail(c, FOGNET_ERR_ARG, "node_energy_j needs the power model (p_busy_w/p_idle_w)");
   hipError_t e = hipSuccess;
   if (which & 1) {
     const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
@@ -250,25 +259,33 @@ int fognet_run_batch(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out*
   if (rc) return rc;
   const size_t R = (size_t)in->R, T = (size_t)in->T, N = (size_t)in->N;
   const size_t NR = in->node_stride ? R : 1;
-  const size_t sizes[] = {R * T * 8, R * T * 4, NR * N * 4, NR * N * 8, NR * N * 8, NR * N * 8,
-                          R * T * 4, R * T * 1, R * T * 8, R * T * 8, R * sizeof(fognet_rep_stats)};
-  const int nbuf = (int)(sizeof sizes / sizeof sizes[0]);
-  void* d[11] = {};
+  const size_t HB = FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(int64_t);
+  const bool pw = in->p_busy_w != nullptr;
+  // inputs 0..7, outputs 8..14
+  const void* hsrc[8] = {in->arrive_tick, in->req_mips, in->mips, in->dl_tick, in->ul_tick, in->init_adv_tick,
+                         in->p_busy_w, in->p_idle_w};
+  const size_t isz[8] = {R * T * 8, R * T * 4, NR * N * 4, NR * N * 8, NR * N * 8, NR * N * 8,
+                         pw ? NR * N * 8 : 0, pw ? NR * N * 8 : 0};
+  void* hdst[7] = {out->node, out->status, out->start_tick, out->done_tick, out->stats, out->node_energy_j,
+                   out->hist};
+  const size_t osz[7] = {R * T * 4, R * T * 1, R * T * 8, R * T * 8, R * sizeof(fognet_rep_stats),
+                         out->node_energy_j ? R * N * 8 : 0, out->hist ? HB : 0};
+  void* d[15] = {};
   auto cleanup = [&]() {
-    for (int i = 0; i < nbuf; ++i)
+    for (int i = 0; i < 15; ++i)
       if (d[i]) (void)hipFree(d[i]);
   };
-  for (int i = 0; i < nbuf; ++i) {
-    hipError_t e = hipMalloc(&d[i], sizes[i] ? sizes[i] : 8);
+  for (int i = 0; i < 15; ++i) {
+    const size_t sz = i < 8 ? isz[i] : osz[i - 8];
+    if (i >= 6 && i < 8 && !pw) continue;
+    if (i >= 13 && !hdst[i - 8]) continue;
+    hipError_t e = hipMalloc(&d[i], sz ? sz : 8);
     if (e != hipSuccess) {
       cleanup();
       return hip_fail(c, e, "hipMalloc batch");
     }
-  }
-  const void* hsrc[6] = {in->arrive_tick, in->req_mips, in->mips, in->dl_tick, in->ul_tick, in->init_adv_tick};
-  for (int i = 0; i < 6; ++i) {
-    if (!sizes[i]) continue;
-    hipError_t e = hipMemcpyAsync(d[i], hsrc[i], sizes[i], hipMemcpyHostToDevice, c->stream);
+    if (i < 8 && sz) e = hipMemcpyAsync(d[i], hsrc[i], sz, hipMemcpyHostToDevice, c->stream);
+    if (i == 14 && e == hipSuccess) e = hipMemcpyAsync(d[i], hdst[6], sz, hipMemcpyHostToDevice, c->stream);
     if (e != hipSuccess) {
       cleanup();
       return hip_fail(c, e, "copy-in");
@@ -281,16 +298,18 @@ int fognet_run_batch(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out*
   din.dl_tick = (const int64_t*)d[3];
   din.ul_tick = (const int64_t*)d[4];
   din.init_adv_tick = (const int64_t*)d[5];
-  fognet_batch_out dout = {(int32_t*)d[6], (uint8_t*)d[7], (int64_t*)d[8], (int64_t*)d[9], (fognet_rep_stats*)d[10]};
+  din.p_busy_w = (const double*)d[6];
+  din.p_idle_w = (const double*)d[7];
+  fognet_batch_out dout = {(int32_t*)d[8], (uint8_t*)d[9], (int64_t*)d[10], (int64_t*)d[11],
+                           (fognet_rep_stats*)d[12], (double*)d[13], (int64_t*)d[14]};
   rc = fognet_run_batch_dev(c, &din, &dout, c->stream);
   if (rc) {
     cleanup();
     return rc;
   }
-  void* hdst[5] = {out->node, out->status, out->start_tick, out->done_tick, out->stats};
-  for (int i = 0; i < 5; ++i) {
-    if (!hdst[i] || !sizes[6 + i]) continue;
-    hipError_t e = hipMemcpyAsync(hdst[i], d[6 + i], sizes[6 + i], hipMemcpyDeviceToHost, c->stream);
+  for (int i = 0; i < 7; ++i) {
+    if (!hdst[i] || !osz[i]) continue;
+    hipError_t e = hipMemcpyAsync(hdst[i], d[8 + i], osz[i], hipMemcpyDeviceToHost, c->stream);
     if (e != hipSuccess) {
       cleanup();
       return hip_fail(c, e, "copy-out");
@@ -350,6 +369,8 @@ void fognet_job_stats_merge(fognet_job_stats* a, const fognet_job_stats* b) {
   if (b->resp_min_ticks < a->resp_min_ticks) a->resp_min_ticks = b->resp_min_ticks;
   if (b->resp_max_ticks > a->resp_max_ticks) a->resp_max_ticks = b->resp_max_ticks;
   if (b->max_pending > a->max_pending) a->max_pending = b->max_pending;
+  a->busy_s += b->busy_s;
+  a->energy_j = a->energy_j + b->energy_j;
   add192_host(a->queue_sum, b->queue_sum);
   add192_host(a->queue_sq, b->queue_sq);
   add192_host(a->resp_sum, b->resp_sum);

@@ -156,6 +156,8 @@ struct ReplayArgs {
   int32_t R, T, N, node_stride;
   int32_t q_log2;  // ring capacity per node = 1 << q_log2
   uint32_t max_s;  // largest admissible service time (keeps busy < 2^32)
+  int32_t policy;  // fognet_policy
+  int32_t pad_;
   const int64_t* arrive;
   const int32_t* req;
   const int32_t* mips;
@@ -168,7 +170,19 @@ struct ReplayArgs {
   int64_t* out_done;
   fognet_rep_stats* out_stats;
   RingEntry* ring;  // [R][N][Q]
+  const double* p_busy;   // [R|1][N] power model (nullable)
+  const double* p_idle;
+  double* out_energy;     // [R][N] (nullable)
+  int64_t* hist;          // [FOGNET_HIST_METRICS][FOGNET_HIST_BINS], added to (nullable)
 };
+
+// FOGNET_HIST_BINS rule (fognet_hip.h): whole milliseconds, log2 bins.
+__device__ __forceinline__ int hist_bin(int64_t ticks) {
+  const uint64_t q = (uint64_t)ticks / 1000000000ull;
+  if (ticks < 0 || q == 0) return 0;
+  const int b = 64 - __clzll((long long)q);
+  return b > FOGNET_HIST_BINS - 1 ? FOGNET_HIST_BINS - 1 : b;
+}
 
 hipError_t launch_replay(const ReplayArgs& a, hipStream_t s);
 hipError_t launch_rep_stats(const ReplayArgs& a, hipStream_t s);

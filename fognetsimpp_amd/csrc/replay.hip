@@ -352,6 +352,37 @@ __device__ __forceinline__ uint32_t view_min(const Slot (&st)[NPL]) {
   return wave_min_u32(m);
 }
 
+// FOGNET_POLICY_EXT_LAT (north-star cost, not in the reference; fognet_hip.h):
+// argmin over j of dl_j + (busy_j + min(req / mips_j, 2^20)) * 1e12 in uint64
+// ticks (dl_j < 2^50 and busy_j < 2^24 keep it below 2^64), ties -> lowest j.
+// The saturation never changes an admissible decision (service <= max_s < 2^16).
+constexpr uint32_t kExtSatS = 1u << 20;
+constexpr int64_t kExtMaxDl = (int64_t)1 << 50;
+
+template <int NPL>
+__device__ __forceinline__ uint32_t ext_argmin(const Slot (&st)[NPL], uint32_t req, const int32_t* s_mips,
+                                               const int64_t* s_dl, int N, int lane) {
+  uint64_t c[NPL];
+  uint64_t m = ~0ull;
+#pragma unroll
+  for (int s = 0; s < NPL; ++s) {
+    const int j = s * kWave + lane;
+    c[s] = ~0ull;
+    if (j < N) {
+      const uint32_t S = min(req / (uint32_t)s_mips[j], kExtSatS);
+      c[s] = (uint64_t)s_dl[j] + (uint64_t)((st[s].vkey >> 8) + S) * (uint64_t)kTicksPerSecond;
+    }
+    m = c[s] < m ? c[s] : m;
+  }
+  m = wave_min_u64(m);
+#pragma unroll
+  for (int s = 0; s < NPL; ++s) {
+    const uint64_t hit = ballot(s * kWave + lane < N && c[s] == m);
+    if (hit) return (uint32_t)(s * kWave + __builtin_ctzll(hit));
+  }
+  return 0u;
+}
+
 // One level of the run scan: combine with the element kCtrl names on the left.
 template <int kCtrl, int kRowMask>
 __device__ __forceinline__ void run_scan_level(uint32_t& Cs, int64_t& Ac) {
@@ -362,10 +393,11 @@ __device__ __forceinline__ void run_scan_level(uint32_t& Cs, int64_t& Ac) {
   Cs = Cl + Cs;
 }
 
-template <int NPL>
+template <int NPL, int POL>
 // 4 waves per SIMD (<= 128 VGPRs): 16 replications resident per CU, so the
 // 4096-replication sweep runs in a single wave of workgroups on 256 CUs.
 __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))) void replay_kernel(ReplayArgs A) {
+  constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
   __shared__ int64_t s_dl[NPL * kWave];
@@ -395,6 +427,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
       u = A.ul[nbase + k];
       const int64_t ia = A.init[nbase + k];
       bad |= (m <= 0) | (d < 0) | (u < 0) | (d > kMaxTick) | (u > kMaxTick) | (ia < u) | (ia >= arrive0);
+      if constexpr (kExt) bad |= d >= kExtMaxDl;
     }
     s_dl[k] = d;
     s_ul[k] = u;
@@ -473,7 +506,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     while (jp < cnt) {
       const int64_t t_p = readlane_i64(ca, jp);
       PROF(p_iter++;)
-      const bool resume = carry && t_p <= E_carry;
+      const bool resume = !kExt && carry && t_p <= E_carry;
       carry = false;
       int64_t E = E_carry;
       if (!resume) {
@@ -496,6 +529,10 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
           }
         });
         TMARK(1)
+        if constexpr (kExt) {
+          // 2') per-publish argmin of the extension cost; every run is one publish
+          best = ext_argmin<NPL>(st, readlane_u32((uint32_t)cr, jp), s_mips, s_dl, N, lane);
+        } else {
         // 2) argmin over the advertised view (ties -> lowest index)
         if (dirty) {
           best = view_min<NPL>(st);
@@ -533,6 +570,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
           }
         });
         E = (int64_t)wave_min_u64((uint64_t)e_lane);  // all candidates are >= 0
+        }  // REF_V3
       } else {
         PROF(p_resume++;)
       }
@@ -570,7 +608,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
       }
 
       // 4) the run: publishes jp .. jq-1 with tick <= E all go to node k
-      const bool in_run = (lane >= jp && lane < cnt && ca <= E) || lane == jp;
+      const bool in_run = kExt ? lane == jp : ((lane >= jp && lane < cnt && ca <= E) || lane == jp);
       const uint64_t run_mask = ballot(in_run);
       const int L = __popcll(run_mask);
       const int jq = jp + L;
@@ -678,7 +716,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
       const uint32_t pend_after = pend_k + (uint32_t)L;
       max_pend = pend_after > max_pend ? pend_after : max_pend;
       n_done += L;
-      if (jq == cnt) {  // the chunk is used up and E still bounds the decision
+      if (!kExt && jq == cnt) {  // the chunk is used up and E still bounds the decision
         carry = true;
         E_carry = E;
       }
@@ -740,7 +778,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
 // summation order.
 
 struct Acc {
-  uint64_t n4, n5;
+  uint64_t n4, n5, busy;
   uint64_t qs_lo, qs_hi, qq_lo, qq_hi, rs_lo, rs_hi, rq_lo, rq_hi;
   int64_t qmin, qmax, rmin, rmax, last;
 };
@@ -760,6 +798,7 @@ __device__ __forceinline__ void add_moment(uint64_t& slo, uint64_t& shi, uint64_
 __device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
   a.n4 += b.n4;
   a.n5 += b.n5;
+  a.busy += b.busy;
   add128(a.qs_lo, a.qs_hi, b.qs_lo, b.qs_hi);
   add128(a.qq_lo, a.qq_hi, b.qq_lo, b.qq_hi);
   add128(a.rs_lo, a.rs_hi, b.rs_lo, b.rs_hi);
@@ -773,13 +812,25 @@ __device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
 
 constexpr int kStatThreads = 256;
 
+// Also the builder-defined statistics of the north star: latency histograms
+// (FOGNET_HIST_BINS, integer counts added into the job histogram) and node
+// energy (fognet_rep_stats.energy_j: per-node service seconds are integers,
+// so only the final per-node products and the index-ordered sum round).
 __global__ __launch_bounds__(kStatThreads) void rep_stats_kernel(ReplayArgs A) {
   const int r = blockIdx.x;
   __shared__ Acc s_acc[kStatThreads];
+  __shared__ unsigned long long s_busy[kWave * kMaxNodesPerLane];  // service seconds per node
+  __shared__ double s_e[kWave * kMaxNodesPerLane];
+  __shared__ uint32_t s_hist[FOGNET_HIST_METRICS * FOGNET_HIST_BINS];
   fognet_rep_stats* S = A.out_stats + r;
   const int32_t n = (int32_t)S->n_tasks;  // written by replay_kernel
   const size_t tbase = (size_t)r * (size_t)A.T;
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
+  const bool energy = A.p_busy != nullptr;
+  const bool hist = A.hist != nullptr;
+  for (int j = threadIdx.x; j < kWave * kMaxNodesPerLane; j += kStatThreads) s_busy[j] = 0ull;
+  for (int h = threadIdx.x; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kStatThreads) s_hist[h] = 0u;
+  __syncthreads();
   Acc a = {};
   a.qmin = a.rmin = INT64_MAX;
   a.qmax = a.rmax = a.last = INT64_MIN;
@@ -790,16 +841,21 @@ __global__ __launch_bounds__(kStatThreads) void rep_stats_kernel(ReplayArgs A) {
     const int64_t st0 = A.out_start[tbase + i];
     const int64_t dn = A.out_done[tbase + i];
     const int64_t resp = dn - t;
+    const uint64_t svc = (uint64_t)(dn - st0) / (uint64_t)kTicksPerSecond;  // whole seconds
+    a.busy += svc;
+    if (energy) atomicAdd(&s_busy[k], (unsigned long long)svc);
     add_moment(a.rs_lo, a.rs_hi, a.rq_lo, a.rq_hi, (uint64_t)resp);
     a.rmin = min(a.rmin, resp);
     a.rmax = max(a.rmax, resp);
     a.last = max(a.last, dn);
+    if (hist) atomicAdd(&s_hist[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
     if (stt == 4) {
       const int64_t q = st0 - (t + A.dl[nbase + k]);
       a.n4 += 1u;
       add_moment(a.qs_lo, a.qs_hi, a.qq_lo, a.qq_hi, (uint64_t)q);
       a.qmin = min(a.qmin, q);
       a.qmax = max(a.qmax, q);
+      if (hist) atomicAdd(&s_hist[hist_bin(q)], 1u);
     } else {
       a.n5 += 1u;
     }
@@ -827,20 +883,53 @@ __global__ __launch_bounds__(kStatThreads) void rep_stats_kernel(ReplayArgs A) {
     S->resp_sum_hi = b.rs_hi;
     S->resp_sq_lo = b.rq_lo;
     S->resp_sq_hi = b.rq_hi;
+    S->busy_s = (int64_t)b.busy;
+    S->energy_j = 0.0;
+  }
+  if (hist) {
+    for (int h = threadIdx.x; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kStatThreads)
+      if (s_hist[h]) atomicAdd((unsigned long long*)&A.hist[h], (unsigned long long)s_hist[h]);
+  }
+  if (energy) {
+    // E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12), IEEE-rounded
+    // products and sums (no contraction), summed in node order by one thread.
+    const int64_t H = n > 0 ? s_acc[0].last : 0;
+    for (int j = threadIdx.x; j < A.N; j += kStatThreads) {
+      const int64_t B = (int64_t)s_busy[j];
+      const double eb = __dmul_rn(A.p_busy[nbase + j], (double)B);
+      const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
+      const double e = __dadd_rn(eb, __dmul_rn(A.p_idle[nbase + j], idle));
+      s_e[j] = e;
+      if (A.out_energy) A.out_energy[(size_t)r * (size_t)A.N + j] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sum = 0.0;
+      for (int j = 0; j < A.N; ++j) sum = __dadd_rn(sum, s_e[j]);
+      S->energy_j = sum;
+    }
   }
 }
 
 }  // namespace
 
-hipError_t launch_replay(const ReplayArgs& a, hipStream_t s) {
+template <int POL>
+void launch_replay_pol(const ReplayArgs& a, hipStream_t s) {
   const int npl = (a.N + kWave - 1) / kWave;
   if (npl <= 1) {
-    hipLaunchKernelGGL(replay_kernel<1>, dim3(a.R), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL((replay_kernel<1, POL>), dim3(a.R), dim3(kWave), 0, s, a);
   } else if (npl == 2) {
-    hipLaunchKernelGGL(replay_kernel<2>, dim3(a.R), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL((replay_kernel<2, POL>), dim3(a.R), dim3(kWave), 0, s, a);
   } else {
-    hipLaunchKernelGGL(replay_kernel<4>, dim3(a.R), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL((replay_kernel<4, POL>), dim3(a.R), dim3(kWave), 0, s, a);
   }
+}
+
+hipError_t launch_replay(const ReplayArgs& a, hipStream_t s) {
+  if (a.policy == FOGNET_POLICY_EXT_LAT)
+    launch_replay_pol<FOGNET_POLICY_EXT_LAT>(a, s);
+  else
+    launch_replay_pol<FOGNET_POLICY_REF_V3>(a, s);
   return hipGetLastError();
 }
 

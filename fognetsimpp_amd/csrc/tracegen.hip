@@ -129,6 +129,8 @@ __device__ __forceinline__ void job_merge(fognet_job_stats& a, const fognet_job_
   a.resp_min_ticks = min(a.resp_min_ticks, b.resp_min_ticks);
   a.resp_max_ticks = max(a.resp_max_ticks, b.resp_max_ticks);
   a.max_pending = max(a.max_pending, b.max_pending);
+  a.busy_s += b.busy_s;
+  a.energy_j = __dadd_rn(a.energy_j, b.energy_j);
   add192(a.queue_sum, b.queue_sum[0], b.queue_sum[1], b.queue_sum[2]);
   add192(a.queue_sq, b.queue_sq[0], b.queue_sq[1], b.queue_sq[2]);
   add192(a.resp_sum, b.resp_sum[0], b.resp_sum[1], b.resp_sum[2]);
@@ -157,6 +159,8 @@ __global__ __launch_bounds__(kRedThreads) void reduce_kernel(const fognet_rep_st
     a.resp_min_ticks = min(a.resp_min_ticks, s.resp_min_ticks);
     a.resp_max_ticks = max(a.resp_max_ticks, s.resp_max_ticks);
     a.max_pending = max(a.max_pending, (int64_t)s.max_pending);
+    a.busy_s += s.busy_s;
+    a.energy_j = __dadd_rn(a.energy_j, s.energy_j);
     add192(a.queue_sum, s.queue_sum_lo, s.queue_sum_hi, 0u);
     add192(a.queue_sq, s.queue_sq_lo, s.queue_sq_hi, 0u);
     add192(a.resp_sum, s.resp_sum_lo, s.resp_sum_hi, 0u);

@@ -25,7 +25,9 @@ from ._abi import FognetError
 _TENSOR_DTYPES = {
     "arrive": torch.int64, "req": torch.int32, "mips": torch.int32,
     "dl": torch.int64, "ul": torch.int64, "init": torch.int64,
+    "p_busy": torch.float64, "p_idle": torch.float64,  # optional power model (a11)
 }
+POLICIES = {"REF_V3": _abi.FOGNET_POLICY_REF_V3, "EXT_LAT": _abi.FOGNET_POLICY_EXT_LAT}
 
 
 def _ptr(t):
@@ -124,18 +126,23 @@ class BatchResult:
     start_tick: torch.Tensor  # [R, T] int64
     done_tick: torch.Tensor   # [R, T] int64
     stats: torch.Tensor       # [R * sizeof(fognet_rep_stats)] uint8 (device)
+    node_energy: torch.Tensor | None = None  # [R, N] float64 (power model only)
+    hist: torch.Tensor | None = None         # [2, 64] int64 job histogram (queueTime, response), added to
 
     def rep_stats(self) -> np.ndarray:
         return self.stats.cpu().numpy().view(_abi.REP_STATS_DTYPE)
 
 
-def allocate_outputs(R: int, T: int, device) -> BatchResult:
+def allocate_outputs(R: int, T: int, device, N: int | None = None, energy: bool = False,
+                     hist: bool = False) -> BatchResult:
     return BatchResult(
         node=torch.empty((R, T), dtype=torch.int32, device=device),
         status=torch.empty((R, T), dtype=torch.uint8, device=device),
         start_tick=torch.empty((R, T), dtype=torch.int64, device=device),
         done_tick=torch.empty((R, T), dtype=torch.int64, device=device),
         stats=torch.zeros(R * _abi.REP_STATS_DTYPE.itemsize, dtype=torch.uint8, device=device),
+        node_energy=torch.zeros((R, N), dtype=torch.float64, device=device) if energy else None,
+        hist=torch.zeros((_abi.HIST_METRICS, _abi.HIST_BINS), dtype=torch.int64, device=device) if hist else None,
     )
 
 
@@ -143,6 +150,8 @@ def as_device_trace(trace: dict, device) -> dict:
     """numpy/torch trace dict -> contiguous device tensors of the ABI dtypes."""
     out = {}
     for k, dt in _TENSOR_DTYPES.items():
+        if k not in trace or trace[k] is None:
+            continue
         v = trace[k]
         t = v if isinstance(v, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(v))
         out[k] = t.to(device=device, dtype=dt).contiguous()
@@ -153,25 +162,30 @@ def as_device_trace(trace: dict, device) -> dict:
 
 
 def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_capacity: int = 0,
-              stream=None, stage: str = "all") -> BatchResult:
+              stream=None, stage: str = "all", policy: str | int = "REF_V3", hist: bool = False) -> BatchResult:
     """Enqueue R trace replays (fognet_run_batch_dev) on the current stream.
 
     ``trace``: device tensors arrive/req [R, T], node params mips/dl/ul/init
-    [R, N] (per replication) or [N] (shared).  ``stage``: "all", "replay"
-    (fognet_replay_dev) or "stats" (fognet_rep_stats_dev).
+    [R, N] (per replication) or [N] (shared), optional power model
+    p_busy/p_idle (W, same shape as mips).  ``stage``: "all", "replay"
+    (fognet_replay_dev) or "stats" (fognet_rep_stats_dev).  ``policy``:
+    "REF_V3" (BrokerBaseApp3) or "EXT_LAT" (north-star cost, not in the
+    reference).  ``hist``: allocate the job histogram when ``out`` is None.
     """
     arrive, req = trace["arrive"], trace["req"]
     R, T = arrive.shape
     mips = trace["mips"]
     N = mips.shape[-1]
     stride = N if mips.dim() == 2 else 0
+    pol = POLICIES[policy] if isinstance(policy, str) else int(policy)
+    energy = trace.get("p_busy") is not None
     if out is None:
-        out = allocate_outputs(R, T, arrive.device)
-    bi = _abi.BatchIn(R, T, N, _abi.FOGNET_POLICY_REF_V3, stride, ring_capacity,
+        out = allocate_outputs(R, T, arrive.device, N=N, energy=energy, hist=hist)
+    bi = _abi.BatchIn(R, T, N, pol, stride, ring_capacity,
                       _ptr(arrive), _ptr(req), _ptr(mips), _ptr(trace["dl"]), _ptr(trace["ul"]),
-                      _ptr(trace["init"]))
+                      _ptr(trace["init"]), _ptr(trace.get("p_busy")), _ptr(trace.get("p_idle")))
     bo = _abi.BatchOut(_ptr(out.node), _ptr(out.status), _ptr(out.start_tick), _ptr(out.done_tick),
-                       _ptr(out.stats))
+                       _ptr(out.stats), _ptr(out.node_energy), _ptr(out.hist))
     s = C.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(arrive.device)
     fn = {"all": ctx._lib.fognet_run_batch_dev, "replay": ctx._lib.fognet_replay_dev,
           "stats": ctx._lib.fognet_rep_stats_dev}[stage]
@@ -223,6 +237,8 @@ def summarize(job) -> dict:
         "response_ms": block(job["n_tasks"], job["resp_sum"], job["resp_sq"], job["resp_min_ticks"],
                              job["resp_max_ticks"]),
         "max_pending": int(job["max_pending"]),
+        "busy_s": int(job["busy_s"]),
+        "energy_j": float(job["energy_j"]),
     }
 
 
@@ -262,3 +278,12 @@ def sweep_params(r_global: np.ndarray, N: int, rho=None, lat_scale=None, req_lo=
           else np.array((1, 10, 100), np.int64)[(r_global // 3) % 3])
     mean_gap = es / (N * rho_r) * _abi.TICKS_PER_SECOND
     return mean_gap, sc
+
+
+def power_model(mips) -> tuple[np.ndarray, np.ndarray]:
+    """Synthetic node power model for the a11 energy statistic (builder-defined;
+    the reference has no fog-node energy model): busy power
+    grows with MIPS, idle power is 35% of it.  Same shape as ``mips``."""
+    m = np.asarray(mips, dtype=np.float64)
+    p_busy = 20.125 + 0.02 * m
+    return p_busy, 0.35 * p_busy

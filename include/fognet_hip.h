@@ -36,8 +36,17 @@
 extern "C" {
 #endif
 
-#define FOGNET_ABI_VERSION 1
+#define FOGNET_ABI_VERSION 2
 #define FOGNET_TICKS_PER_SECOND 1000000000000LL
+
+/* Latency histograms (device-side statistics, summed over replications; the
+ * only data the multi-GPU path all-reduces over RCCL together with energy).
+ * Metric 0 = queueTime (ComputeBrokerApp3.cc:238, queued tasks only),
+ * metric 1 = response (completion tick - publish tick at the broker).
+ * A value of v ticks has q = v / 10^9 whole milliseconds and falls in bin
+ * 0 if q == 0, else min(63, floor(log2 q) + 1): bin b >= 1 holds [2^(b-1), 2^b) ms. */
+#define FOGNET_HIST_METRICS 2
+#define FOGNET_HIST_BINS 64
 
 typedef int64_t fognet_tick;
 typedef struct fognet_ctx fognet_ctx;
@@ -55,8 +64,13 @@ typedef enum fognet_status {
 } fognet_status;
 
 typedef enum fognet_policy {
-    FOGNET_POLICY_REF_V3 = 1 /* BrokerBaseApp3: argmin(busy_j + req / mips_0), int division,
-                                strict '<' (ties -> lowest index), stale advertised view        */
+    FOGNET_POLICY_REF_V3 = 1,   /* BrokerBaseApp3: argmin(busy_j + req / mips_0), int division,
+                                   strict '<' (ties -> lowest index), stale advertised view      */
+    FOGNET_POLICY_EXT_LAT = 16  /* north-star cost, NOT in the reference (parity vs the oracle's
+                                   restatement only): argmin over j of
+                                   dl_j + adv_busy_j * 1e12 + (req / mips_j) * 1e12 ticks
+                                   (int division by the node's OWN MIPS, exact int64 ticks,
+                                   ties -> lowest index); same stale view and node model      */
 } fognet_policy;
 
 /* Per-replication statistics.  Times are kept in exact ticks; 128-bit sums are
@@ -74,6 +88,12 @@ typedef struct fognet_rep_stats {
     int32_t max_pending;      /* max tasks assigned to one node whose completion advert had not
                                  reached the broker yet (ring occupancy)                          */
     int32_t status;           /* fognet_status of this replication                                */
+    int64_t busy_s;           /* sum of service seconds (req / MIPS) over all tasks               */
+    double energy_j;          /* node energy (builder-defined, not in the reference; 0 when no
+                                 power model): sum over j in index order of
+                                 P_busy_j * B_j + P_idle_j * ((H - B_j * 1e12) / 1e12), with
+                                 B_j = node j's service seconds, H = last_tick (0 if no task);
+                                 IEEE fp64, no fused multiply-add                                 */
 } fognet_rep_stats;
 
 /* Job-level statistics: the exact sum of any set of fognet_rep_stats.  Sums
@@ -88,6 +108,9 @@ typedef struct fognet_job_stats {
     uint64_t queue_sum[3], queue_sq[3], resp_sum[3], resp_sq[3];
     int64_t events;
     int64_t max_pending;
+    int64_t busy_s;
+    double energy_j;          /* fp64 sum over replications (fixed tree order on one device;
+                                 across GPUs within 1e-9 relative)                               */
 } fognet_job_stats;
 
 /* R trace replays of T tasks over N fog nodes, SoA, row-major [R][T] / [R|1][N]. */
@@ -103,6 +126,8 @@ typedef struct fognet_batch_in {
     const int64_t *ul_tick;       /* [R|1][N] node -> broker delivery latency (>= 0)               */
     const int64_t *init_adv_tick; /* [R|1][N] arrival of the node's first advert at the broker;
                                      ul <= init_adv < arrive[0] (all adverts land before task 0)  */
+    const double *p_busy_w;       /* [R|1][N] node power while serving, W (nullable: no energy)   */
+    const double *p_idle_w;       /* [R|1][N] node power while idle, W (null iff p_busy_w is)     */
 } fognet_batch_in;
 
 typedef struct fognet_batch_out {
@@ -112,6 +137,9 @@ typedef struct fognet_batch_out {
     int64_t *done_tick;       /* [R][T] completion (RELEASERESOURCE) tick                         */
     fognet_rep_stats *stats;  /* [R] (all five arrays are required; a stats-only mode that skips
                                  the per-task arrays is not implemented yet: ERR_UNSUPPORTED)    */
+    double *node_energy_j;    /* [R][N] per-node energy (nullable; needs the power model)         */
+    int64_t *hist;            /* [FOGNET_HIST_METRICS][FOGNET_HIST_BINS] job histogram, ADDED to
+                                 (the caller zeroes it; nullable)                                 */
 } fognet_batch_out;
 
 /* Synthetic trace recipe, generated on the device.

@@ -100,6 +100,7 @@ typedef struct {
     req_t *q;              /* FIFO `requests` (push_back / erase(begin)) */
     int64_t qh, qn, qcap;
     int64_t pending;       /* assigned by the broker, advert of its completion not yet at broker */
+    int64_t served_s;      /* service seconds of completed tasks (energy model, a11) */
 } node_t;
 
 typedef struct {
@@ -126,6 +127,18 @@ static void acc_moment(uint64_t *sum_lo, uint64_t *sum_hi, uint64_t *sq_lo, uint
     unsigned __int128 sq = (unsigned __int128)(uint64_t)v * (uint64_t)v;
     acc128(sum_lo, sum_hi, (uint64_t)v, 0);
     acc128(sq_lo, sq_hi, (uint64_t)sq, (uint64_t)(sq >> 64));
+}
+
+int orc_hist_bin(int64_t ticks) {
+    /* fognet_hip.h FOGNET_HIST_BINS: whole milliseconds, log2 bins */
+    uint64_t q = (uint64_t)ticks / 1000000000ull;
+    if (ticks < 0 || q == 0) return 0;
+    int b = 64 - __builtin_clzll(q);
+    return b > ORC_HIST_BINS - 1 ? ORC_HIST_BINS - 1 : b;
+}
+
+static void hist_add(sim_t *s, int metric, int64_t ticks) {
+    if (s->out->hist) s->out->hist[metric * ORC_HIST_BINS + orc_hist_bin(ticks)]++;
 }
 
 static int schedule(sim_t *s, ev_t *e) {
@@ -179,12 +192,15 @@ static int node_release(sim_t *s, int32_t k) {
     /* ack status 6 to the broker (:228-233) -- relay only, no decision effect */
     nd->busyTime = nd->busyTime - nd->currentTask.required_time; /* :232 */
     nd->resourceStatus = 0;                                      /* :234 */
+    nd->served_s += (int64_t)nd->currentTask.required_time;
+    s->st.busy_s += (int64_t)nd->currentTask.required_time;
     if (s->out->done_tick) s->out->done_tick[t] = s->now;
     {
         int64_t resp = s->now - s->in->arrive_tick[t];
         acc_moment(&s->st.resp_sum_lo, &s->st.resp_sum_hi, &s->st.resp_sq_lo, &s->st.resp_sq_hi, resp);
         if (resp < s->st.resp_min_ticks) s->st.resp_min_ticks = resp;
         if (resp > s->st.resp_max_ticks) s->st.resp_max_ticks = resp;
+        hist_add(s, 1, resp);
         if (s->now > s->st.last_tick) s->st.last_tick = s->now;
     }
     if (nd->qn > 0) { /* :236-252 */
@@ -195,6 +211,7 @@ static int node_release(sim_t *s, int32_t k) {
         acc_moment(&s->st.queue_sum_lo, &s->st.queue_sum_hi, &s->st.queue_sq_lo, &s->st.queue_sq_hi, qt);
         if (qt < s->st.queue_min_ticks) s->st.queue_min_ticks = qt;
         if (qt > s->st.queue_max_ticks) s->st.queue_max_ticks = qt;
+        hist_add(s, 0, qt);
         nd->currentTask = *h; /* :240-244 */
         nd->qh = (nd->qh + 1) % nd->qcap; /* requests.erase(begin) (:246) */
         nd->qn--;
@@ -265,12 +282,39 @@ int orc_decide_v3(int32_t n, const double *adv_busy, const int32_t *adv_mips, in
     return ORC_OK;
 }
 
+int orc_decide_ext_lat(int32_t n, const double *adv_busy, const int32_t *mips, const int64_t *dl, int32_t req,
+                       int32_t *out_node) {
+    /* Extension policy (BASELINE.json north_star cost; NOT in the reference): network
+     * delay + advertised backlog + service time at the node's own MIPS, in exact uint64
+     * ticks: dl_j + (busy_j + min(req / mips_j, 2^20)) * 1e12, ties -> lowest j. */
+    if (n <= 0) return ORC_ERR_NO_NODES;
+    int32_t best = -1;
+    uint64_t best_c = 0;
+    for (int32_t j = 0; j < n; j++) {
+        if (mips[j] <= 0) return ORC_ERR_DIV0;
+        if (dl[j] < 0 || dl[j] >= (1LL << 50)) return ORC_ERR_ARG; /* keeps the cost below 2^64 */
+        uint64_t s = (uint64_t)(req / mips[j]);
+        if (s > (1u << 20)) s = 1u << 20; /* saturation (fognet_hip.h), never decisive for admissible tasks */
+        uint64_t c = (uint64_t)dl[j] + ((uint64_t)adv_busy[j] + s) * (uint64_t)TICKS_PER_SECOND;
+        if (best < 0 || c < best_c) {
+            best_c = c;
+            best = j;
+        }
+    }
+    *out_node = best;
+    return ORC_OK;
+}
+
 /* BrokerBaseApp3::handleMessageWhenUp, MqttMsgPublish branch (:138-158) + sendPubAck(false). */
 static int broker_publish(sim_t *s, int64_t t) {
     /* QoS==1 in every trace publish; the status-4 pubAck to the user (:145-150) and the
      * `delay` emit (:143) do not influence the decision. */
     int32_t k;
-    int rc = orc_decide_v3(s->in->n_nodes, s->adv_busy, s->adv_mips, s->in->req_mips[t], &k);
+    int rc;
+    if (s->in->policy == ORC_POLICY_EXT_LAT)
+        rc = orc_decide_ext_lat(s->in->n_nodes, s->adv_busy, s->in->mips, s->in->dl_tick, s->in->req_mips[t], &k);
+    else
+        rc = orc_decide_v3(s->in->n_nodes, s->adv_busy, s->adv_mips, s->in->req_mips[t], &k);
     if (rc) return rc;
     if (s->out->node) s->out->node[t] = k;
     s->st.n_tasks++;
@@ -417,6 +461,20 @@ int orc_run_rep(const orc_rep_in *in, orc_rep_out *out) {
     }
     if (out->final_view_busy)
         for (int32_t k = 0; k < N; k++) out->final_view_busy[k] = s.adv_busy[k];
+    if (in->p_busy_w && in->p_idle_w) {
+        /* a11 energy (builder-defined, fognet_hip.h fognet_rep_stats.energy_j) */
+        int64_t H = s.st.n_tasks > 0 ? s.st.last_tick : 0;
+        double e_sum = 0.0;
+        for (int32_t k = 0; k < N; k++) {
+            double eb = in->p_busy_w[k] * (double)s.nodes[k].served_s;
+            double idle = (double)(H - s.nodes[k].served_s * TICKS_PER_SECOND) / 1e12;
+            double ei = in->p_idle_w[k] * idle;
+            double e = eb + ei;
+            if (out->node_energy_j) out->node_energy_j[k] = e;
+            e_sum = e_sum + e;
+        }
+        s.st.energy_j = e_sum;
+    }
 done:
     s.st.status = rc;
     if (out->stats) *out->stats = s.st;
@@ -432,15 +490,18 @@ done:
 /* ---------------------------------------------------------------- batch driver */
 
 typedef struct {
-    int32_t R, N, node_stride;
+    int32_t R, N, node_stride, policy;
     int64_t T;
     const int64_t *arrive_tick;
     const int32_t *req_mips, *mips;
     const int64_t *dl, *ul, *init_adv;
+    const double *p_busy, *p_idle;
     int32_t *node;
     uint8_t *status;
     int64_t *start_tick, *done_tick;
     orc_rep_stats *stats;
+    double *node_energy;
+    int64_t *hist;
     int64_t next; /* work counter */
     pthread_mutex_t mu;
 } batch_t;
@@ -454,10 +515,13 @@ static void *batch_worker(void *arg) {
         if (r >= b->R) break;
         size_t to = (size_t)r * (size_t)b->T, no = (size_t)r * (size_t)b->node_stride;
         orc_rep_in in = {b->N, b->T, b->arrive_tick + to, b->req_mips + to, b->mips + no,
-                         b->dl + no, b->ul + no, b->init_adv + no};
+                         b->dl + no, b->ul + no, b->init_adv + no,
+                         b->p_busy ? b->p_busy + no : 0, b->p_idle ? b->p_idle + no : 0, b->policy};
         orc_rep_out out = {b->node ? b->node + to : 0, b->status ? b->status + to : 0,
                            b->start_tick ? b->start_tick + to : 0, b->done_tick ? b->done_tick + to : 0,
-                           0, b->stats ? b->stats + r : 0};
+                           0, b->stats ? b->stats + r : 0,
+                           b->node_energy ? b->node_energy + (size_t)r * (size_t)b->N : 0,
+                           b->hist ? b->hist + (size_t)r * ORC_HIST_METRICS * ORC_HIST_BINS : 0};
         orc_run_rep(&in, &out);
     }
     return 0;
@@ -468,8 +532,18 @@ int orc_run_batch(int32_t R, int64_t T, int32_t N, int32_t node_stride,
                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
                   orc_rep_stats *stats, int threads) {
-    batch_t b = {R, N, node_stride, T, arrive_tick, req_mips, mips, dl, ul, init_adv,
-                 node, status, start_tick, done_tick, stats, 0};
+    return orc_run_batch2(R, T, N, node_stride, ORC_POLICY_REF_V3, arrive_tick, req_mips, mips, dl, ul, init_adv,
+                          0, 0, node, status, start_tick, done_tick, stats, 0, 0, threads);
+}
+
+int orc_run_batch2(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
+                   const int64_t *arrive_tick, const int32_t *req_mips,
+                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                   const double *p_busy_w, const double *p_idle_w,
+                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                   orc_rep_stats *stats, double *node_energy_j, int64_t *hist, int threads) {
+    batch_t b = {R, N, node_stride, policy, T, arrive_tick, req_mips, mips, dl, ul, init_adv, p_busy_w, p_idle_w,
+                 node, status, start_tick, done_tick, stats, node_energy_j, hist, 0};
     pthread_mutex_init(&b.mu, 0);
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;

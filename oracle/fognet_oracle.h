@@ -29,8 +29,19 @@ enum {
     ORC_ERR_NO_NODES = 2, /* BrokerBaseApp3.cc:268 reads brokers[0] before the size check (UB) */
     ORC_ERR_DIV0 = 3,     /* BrokerBaseApp3.cc:268 / ComputeBrokerApp3.cc:276 int division by MIPS 0 (SIGFPE) */
     ORC_ERR_STATE = 4,    /* ComputeBrokerApp3.cc:301 scheduleAt() on a pending selfMsg (cRuntimeError) */
-    ORC_ERR_OOM = 6
+    ORC_ERR_OOM = 6,
+    ORC_ERR_UNSUPPORTED = 8
 };
+
+/* Broker allocation policies (values mirror include/fognet_hip.h). */
+enum {
+    ORC_POLICY_REF_V3 = 1,  /* BrokerBaseApp3::sendPubAck, BrokerBaseApp3.cc:265-281            */
+    ORC_POLICY_EXT_LAT = 16 /* north-star cost (not in the reference): dl_j + busy_j + req/mips_j */
+};
+
+/* Histograms (fognet_hip.h FOGNET_HIST_*): metric 0 queueTime, 1 response. */
+#define ORC_HIST_METRICS 2
+#define ORC_HIST_BINS 64
 
 /* One replication: a pre-generated trace replayed through the broker/node handlers. */
 typedef struct {
@@ -42,6 +53,9 @@ typedef struct {
     const int64_t *dl_tick;       /* [N] broker -> node delivery latency, ticks        */
     const int64_t *ul_tick;       /* [N] node -> broker delivery latency, ticks        */
     const int64_t *init_adv_tick; /* [N] arrival tick of node's first advertisement    */
+    const double *p_busy_w;       /* [N] power while serving, W (nullable: no energy)  */
+    const double *p_idle_w;       /* [N] power while idle, W                           */
+    int32_t policy;               /* ORC_POLICY_*; 0 means REF_V3                      */
 } orc_rep_in;
 
 typedef struct {
@@ -54,6 +68,8 @@ typedef struct {
     int64_t events;               /* FES events processed (diagnostic) */
     int32_t max_pending;          /* max tasks assigned-but-not-advertised on one node */
     int32_t status;
+    int64_t busy_s;               /* sum of service seconds over all tasks             */
+    double energy_j;              /* builder-defined node energy (fognet_hip.h)        */
 } orc_rep_stats;
 
 typedef struct {
@@ -63,12 +79,22 @@ typedef struct {
     int64_t *done_tick;  /* [T] RELEASERESOURCE tick                              */
     double *final_view_busy; /* [N] broker view busyTime after the last event (nullable) */
     orc_rep_stats *stats;
+    double *node_energy_j;   /* [N] per-node energy (nullable)                         */
+    int64_t *hist;           /* [2][64] histogram counts, ADDED to (nullable)          */
 } orc_rep_out;
 
 int orc_run_rep(const orc_rep_in *in, orc_rep_out *out);
 
 /* Scalar decision core, BrokerBaseApp3.cc:267-281. */
 int orc_decide_v3(int32_t n, const double *adv_busy, const int32_t *adv_mips, int32_t req, int32_t *out_node);
+
+/* North-star extension cost (not in the reference): argmin over j of
+ * dl_j + adv_busy_j * 1e12 + (req / mips_j) * 1e12 in int64 ticks, ties -> lowest j. */
+int orc_decide_ext_lat(int32_t n, const double *adv_busy, const int32_t *mips, const int64_t *dl, int32_t req,
+                       int32_t *out_node);
+
+/* Histogram bin of a duration in ticks (fognet_hip.h FOGNET_HIST_BINS rule). */
+int orc_hist_bin(int64_t ticks);
 
 /* Batch of R replications sharing T and N; node params have stride node_stride
  * (0 = shared).  Runs on `threads` pthreads, one replication per thread at a time. */
@@ -77,6 +103,15 @@ int orc_run_batch(int32_t R, int64_t T, int32_t N, int32_t node_stride,
                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
                   orc_rep_stats *stats, int threads);
+
+/* The same with a policy, an optional power model ([R|1][N], node_stride) and
+ * optional per-node energy [R][N] and per-replication histograms [R][2][64]. */
+int orc_run_batch2(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
+                   const int64_t *arrive_tick, const int32_t *req_mips,
+                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                   const double *p_busy_w, const double *p_idle_w,
+                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                   orc_rep_stats *stats, double *node_energy_j, int64_t *hist, int threads);
 
 #ifdef __cplusplus
 }

@@ -26,11 +26,14 @@ class OrcRepStats(C.Structure):
         ("resp_sum_lo", C.c_uint64), ("resp_sum_hi", C.c_uint64),
         ("resp_sq_lo", C.c_uint64), ("resp_sq_hi", C.c_uint64),
         ("events", C.c_int64), ("max_pending", C.c_int32), ("status", C.c_int32),
+        ("busy_s", C.c_int64), ("energy_j", C.c_double),
     ]
 
 
-ORC_STATS_DTYPE = np.dtype([(n, np.int64 if t in (C.c_int64,) else np.uint64 if t is C.c_uint64 else np.int32)
-                            for n, t in OrcRepStats._fields_])
+_NP = {C.c_int64: np.int64, C.c_uint64: np.uint64, C.c_int32: np.int32, C.c_double: np.float64}
+ORC_STATS_DTYPE = np.dtype([(n, _NP[t]) for n, t in OrcRepStats._fields_])
+assert ORC_STATS_DTYPE.itemsize == C.sizeof(OrcRepStats)
+POLICY_REF_V3, POLICY_EXT_LAT = 1, 16
 
 _lib = None
 
@@ -49,6 +52,12 @@ def lib():
         p = C.c_void_p
         _lib.orc_run_batch.argtypes = [C.c_int32, C.c_int64, C.c_int32, C.c_int32] + [p] * 11 + [C.c_int]
         _lib.orc_run_batch.restype = C.c_int
+        _lib.orc_run_batch2.argtypes = [C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [p] * 15 + [C.c_int]
+        _lib.orc_run_batch2.restype = C.c_int
+        _lib.orc_decide_ext_lat.argtypes = [C.c_int32, p, p, p, C.c_int32, C.POINTER(C.c_int32)]
+        _lib.orc_decide_ext_lat.restype = C.c_int
+        _lib.orc_hist_bin.argtypes = [C.c_int64]
+        _lib.orc_hist_bin.restype = C.c_int
         _lib.orc_decide_v3.argtypes = [C.c_int32, p, p, C.c_int32, C.POINTER(C.c_int32)]
         _lib.orc_decide_v3.restype = C.c_int
     return _lib
@@ -66,8 +75,20 @@ def decide_v3(adv_busy, adv_mips, req):
     return rc, out.value
 
 
-def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool = True):
-    """Replay R replications.  arrive/req: [R,T]; node params [R,N] or [N] (shared)."""
+def decide_ext_lat(adv_busy, mips, dl, req):
+    adv_busy = np.ascontiguousarray(adv_busy, dtype=np.float64)
+    mips = np.ascontiguousarray(mips, dtype=np.int32)
+    dl = np.ascontiguousarray(dl, dtype=np.int64)
+    out = C.c_int32(-7)
+    rc = lib().orc_decide_ext_lat(len(adv_busy), _ptr(adv_busy), _ptr(mips), _ptr(dl), int(req), C.byref(out))
+    return rc, out.value
+
+
+def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool = True, policy: int = 1,
+              p_busy=None, p_idle=None, hist: bool = False):
+    """Replay R replications.  arrive/req: [R,T]; node params [R,N] or [N] (shared).
+    ``p_busy``/``p_idle`` (same shape as mips) enable the energy model; ``hist``
+    returns per-replication histograms [R, 2, 64]."""
     arrive = np.ascontiguousarray(np.atleast_2d(arrive), dtype=np.int64)
     req = np.ascontiguousarray(np.atleast_2d(req), dtype=np.int32)
     R, T = arrive.shape
@@ -81,8 +102,13 @@ def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool =
     status = np.zeros((R, T), np.uint8) if outputs else None
     start = np.zeros((R, T), np.int64) if outputs else None
     done = np.zeros((R, T), np.int64) if outputs else None
+    pb = np.ascontiguousarray(p_busy, dtype=np.float64) if p_busy is not None else None
+    pi = np.ascontiguousarray(p_idle, dtype=np.float64) if p_idle is not None else None
+    energy = np.zeros((R, N), np.float64) if pb is not None else None
+    h = np.zeros((R, 2, 64), np.int64) if hist else None
     stats = (OrcRepStats * R)()
-    lib().orc_run_batch(R, T, N, stride, _ptr(arrive), _ptr(req), _ptr(mips), _ptr(dl), _ptr(ul), _ptr(init),
-                        _ptr(node), _ptr(status), _ptr(start), _ptr(done), C.cast(stats, C.c_void_p), threads)
+    lib().orc_run_batch2(R, T, N, stride, policy, _ptr(arrive), _ptr(req), _ptr(mips), _ptr(dl), _ptr(ul),
+                         _ptr(init), _ptr(pb), _ptr(pi), _ptr(node), _ptr(status), _ptr(start), _ptr(done),
+                         C.cast(stats, C.c_void_p), _ptr(energy), _ptr(h), threads)
     st = np.frombuffer(stats, dtype=ORC_STATS_DTYPE, count=R).copy()
-    return dict(node=node, status=status, start=start, done=done, stats=st)
+    return dict(node=node, status=status, start=start, done=done, stats=st, node_energy=energy, hist=h)

@@ -117,3 +117,69 @@ def test_oracle_state_error_when_task_meets_pending_advert_timer():
     # t0, t1 -> node 0; node 0 advertises busy 2 at 2e12+115; t2 -> node 1 at 3e12+5
     assert o["node"][0][:2].tolist() == [0, 0]
     assert o["stats"]["status"][0] == 4
+
+
+# ------------------------------------------------------------------ builder-defined rows (a10/a11, EXT_LAT)
+# None of these is in the reference: the answers below are derived by hand from
+# the definitions in include/fognet_hip.h (parity unpinned against FogNetSim++).
+
+@pytest.mark.parametrize("ticks,b", [(0, 0), (999_999_999, 0), (10**9, 1), (2 * 10**9 - 1, 1), (2 * 10**9, 2),
+                                     (3 * 10**9, 2), (4 * 10**9, 3), (1023 * 10**9, 10), (1024 * 10**9, 11),
+                                     (2**62, 33), (-5, 0)])
+def test_hist_bin_rule(ticks, b):
+    assert ol.lib().orc_hist_bin(ticks) == b
+
+
+def test_ext_lat_decide_known_answers():
+    # cost_j = dl_j + (busy_j + min(req // mips_j, 2^20)) * 1e12
+    busy = [3.0, 1.0, 1.0, 0.0]
+    mips = [1000, 1000, 4000, 500]
+    dl = [0, 5 * 10**11, 10**11, 0]
+    # req 4000: costs 7e12, 5.5e12, 2.1e12, 8e12 -> node 2
+    assert ol.decide_ext_lat(busy, mips, dl, 4000) == (0, 2)
+    # req 0: costs 3e12, 1.5e12, 1.1e12, 0 -> node 3
+    assert ol.decide_ext_lat(busy, mips, dl, 0) == (0, 3)
+    # tie on cost -> lowest index
+    assert ol.decide_ext_lat([1.0, 1.0], [1000, 1000], [7, 7], 2500) == (0, 0)
+    # network delay decides between otherwise equal nodes
+    assert ol.decide_ext_lat([0.0, 0.0], [1000, 1000], [9, 8], 2500) == (0, 1)
+    # saturation: both service times exceed 2^20 s -> equal saturated service, busy decides
+    assert ol.decide_ext_lat([5.0, 4.0], [1, 2], [0, 0], 2**31 - 1) == (0, 1)
+    assert ol.decide_ext_lat([], [], [], 5)[0] == 2  # NO_NODES
+    assert ol.decide_ext_lat([0.0], [0], [0], 5)[0] == 3  # DIV0
+
+
+def test_energy_known_answer():
+    """One node, two tasks of 3 s and 5 s back to back, plus an idle node:
+    H = last completion; E_j = Pb*B_j + Pi*(H - B_j)."""
+    dl = np.array([10**9, 10**9], np.int64)
+    ul = np.array([10**9, 10**9], np.int64)
+    init = ul.copy()
+    arrive = np.array([10**10, 10**10 + 1], np.int64)
+    req = np.array([3000, 5000], np.int32)
+    mips = np.array([1000, 1000], np.int32)
+    pb = np.array([50.5, 70.0])
+    pi = np.array([10.25, 20.0])
+    o = ol.run_batch(arrive, req, mips, dl, ul, init, p_busy=pb, p_idle=pi, hist=True)
+    st = o["stats"][0]
+    assert st["status"] == 0 and (o["node"][0] == 0).all()  # stale view: node 0 twice
+    H = 10**10 + 10**9 + 8 * TPS
+    assert st["last_tick"] == H and st["busy_s"] == 8
+    e0 = 50.5 * 8 + 10.25 * ((H - 8 * TPS) / 1e12)
+    e1 = 0.0 + 20.0 * (H / 1e12)
+    assert o["node_energy"][0].tolist() == [e0, e1]
+    assert st["energy_j"] == e0 + e1
+    # histograms: task 1 queued 3 s - 1 tick (bin 12: 2048..4095 ms); responses 3.001 s and 8.001 s - 1 tick
+    h = o["hist"][0]
+    assert h[0].sum() == 1 and h[0][12] == 1
+    assert h[1].sum() == 2 and h[1][12] == 1 and h[1][13] == 1
+
+
+def test_ext_lat_replay_invariants():
+    tr = tg.make_batch(77, 4, 64, 3000, sweep=True)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=4,
+                     policy=ol.POLICY_EXT_LAT)
+    assert (o["stats"]["status"] == 0).all()
+    # spreads load (the reference policy herds onto one node between adverts)
+    assert all(len(np.unique(o["node"][r])) > 8 for r in range(4))
+    check_fifo_invariants(tr, o)

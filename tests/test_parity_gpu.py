@@ -280,3 +280,80 @@ def test_full_size_sweep_properties(ctx):
     np.testing.assert_array_equal(out.node[r].cpu().numpy(), o["node"][0])
     np.testing.assert_array_equal(out.done_tick[r].cpu().numpy(), o["done"][0])
     assert st[r].tobytes() == o["stats"][0].tobytes()
+
+
+# ------------------------------------------------------------------ a10/a11 statistics and the EXT_LAT policy
+# Builder-defined rows (include/fognet_hip.h): parity against the oracle's
+# restatement of the same definitions (not pinned by the reference).
+
+def run_gpu_full(ctx, tr, policy="REF_V3", ring_capacity=0):
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(tr, dev)
+    out = fa.run_batch(ctx, d, ring_capacity=ring_capacity, policy=policy, hist=True)
+    torch.cuda.synchronize()
+    return dict(node=out.node.cpu().numpy(), status=out.status.cpu().numpy(),
+                start=out.start_tick.cpu().numpy(), done=out.done_tick.cpu().numpy(),
+                stats=out.rep_stats(), raw=out,
+                energy=out.node_energy.cpu().numpy() if out.node_energy is not None else None,
+                hist=out.hist.cpu().numpy())
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_energy_and_histograms_match_oracle(ctx, shared):
+    tr = tg.make_batch(0x5EED0003, 12, 256, 3000, sweep=True)
+    if shared:
+        tr = dict(tr, mips=tr["mips"][0], dl=tr["dl"][0], ul=tr["ul"][0], init=tr["init"][0])
+    pb, pi = fa.power_model(tr["mips"])
+    tr = dict(tr, p_busy=pb, p_idle=pi)
+    g = run_gpu_full(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8,
+                     p_busy=pb, p_idle=pi, hist=True)
+    assert_parity(tr, g, o)
+    # same IEEE operation sequence on both sides: bit-identical (north star asks 1e-9 relative)
+    np.testing.assert_array_equal(g["energy"], o["node_energy"])
+    assert g["stats"].tobytes() == o["stats"].tobytes()
+    np.testing.assert_array_equal(g["hist"], o["hist"].sum(axis=0))
+    assert g["hist"][0].sum() == o["stats"]["n_queued"].sum() and g["hist"][1].sum() == 12 * 3000
+    job = fa.reduce_stats(ctx, g["raw"].stats, 12)
+    assert int(job["busy_s"]) == int(o["stats"]["busy_s"].sum())
+    np.testing.assert_allclose(float(job["energy_j"]), float(o["stats"]["energy_j"].sum()), rtol=1e-12)
+
+
+def test_histogram_accumulates_across_calls(ctx):
+    tr = tg.make_batch(3, 4, 32, 1000)
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(tr, dev)
+    out = fa.run_batch(ctx, d, hist=True)
+    fa.run_batch(ctx, d, out=out)
+    torch.cuda.synchronize()
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], hist=True)
+    np.testing.assert_array_equal(out.hist.cpu().numpy(), 2 * o["hist"].sum(axis=0))
+
+
+@pytest.mark.parametrize("N,T,R,rho", [(1, 500, 2, 0.9), (5, 2000, 3, 0.8), (64, 3000, 4, 0.8), (100, 2000, 3, 0.95),
+                                       (256, 2500, 6, None)])
+def test_ext_lat_policy_matches_oracle(ctx, N, T, R, rho):
+    tr = tg.make_batch(4242 + N, R, N, T, sweep=rho is None, rho=rho or 0.8)
+    g = run_gpu_full(ctx, tr, policy="EXT_LAT")
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8,
+                     policy=ol.POLICY_EXT_LAT, hist=True)
+    assert (o["stats"]["status"] == 0).all()
+    assert_parity(tr, g, o)
+    np.testing.assert_array_equal(g["hist"], o["hist"].sum(axis=0))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_ext_lat_tie_heavy(ctx, seed):
+    tr = tie_heavy(100 + seed, 8, 3 + 40 * seed, 1500)
+    g = run_gpu_full(ctx, tr, policy="EXT_LAT", ring_capacity=4096)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8,
+                     policy=ol.POLICY_EXT_LAT, hist=True)
+    assert_parity(tr, g, o)
+
+
+def test_ext_lat_latency_bound(ctx):
+    tr = tg.make_batch(9, 2, 8, 100)
+    tr = {k: v.copy() for k, v in tr.items()}
+    tr["dl"][1, 2] = 2**50
+    g = run_gpu_full(ctx, tr, policy="EXT_LAT")
+    assert g["stats"]["status"][0] == 0 and g["stats"]["status"][1] == _abi.FOGNET_ERR_ARG

@@ -18,11 +18,13 @@ def regs_of(s):
 def audit(path, kernel_prefix="_ZN6fognet12_GLOBAL__N_113replay_kernelILi"):
     text = open(path).read().split("\n")
     bad_total = 0
-    for npl in (1, 2, 4):
-        name = f"{kernel_prefix}{npl}EEEvNS_10ReplayArgsE"
+    found = 0
+    for npl, pol in [(n, p) for n in (1, 2, 4) for p in (1, 16)]:  # policies REF_V3, EXT_LAT
+        name = f"{kernel_prefix}{npl}ELi{pol}EEEvNS_10ReplayArgsE"
         starts = [i for i, ln in enumerate(text) if ln.startswith(f"{name}:")]
         if not starts:
             continue
+        found += 1
         s = starts[0]
         body = []
         for ln in text[s + 1:]:
@@ -52,10 +54,11 @@ def audit(path, kernel_prefix="_ZN6fognet12_GLOBAL__N_113replay_kernelILi"):
                 continue
             if not in_asm and regs_of(ln) & nh:
                 bad.append(ln)
-        print(f"NPL={npl}: prefetch registers {sorted(nh)}; compiler references outside asm: {len(bad)}")
+        print(f"NPL={npl} policy={pol}: prefetch registers {sorted(nh)}; compiler references outside asm: {len(bad)}")
         for b in bad[:20]:
             print("   ", b)
         bad_total += len(bad)
+    assert found == 6, f"expected 6 replay_kernel instantiations in the ISA, found {found}"
     return bad_total
 
 
