@@ -1,14 +1,22 @@
 """Benchmark: task-offload decisions/sec of the batched FogNetSim++ replay engine.
 
-Workload (BASELINE.json configs[2], SURVEY.md §8(d) C3 "policy sweep"): per GPU
-R = 4096 replications x T = 100,000 tasks x N = 256 fog nodes, rho x latency
-sweep, synthetic traces generated on the device (Philox recipe, untimed).  One
-step = one pass of the hot path over the batch: the replay kernel (decisions +
-node queues + adverts), the per-replication statistics pass and the exact
-job-level reduction (+ an all-gather of the job record when N > 1).
-Replications are sharded over ranks (weak scaling; no data-path collective).
+Default workload (BASELINE.json configs[2], SURVEY.md §8(d) C3 "policy sweep"):
+per GPU R = 4096 replications x T = 100,000 tasks x N = 256 fog nodes, rho x
+latency sweep, synthetic traces generated on the device (Philox recipe,
+untimed).  One step = one pass of the hot path over the batch: the replay
+kernel (decisions + node queues + adverts), the statistics pass (queueTime /
+response moments, latency histograms, node energy) and the exact job-level
+reduction; with N > 1 ranks also the all-gather of the job record and the
+RCCL all-reduce of histograms + energy.  Replications are sharded over ranks
+(weak scaling; no data-path collective).
 
-  python bench.py [--gpus N --steps K --warmup W]
+``--workload c4`` runs config C4 (Monte Carlo what-if, BASELINE.json
+configs[3]): 1M replications x T = 10,000 x N = 256 in total, sharded over the
+ranks (strong scaling), traces generated on the device INSIDE the timed
+region in blocks of ``--block`` replications (the whole trace would be
+~120 GB), only statistics kept.
+
+  python bench.py [--gpus N --steps K --warmup W] [--workload c3|c4]
   torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -26,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import fognetsimpp_amd as fa  # noqa: E402
+import fognetsimpp_amd.dist  # noqa: E402,F401
 from fognetsimpp_amd import _abi  # noqa: E402
 
 METRIC = "task-offload decisions/sec (node) at R×T×N; % of HBM roofline"
@@ -51,12 +60,21 @@ def main():
     ap.add_argument("--R", type=int, default=4096, help="replications per GPU")
     ap.add_argument("--T", type=int, default=100_000)
     ap.add_argument("--N", type=int, default=256)
-    ap.add_argument("--ring", type=int, default=1024)
+    ap.add_argument("--ring", type=int, default=2048)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0003)
     ap.add_argument("--cpu-reps", type=int, default=1024, help="replications in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--policy", default="REF_V3", choices=("REF_V3", "EXT_LAT"))
+    ap.add_argument("--workload", default="c3", choices=("c3", "c4"))
+    ap.add_argument("--R-total", type=int, default=1_000_000, help="c4: replications over all ranks")
+    ap.add_argument("--block", type=int, default=4096, help="c4: replications per device block")
     args = ap.parse_args()
+    if args.workload == "c4":
+        if args.T == 100_000:
+            args.T = 10_000
+        if args.seed == 0x5EED0003:
+            args.seed = 0x5EED0004
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -70,33 +88,42 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
+    ctx = fa.Context(local)
+    if args.workload == "c4":
+        return bench_c4(args, ctx, dev, dist, world, rank)
     R, T, N = args.R, args.T, args.N
     r0 = rank * R  # contiguous shard of the global replication index space
-    ctx = fa.Context(local)
     mg, sc = fa.sweep_params(np.arange(r0, r0 + R), N)
     t0 = time.time()
     trace = fa.generate_trace(ctx, args.seed, R, T, N, mg, sc, r0=r0)
-    out = fa.allocate_outputs(R, T, dev)
+    pb, pi = fa.power_model(trace["mips"].cpu().numpy())
+    trace["p_busy"] = torch.from_numpy(pb).to(dev)
+    trace["p_idle"] = torch.from_numpy(pi).to(dev)
+    out = fa.allocate_outputs(R, T, dev, N=N, energy=False, hist=True)
     torch.cuda.synchronize()
     log(f"[rank {rank}] trace generated R={R} T={T} N={N} in {time.time() - t0:.2f}s")
 
     job_buf = None
+    energy = None
 
     def step(ev_a=None, ev_b=None):
-        nonlocal job_buf
+        nonlocal job_buf, energy
+        out.hist.zero_()
         if ev_a is not None:
             ev_a.record()
-        fa.run_batch(ctx, trace, out, ring_capacity=args.ring, stage="replay")
+        fa.run_batch(ctx, trace, out, ring_capacity=args.ring, stage="replay", policy=args.policy)
         if ev_b is not None:
             ev_b.record()
-        fa.run_batch(ctx, trace, out, ring_capacity=args.ring, stage="stats")
+        fa.run_batch(ctx, trace, out, ring_capacity=args.ring, stage="stats", policy=args.policy)
         job_buf = torch.zeros(_abi.JOB_STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         ctx.check(ctx._lib.fognet_reduce_stats_dev(ctx.handle, fa.engine._ptr(out.stats), R,
                                                    fa.engine._ptr(job_buf), fa.engine._stream_ptr(dev)), "reduce")
+        energy = job_buf[-8:].view(torch.float64).clone()  # fognet_job_stats.energy_j (last field)
         if dist is not None:
             gathered = [torch.empty_like(job_buf) for _ in range(world)]
             dist.all_gather(gathered, job_buf)
             job_buf = torch.cat(gathered)
+            fa.dist.allreduce_hist_energy(out.hist, energy)
 
     for i in range(args.warmup):
         step()
@@ -127,6 +154,7 @@ def main():
     jobs = job_buf.cpu().numpy().view(_abi.JOB_STATS_DTYPE)
     job = fa.merge_job_stats(list(jobs))
     summary = fa.summarize(job)
+    hist = out.hist.cpu().numpy()
 
     decisions = world * R * T * args.steps
     value = decisions / elapsed
@@ -162,7 +190,9 @@ def main():
             "dtype": "int64",
             "data": "synthetic (device-generated Philox traces, C3 policy-sweep recipe)",
             "config": {"workload": "C3 policy sweep (BASELINE.json configs[2])", "R_per_gpu": R, "T": T, "N": N,
-                       "R_total": R * world, "ring_capacity": args.ring, "policy": "REF_V3 (BrokerBaseApp3)",
+                       "R_total": R * world, "ring_capacity": args.ring,
+                       "policy": "REF_V3 (BrokerBaseApp3)" if args.policy == "REF_V3" else
+                       "EXT_LAT (north-star cost; not in the reference)",
                        "parallelism": f"replications sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
@@ -172,7 +202,112 @@ def main():
             "failed_replications": failed,
             "stats": {"queueTime_ms_mean": summary["queueTime_ms"].get("mean"),
                       "response_ms_mean": summary["response_ms"].get("mean"),
-                      "max_pending": summary["max_pending"], "decisions": summary["decisions"]},
+                      "max_pending": summary["max_pending"], "decisions": summary["decisions"],
+                      "energy_j": float(energy[0]), "busy_s": summary["busy_s"],
+                      "hist_counts": [int(hist[0].sum()), int(hist[1].sum())]},
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_c4(args, ctx, dev, dist, world, rank):
+    """Config C4: R_total replications (sharded over ranks) x T x N; per block
+    of ``args.block`` replications the device generates the traces, replays
+    them and reduces statistics; only the job record, the histograms and the
+    energy survive a block.  Generation is inside the timed region."""
+    from fognetsimpp_amd.dist import shard
+    T, N, B = args.T, args.N, args.block
+    r0, n = shard(args.R_total, world, rank)
+    blocks = [(r0 + b, min(B, n - b)) for b in range(0, n, B)]
+    mg_all, sc_all = fa.sweep_params(np.arange(r0, r0 + n), N)
+    mg_d = torch.from_numpy(np.ascontiguousarray(mg_all)).to(dev)
+    sc_d = torch.from_numpy(np.ascontiguousarray(sc_all)).to(dev)
+    bufs = fa.allocate_trace(B, T, N, dev)
+    pb, pi = fa.power_model(1000 * (1 + np.arange(N) % 4))  # the generator's MIPS pattern
+    bufs["p_busy"] = torch.from_numpy(np.tile(pb, (B, 1))).to(dev)  # same [R][N] layout as mips
+    bufs["p_idle"] = torch.from_numpy(np.tile(pi, (B, 1))).to(dev)
+    out = fa.allocate_outputs(B, T, dev, N=N, energy=False, hist=True)
+    jrec = torch.zeros((max(1, len(blocks)), _abi.JOB_STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    stream = fa.engine._stream_ptr(dev)
+    log(f"[rank {rank}] c4: {n} replications in {len(blocks)} blocks of <= {B}, T={T} N={N}")
+
+    def step(evs=None):
+        out.hist.zero_()
+        for i, (b0, nb) in enumerate(blocks):
+            tr = {k: v[:nb] for k, v in bufs.items()}
+            o = fa.BatchResult(out.node[:nb], out.status[:nb], out.start_tick[:nb], out.done_tick[:nb],
+                               out.stats[: nb * _abi.REP_STATS_DTYPE.itemsize], None, out.hist)
+            fa.generate_trace(ctx, args.seed, nb, T, N, mg_d[b0 - r0: b0 - r0 + nb], sc_d[b0 - r0: b0 - r0 + nb],
+                              r0=b0, out=tr)
+            if evs is not None:
+                evs[i][0].record()
+            fa.run_batch(ctx, tr, o, ring_capacity=args.ring, stage="replay", policy=args.policy)
+            if evs is not None:
+                evs[i][1].record()
+            fa.run_batch(ctx, tr, o, ring_capacity=args.ring, stage="stats", policy=args.policy)
+            ctx.check(ctx._lib.fognet_reduce_stats_dev(ctx.handle, fa.engine._ptr(o.stats), nb,
+                                                       fa.engine._ptr(jrec[i]), stream), "reduce")
+        job = fa.merge_job_stats(list(jrec.cpu().numpy().view(_abi.JOB_STATS_DTYPE).reshape(-1)[:len(blocks)]))
+        if dist is not None:
+            jb = fa.dist.job_record_tensor(job, dev)
+            job = fa.dist.allgather_job_stats(jb)
+            energy = torch.tensor([float(job["energy_j"])], dtype=torch.float64, device=dev)
+            fa.dist.allreduce_hist_energy(out.hist, energy)
+        return job
+
+    for i in range(args.warmup):
+        step()
+        torch.cuda.synchronize()
+        log(f"[rank {rank}] warmup {i + 1}/{args.warmup} done")
+    evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in blocks]
+           for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        job = step(evs[i])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    replay_ms = float(np.mean([sum(a.elapsed_time(b) for a, b in e) for e in evs]))
+    summary = fa.summarize(job)
+    hist = out.hist.cpu().numpy()
+    decisions = args.R_total * T * args.steps
+    bpd = algorithmic_bytes_per_decision(T, N)
+    achieved_gbs = n * T * bpd / (replay_ms / 1e3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        nb = blocks[0][1]
+        tr = {k: v[:nb] for k, v in bufs.items() if k not in ("p_busy", "p_idle")}
+        fa.generate_trace(ctx, args.seed, nb, T, N, mg_d[:nb], sc_d[:nb], r0=r0, out=tr)
+        torch.cuda.synchronize()
+        cpu = cpu_baseline(tr, args, nb, T, N)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": decisions / elapsed, "unit": "decisions/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (Philox traces generated on the device inside the timed region, C4 recipe)",
+            "config": {"workload": "C4 Monte Carlo what-if (BASELINE.json configs[3])", "R_total": args.R_total,
+                       "T": T, "N": N, "block": B, "ring_capacity": args.ring, "policy": args.policy,
+                       "parallelism": f"replications sharded over {world} GPU(s); RCCL all-reduce of histograms"
+                                      f" + energy, all-gather of the job record"},
+            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None, "kernel": "replay_kernel",
+                         "kernel_ms_per_step": replay_ms, "bytes_per_decision": bpd,
+                         "note": "per-task outputs go to a reused block scratch buffer"},
+            "cpu_baseline": cpu,
+            "failed_replications": summary["failed"],
+            "stats": {"decisions": summary["decisions"], "queueTime_ms_mean": summary["queueTime_ms"].get("mean"),
+                      "response_ms_mean": summary["response_ms"].get("mean"), "energy_j": summary["energy_j"],
+                      "max_pending": summary["max_pending"], "hist_counts": [int(hist[0].sum()), int(hist[1].sum())]},
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -7,7 +7,7 @@ independent what-if replications on gfx950 behind the C ABI in
 include/fognet_hip.h (libfognet_hip.so, built in-tree).
 """
 from ._abi import FognetError, load as _load_lib  # noqa: F401
-from .engine import (BatchResult, BrokerBaseApp3, Context, allocate_outputs, as_device_trace,  # noqa: F401
+from .engine import (BatchResult, BrokerBaseApp3, Context, allocate_outputs, allocate_trace, as_device_trace,  # noqa: F401
                      generate_trace, merge_job_stats, power_model, reduce_stats, run_batch, summarize,
                      sweep_params)
 

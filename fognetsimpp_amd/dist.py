@@ -45,3 +45,16 @@ def allgather_job_stats(job_bytes: torch.Tensor, group=None) -> np.ndarray:
     dist.all_gather(parts, job_bytes.contiguous(), group=group)
     recs = [p.cpu().numpy().view(_abi.JOB_STATS_DTYPE)[0] for p in parts]
     return merge_job_stats(recs)
+
+
+def allreduce_hist_energy(hist: torch.Tensor, energy: torch.Tensor, group=None) -> None:
+    """In-place sum over ranks of the job latency histograms (int64
+    [FOGNET_HIST_METRICS, FOGNET_HIST_BINS], exact) and of the energy
+    statistics (float64 tensor: job energy and per-node energy totals).  This
+    is the one RCCL collective of the data path (north star: "RCCL over xGMI
+    used only for the final all-reduce of latency histograms and energy
+    statistics"); ~1 KB + 8 B x nodes, so it is latency-bound."""
+    import torch.distributed as dist
+
+    dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(energy, op=dist.ReduceOp.SUM, group=group)

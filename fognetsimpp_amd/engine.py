@@ -179,6 +179,14 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
     stride = N if mips.dim() == 2 else 0
     pol = POLICIES[policy] if isinstance(policy, str) else int(policy)
     energy = trace.get("p_busy") is not None
+    # host-side shape checks: the kernels index every array with these strides
+    for k in ("dl", "ul", "init") + (("p_busy", "p_idle") if energy else ()):
+        if tuple(trace[k].shape) != tuple(mips.shape):
+            raise FognetError(_abi.FOGNET_ERR_ARG, f"{k} has shape {tuple(trace[k].shape)}, mips {tuple(mips.shape)}")
+    if tuple(req.shape) != (R, T) or (mips.dim() == 2 and mips.shape[0] != R):
+        raise FognetError(_abi.FOGNET_ERR_ARG, "trace arrays disagree on R/T")
+    if out is not None and (tuple(out.node.shape) != (R, T) or out.stats.numel() < R * _abi.REP_STATS_DTYPE.itemsize):
+        raise FognetError(_abi.FOGNET_ERR_ARG, "output buffers too small for the trace")
     if out is None:
         out = allocate_outputs(R, T, arrive.device, N=N, energy=energy, hist=hist)
     bi = _abi.BatchIn(R, T, N, pol, stride, ring_capacity,
@@ -242,14 +250,9 @@ def summarize(job) -> dict:
     }
 
 
-def generate_trace(ctx: Context, seed: int, R: int, T: int, N: int, mean_gap_ticks, lat_scale,
-                   r0: int = 0, req_lo: int = 1000, req_hi: int = 64000, device=None) -> dict:
-    """Device trace generator (recipe: csrc/tracegen.hip); per-replication
-    ``mean_gap_ticks`` (float64 [R]) and ``lat_scale`` (int64 [R])."""
-    device = device if device is not None else torch.device("cuda", ctx.device)
-    mg = torch.as_tensor(np.asarray(mean_gap_ticks, dtype=np.float64).reshape(R), device=device)
-    ls = torch.as_tensor(np.asarray(lat_scale, dtype=np.int64).reshape(R), device=device)
-    tr = {
+def allocate_trace(R: int, T: int, N: int, device) -> dict:
+    """Device buffers of one trace batch (arrive/req [R, T], node params [R, N])."""
+    return {
         "arrive": torch.empty((R, T), dtype=torch.int64, device=device),
         "req": torch.empty((R, T), dtype=torch.int32, device=device),
         "mips": torch.empty((R, N), dtype=torch.int32, device=device),
@@ -257,6 +260,20 @@ def generate_trace(ctx: Context, seed: int, R: int, T: int, N: int, mean_gap_tic
         "ul": torch.empty((R, N), dtype=torch.int64, device=device),
         "init": torch.empty((R, N), dtype=torch.int64, device=device),
     }
+
+
+def generate_trace(ctx: Context, seed: int, R: int, T: int, N: int, mean_gap_ticks, lat_scale,
+                   r0: int = 0, req_lo: int = 1000, req_hi: int = 64000, device=None, out: dict | None = None) -> dict:
+    """Device trace generator (recipe: csrc/tracegen.hip); per-replication
+    ``mean_gap_ticks`` (float64 [R]) and ``lat_scale`` (int64 [R]), host arrays
+    or device tensors.  ``out``: reuse these buffers (allocate_trace layout)."""
+    device = device if device is not None else torch.device("cuda", ctx.device)
+    if isinstance(mean_gap_ticks, torch.Tensor):
+        mg, ls = mean_gap_ticks.reshape(R).contiguous(), lat_scale.reshape(R).contiguous()
+    else:
+        mg = torch.as_tensor(np.asarray(mean_gap_ticks, dtype=np.float64).reshape(R), device=device)
+        ls = torch.as_tensor(np.asarray(lat_scale, dtype=np.int64).reshape(R), device=device)
+    tr = out if out is not None else allocate_trace(R, T, N, device)
     gp = _abi.GenParams(seed & 0xFFFFFFFF, req_lo, req_hi, 0, _ptr(mg), _ptr(ls))
     rc = ctx._lib.fognet_gen_trace_dev(ctx.handle, C.byref(gp), r0, R, T, N, _ptr(tr["arrive"]), _ptr(tr["req"]),
                                        _ptr(tr["mips"]), _ptr(tr["dl"]), _ptr(tr["ul"]), _ptr(tr["init"]),

@@ -11,7 +11,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from fognetsimpp_amd import _abi
-from fognetsimpp_amd.dist import allgather_job_stats, job_record_tensor, shard
+from fognetsimpp_amd.dist import allgather_job_stats, allreduce_hist_energy, job_record_tensor, shard
 from fognetsimpp_amd.engine import merge_job_stats
 
 
@@ -21,8 +21,9 @@ def job_from_rep_stats(st):
     rec["n_reps"] = len(st)
     ok = st[st["status"] == 0]
     rec["n_failed"] = len(st) - len(ok)
-    for f in ("n_tasks", "n_queued", "n_started", "events"):
+    for f in ("n_tasks", "n_queued", "n_started", "events", "busy_s"):
         rec[f] = int(ok[f].sum())
+    rec["energy_j"] = float(np.sum(ok["energy_j"]))
     big = np.iinfo(np.int64)
     rec["last_tick"] = int(ok["last_tick"].max()) if len(ok) else big.min
     rec["queue_min_ticks"] = int(ok["queue_min_ticks"].min()) if len(ok) else big.max
@@ -54,14 +55,26 @@ def _worker(rank, world, port, reps, q):
     import tracegen as tg
     r0, n = shard(reps, world, rank)
     recs = []
+    hist = torch.zeros((_abi.HIST_METRICS, _abi.HIST_BINS), dtype=torch.int64)
     for r in range(r0, r0 + n):
-        rp = tg.make_replication(77, r, 16, 400, rho=(0.5, 0.9)[r % 2])
-        recs.append(ol.run_batch(rp["arrive"], rp["req"], rp["mips"], rp["dl"], rp["ul"], rp["init"])["stats"])
+        o = _replicate(ol, tg, r)
+        recs.append(o["stats"])
+        hist += torch.from_numpy(o["hist"].sum(axis=0))
     st = np.concatenate(recs).view(_abi.REP_STATS_DTYPE) if recs else np.zeros(0, _abi.REP_STATS_DTYPE)
     merged = allgather_job_stats(job_record_tensor(job_from_rep_stats(st), torch.device("cpu")))
+    energy = torch.tensor([float(np.sum(st["energy_j"]))], dtype=torch.float64)
+    allreduce_hist_energy(hist, energy)
     if rank == 0:
-        q.put(merged.tobytes())
+        q.put((merged.tobytes(), hist.numpy().copy(), float(energy[0])))
     dist.destroy_process_group()
+
+
+def _replicate(ol, tg, r):
+    import fognetsimpp_amd as fa
+    rp = tg.make_replication(77, r, 16, 400, rho=(0.5, 0.9)[r % 2])
+    pb, pi = fa.power_model(rp["mips"])
+    return ol.run_batch(rp["arrive"], rp["req"], rp["mips"], rp["dl"], rp["ul"], rp["init"], p_busy=pb, p_idle=pi,
+                        hist=True)
 
 
 def free_port():
@@ -83,15 +96,16 @@ def test_gloo_world2_job_stats_match_single_process():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, reps, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=110)
+    got, got_hist, got_energy = q.get(timeout=110)
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    sts = []
-    for r in range(reps):
-        rp = tg.make_replication(77, r, 16, 400, rho=(0.5, 0.9)[r % 2])
-        sts.append(ol.run_batch(rp["arrive"], rp["req"], rp["mips"], rp["dl"], rp["ul"], rp["init"])["stats"])
-    st = np.concatenate(sts).view(_abi.REP_STATS_DTYPE)
+    outs = [_replicate(ol, tg, r) for r in range(reps)]
+    st = np.concatenate([o["stats"] for o in outs]).view(_abi.REP_STATS_DTYPE)
+    np.testing.assert_array_equal(got_hist, sum(o["hist"].sum(axis=0) for o in outs))
+    assert got_hist[1].sum() == reps * 400
+    np.testing.assert_allclose(got_energy, float(np.sum(st["energy_j"])), rtol=1e-12)
+    assert got_energy > 0
     single = job_from_rep_stats(st)
     assert got == merge_job_stats([single]).tobytes()
     # and the merge is associative: per-replication records merged one by one

@@ -16,4 +16,4 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_W
   echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/p$i.log; exit $rc; fi
 done
-python3 tools/pmc_summary.py replay_kernel 409600000 gpurun_out/pmc/pmc_traffic.json > /dev/null
+python3 tools/pmc_summary.py replay_kernel 409600000 gpurun_out/pmc/pmc_traffic.json 2048 > /dev/null

@@ -42,7 +42,7 @@ def main():
                 out[k + "_frac_of_wave_cycles"] = per[k] / per["SQ_WAVE_CYCLES"]
     # the record bench.py reads (profiles/pmc_traffic.json): C3 default config
     if "hbm_bytes_per_launch" in out:
-        out["config"] = {"R": 4096, "T": 100000, "N": 256, "ring": 1024}
+        out["config"] = {"R": 4096, "T": 100000, "N": 256, "ring": int(sys.argv[4]) if len(sys.argv) > 4 else 2048}
         out["replay_hbm_bytes_per_launch"] = out["hbm_bytes_per_launch"]
     txt = json.dumps(out, indent=1)
     print(txt)
