@@ -225,6 +225,89 @@ __device__ __forceinline__ void refill_nh(int s, const Slot& st, const RingEntry
   }
 }
 
+// ---- trace chunk staging (LDS-DMA)
+//
+// The next 64 publishes {arrive lo, arrive hi, req} are copied global -> LDS
+// by three global_load_lds_dword while the current chunk is replayed, so a
+// chunk boundary costs an LDS read instead of an HBM round trip.  The copies
+// are inline asm (hipcc neither sees nor waits for them): they are tallied in
+// `ops` like the head+1 prefetches and waited for by age with wait_vm.  M0 is
+// written and restored inside the statement (it is compiler-reserved).  The
+// instruction offset is added to the LDS address as well as to the global one
+// (LDS = M0 + inst_offset + 4*lane), so the high-dword copy sets
+// M0 = base + 0x100 - 4 and lands at base + 0x100 + 4*lane.
+__device__ __forceinline__ void chunk_dma(const int64_t* arrive_c, const int32_t* req_c, uint32_t lane_cl,
+                                          uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %5\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, %3\n\t"
+      "s_add_u32 m0, %5, 0xfc\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, %3 offset:4\n\t"
+      "s_add_u32 m0, %5, 0x200\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %2, %4\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(lane_cl * 8u), "v"(lane_cl * 4u), "s"(arrive_c), "s"(req_c), "s"(lds)
+      : "memory");
+}
+constexpr uint32_t kChunkOps = 3;
+
+// s_waitcnt vmcnt(min(m, 8)) for a wave-uniform m (the immediate needs a branch ladder).
+__device__ __forceinline__ void wait_vm(uint32_t m) {
+  asm volatile(
+      "s_cmp_lt_u32 %0, 8\n\t"
+      "s_cbranch_scc1 1f\n\t"
+      "s_waitcnt vmcnt(8)\n\t"
+      "s_branch 9f\n"
+      "1:\n\t"
+      "s_cmp_lt_u32 %0, 4\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_cmp_lt_u32 %0, 6\n\t"
+      "s_cbranch_scc1 3f\n\t"
+      "s_cmp_eq_u32 %0, 6\n\t"
+      "s_cbranch_scc1 4f\n\t"
+      "s_waitcnt vmcnt(7)\n\t"
+      "s_branch 9f\n"
+      "4:\n\t"
+      "s_waitcnt vmcnt(6)\n\t"
+      "s_branch 9f\n"
+      "3:\n\t"
+      "s_cmp_eq_u32 %0, 4\n\t"
+      "s_cbranch_scc1 5f\n\t"
+      "s_waitcnt vmcnt(5)\n\t"
+      "s_branch 9f\n"
+      "5:\n\t"
+      "s_waitcnt vmcnt(4)\n\t"
+      "s_branch 9f\n"
+      "2:\n\t"
+      "s_cmp_lt_u32 %0, 2\n\t"
+      "s_cbranch_scc1 6f\n\t"
+      "s_cmp_eq_u32 %0, 2\n\t"
+      "s_cbranch_scc1 7f\n\t"
+      "s_waitcnt vmcnt(3)\n\t"
+      "s_branch 9f\n"
+      "7:\n\t"
+      "s_waitcnt vmcnt(2)\n\t"
+      "s_branch 9f\n"
+      "6:\n\t"
+      "s_cmp_eq_u32 %0, 1\n\t"
+      "s_cbranch_scc0 8f\n\t"
+      "s_waitcnt vmcnt(1)\n\t"
+      "s_branch 9f\n"
+      "8:\n\t"
+      "s_waitcnt vmcnt(0)\n"
+      "9:"
+      :
+      : "s"(m)
+      : "scc", "memory");
+}
+
 // S seconds in ticks: S * 1e12 = (S * 5^12) << 12, one v_mad_u64_u32 + shift.
 __device__ __forceinline__ int64_t ticks_of(uint32_t s) {
   static_assert(kTicksPerSecond == 244140625ll << 12, "1e12 ticks per second");
@@ -406,12 +489,16 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
   __shared__ int64_t s_tld[NPL * kWave];   // tail completion tick (INT64_MIN: node never used)
   __shared__ uint32_t s_tlC[NPL * kWave];  // tail cumulative service (mod 2^32)
   __shared__ uint32_t s_tlS[NPL * kWave];  // tail service seconds
+  __shared__ uint32_t s_ch[3 * kWave];     // staged trace chunk: arrive lo | arrive hi | req
 
   const int T = A.T, N = A.N;
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)T;
   const uint32_t qmask = (1u << A.q_log2) - 1u;
   const int64_t arrive0 = T > 0 ? A.arrive[tbase] : kNever;
+  const uint32_t lds_ch = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)s_ch;
+  uint32_t ch_stamp = 0u;  // `ops` after the staged chunk's copies were issued
+  if (T > 0) chunk_dma(A.arrive + tbase, A.req + tbase, (uint32_t)min(lane, min(kWave, T) - 1), lds_ch);
 
   // ---- node parameters + preconditions (fognet_hip.h, fognet_batch_in)
   bool bad = false;
@@ -467,11 +554,12 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
   bool dirty = false;
   int64_t prev_t = INT64_MIN;
   uint32_t max_pend = 0u;
-  uint32_t ops = 0u;  // tally of issued vector-memory instructions (see kPrefetchOps)
+  uint32_t ops = T > 0 ? kChunkOps : 0u;  // tally of issued vector-memory instructions (see kPrefetchOps)
+  ch_stamp = ops;
   int64_t n_done = 0;
   uint32_t scan = 0u;  // profile builds: ring entries read by c_arrived (per lane)
 #if FOGNET_REPLAY_PROFILE == 2
-  uint64_t p_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t p_t[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t p_start = __builtin_amdgcn_s_memtime();
   uint64_t p_last = p_start;
 #endif
@@ -488,9 +576,10 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
     const bool live = lane < cnt;
-    const int64_t ca = live ? A.arrive[tbase + c0 + lane] : kNever;
-    const int32_t cr = live ? A.req[tbase + c0 + lane] : 0;
-    ops += 2u;  // the two chunk loads (lane 0 is always live)
+    wait_vm((ops - ch_stamp) & 0xFFu);  // the staged chunk has landed in LDS
+    const uint32_t l_ch = lane_now();
+    const int64_t ca = live ? (int64_t)(((uint64_t)s_ch[kWave + l_ch] << 32) | s_ch[l_ch]) : kNever;
+    const int32_t cr = live ? (int32_t)s_ch[2 * kWave + l_ch] : 0;
     PROF(p_chunks++;)
     TMARK(0)
     // trace preconditions: nondecreasing ticks, requirement >= 0, ticks < 2^61
@@ -501,6 +590,13 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     }
     prev_t = readlane_i64(ca, cnt - 1);
     const int64_t t_last = prev_t;  // only picks which horizons are evaluated exactly
+    if (c0 + kWave < T) {  // stage the next chunk (ca/cr were consumed above: LDS reads are done)
+      const int cn = min(kWave, T - c0 - kWave);
+      chunk_dma(A.arrive + tbase + c0 + kWave, A.req + tbase + c0 + kWave, (uint32_t)min(lane, cn - 1), lds_ch);
+      ops += kChunkOps;
+      ch_stamp = ops;
+    }
+    TMARK(0)
 
     int jp = 0;
     while (jp < cnt) {
@@ -518,7 +614,9 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
             if (!ballot(due)) break;
             dirty = true;
             PROF(p_advit++; p_adv += __popcll(ballot(due)); p_rd++; p_w0 += young(st[s], due && pending(st[s]) >= 2u);)
+            TMARK(1)
             const u32x4 nhw = read_nh<s>(st[s], due && pending(st[s]) >= 2u, ops);
+            TMARK(8)
             // apply_advert prefetches head+2 where >= 3 are pending: tally it
             // first, so the stamp already counts the load itself
             if (ballot(due && pending(st[s]) >= 3u)) ops += 1u;
@@ -562,7 +660,9 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
           }
           if (ballot(deep)) {
             PROF(p_hz++; p_rd++; p_w0 += young(st[s], deep && pending(st[s]) >= 2u);)
+            TMARK(3)
             const u32x4 nhw = read_nh<s>(st[s], deep && pending(st[s]) >= 2u, ops);
+            TMARK(9)
             if (deep) {
               const int64_t h = horizon(st[s], nhw, j, best, s_tlC[j], s_dl[j], s_ul[j], ring_s(s), qmask, scan);
               e_lane = h < e_lane ? h : e_lane;
@@ -750,6 +850,8 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     S->resp_min_ticks = p_t[5];
     S->resp_max_ticks = p_t[6];
     S->queue_sum_lo = p_t[7];
+    S->queue_sq_lo = p_t[8];
+    S->queue_sq_hi = p_t[9];
     S->queue_sum_hi = p_last - p_start;
 #endif
 #if FOGNET_REPLAY_PROFILE == 1
