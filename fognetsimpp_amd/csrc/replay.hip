@@ -606,12 +606,17 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
       carry = false;
       int64_t E = E_carry;
       if (!resume) {
-        // 1) completion adverts that reached the broker strictly before t_p
-        static_for<0, NPL>([&](auto sc) {
-          constexpr int s = decltype(sc)::value;
-          for (;;) {
+        // 1) completion adverts that reached the broker strictly before t_p.
+        //    Adverts of different nodes commute (each sets only its node's
+        //    key), so rounds go over the slots round-robin: a node's next
+        //    head+1 wait is then covered by the other slots' work.
+        for (;;) {
+          bool any = false;
+          static_for<0, NPL>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
             const bool due = st[s].nxt < t_p;
-            if (!ballot(due)) break;
+            if (!ballot(due)) return;
+            any = true;
             dirty = true;
             PROF(p_advit++; p_adv += __popcll(ballot(due)); p_rd++; p_w0 += young(st[s], due && pending(st[s]) >= 2u);)
             TMARK(1)
@@ -624,8 +629,9 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
               const int k = s * kWave + lane;
               apply_advert<s>(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops, scan);
             }
-          }
-        });
+          });
+          if (!any) break;
+        }
         TMARK(1)
         if constexpr (kExt) {
           // 2') per-publish argmin of the extension cost; every run is one publish
