@@ -223,6 +223,9 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
   a.hist = out->hist;
   if (a.out_energy && !a.p_busy) return fail(c, FOGNET_ERR_ARG, "node_energy_j needs the power model (p_busy_w/p_idle_w)");
   hipError_t e = hipSuccess;
+  // both stages: the replay kernel runs the statistics pass as its epilogue
+  a.fuse_stats = which == 3 ? 1 : 0;
+  if (a.fuse_stats) which = 1;
   if (which & 1) {
     const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
     rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ring_bytes, "ring workspace");

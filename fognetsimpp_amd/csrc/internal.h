@@ -157,7 +157,7 @@ struct ReplayArgs {
   int32_t q_log2;  // ring capacity per node = 1 << q_log2
   uint32_t max_s;  // largest admissible service time (keeps busy < 2^32)
   int32_t policy;  // fognet_policy
-  int32_t pad_;
+  int32_t fuse_stats;  // 1: replay_kernel also computes the statistics pass (rep_stats) as an epilogue
   const int64_t* arrive;
   const int32_t* req;
   const int32_t* mips;

@@ -476,6 +476,187 @@ __device__ __forceinline__ void run_scan_level(uint32_t& Cs, int64_t& Ac) {
   Cs = Cl + Cs;
 }
 
+// ---------------------------------------------------------------- statistics
+// Exact per-replication statistics from the replay outputs: queueTime
+// (ComputeBrokerApp3.cc:238) over queued tasks, response (done - publish
+// arrival) over all tasks.  128-bit integer sums are bit-identical for any
+// summation order, so the replay kernel's fused epilogue (one wave) and
+// rep_stats_kernel (256 threads) write the same record.
+
+struct Acc {
+  uint64_t n4, n5, busy;
+  uint64_t qs_lo, qs_hi, qq_lo, qq_hi, rs_lo, rs_hi, rq_lo, rq_hi;
+  int64_t qmin, qmax, rmin, rmax, last;
+};
+
+__device__ __forceinline__ Acc acc_identity() {
+  Acc a = {};
+  a.qmin = a.rmin = INT64_MAX;
+  a.qmax = a.rmax = a.last = INT64_MIN;
+  return a;
+}
+
+__device__ __forceinline__ void add128(uint64_t& lo, uint64_t& hi, uint64_t vlo, uint64_t vhi) {
+  const uint64_t o = lo;
+  lo += vlo;
+  hi += vhi + (lo < o ? 1u : 0u);
+}
+
+__device__ __forceinline__ void add_moment(uint64_t& slo, uint64_t& shi, uint64_t& qlo, uint64_t& qhi,
+                                           uint64_t v) {
+  add128(slo, shi, v, 0u);
+  add128(qlo, qhi, v * v, __umul64hi(v, v));
+}
+
+__device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
+  a.n4 += b.n4;
+  a.n5 += b.n5;
+  a.busy += b.busy;
+  add128(a.qs_lo, a.qs_hi, b.qs_lo, b.qs_hi);
+  add128(a.qq_lo, a.qq_hi, b.qq_lo, b.qq_hi);
+  add128(a.rs_lo, a.rs_hi, b.rs_lo, b.rs_hi);
+  add128(a.rq_lo, a.rq_hi, b.rq_lo, b.rq_hi);
+  a.qmin = min(a.qmin, b.qmin);
+  a.qmax = max(a.qmax, b.qmax);
+  a.rmin = min(a.rmin, b.rmin);
+  a.rmax = max(a.rmax, b.rmax);
+  a.last = max(a.last, b.last);
+}
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, kWave);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, kWave);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Butterfly merge over the 64 lanes of a wave: every lane ends with the total.
+__device__ __forceinline__ Acc wave_merge(Acc a) {
+#pragma unroll 1
+  for (int m = kWave / 2; m > 0; m >>= 1) {
+    Acc b;
+    b.n4 = shfl_xor_u64(a.n4, m);
+    b.n5 = shfl_xor_u64(a.n5, m);
+    b.busy = shfl_xor_u64(a.busy, m);
+    b.qs_lo = shfl_xor_u64(a.qs_lo, m);
+    b.qs_hi = shfl_xor_u64(a.qs_hi, m);
+    b.qq_lo = shfl_xor_u64(a.qq_lo, m);
+    b.qq_hi = shfl_xor_u64(a.qq_hi, m);
+    b.rs_lo = shfl_xor_u64(a.rs_lo, m);
+    b.rs_hi = shfl_xor_u64(a.rs_hi, m);
+    b.rq_lo = shfl_xor_u64(a.rq_lo, m);
+    b.rq_hi = shfl_xor_u64(a.rq_hi, m);
+    b.qmin = (int64_t)shfl_xor_u64((uint64_t)a.qmin, m);
+    b.qmax = (int64_t)shfl_xor_u64((uint64_t)a.qmax, m);
+    b.rmin = (int64_t)shfl_xor_u64((uint64_t)a.rmin, m);
+    b.rmax = (int64_t)shfl_xor_u64((uint64_t)a.rmax, m);
+    b.last = (int64_t)shfl_xor_u64((uint64_t)a.last, m);
+    acc_merge(a, b);
+  }
+  return a;
+}
+
+// Accumulate tasks i = i0, i0 + stride, ... < n of one replication into `a`
+// (plus the per-node service seconds s_busy and the histogram s_hist in LDS
+// when those statistics are on).  The loads of UNROLL tasks are issued
+// before any is used.  dl_of(k): node k's downlink latency.
+template <int UNROLL, class DlOf>
+__device__ __forceinline__ void stats_accumulate(const ReplayArgs& A, size_t tbase, int n, int i0, int stride, Acc& a,
+                                                 unsigned long long* s_busy, uint32_t* s_hist, DlOf dl_of) {
+  const bool energy = A.p_busy != nullptr;
+  const bool hist = A.hist != nullptr;
+  for (int ib = i0; ib < n; ib += stride * UNROLL) {
+    int64_t t[UNROLL], st0[UNROLL], dn[UNROLL];
+    int32_t kk[UNROLL];
+    uint32_t stt[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int i = ib + u * stride;
+      const size_t o = tbase + (size_t)(i < n ? i : ib);  // past the end: reload task ib (in bounds, unused)
+      t[u] = A.arrive[o];
+      kk[u] = A.out_node[o];
+      stt[u] = A.out_status[o];
+      st0[u] = A.out_start[o];
+      dn[u] = A.out_done[o];
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (ib + u * stride < n) {
+        const int32_t k = kk[u];
+        const int64_t resp = dn[u] - t[u];
+        const uint64_t svc = (uint64_t)(dn[u] - st0[u]) / (uint64_t)kTicksPerSecond;  // whole seconds
+        a.busy += svc;
+        if (energy) atomicAdd(&s_busy[k], (unsigned long long)svc);
+        add_moment(a.rs_lo, a.rs_hi, a.rq_lo, a.rq_hi, (uint64_t)resp);
+        a.rmin = min(a.rmin, resp);
+        a.rmax = max(a.rmax, resp);
+        a.last = max(a.last, dn[u]);
+        if (hist) atomicAdd(&s_hist[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
+        if (stt[u] == 4u) {
+          const int64_t q = st0[u] - (t[u] + dl_of(k));
+          a.n4 += 1u;
+          add_moment(a.qs_lo, a.qs_hi, a.qq_lo, a.qq_hi, (uint64_t)q);
+          a.qmin = min(a.qmin, q);
+          a.qmax = max(a.qmax, q);
+          if (hist) atomicAdd(&s_hist[hist_bin(q)], 1u);
+        } else {
+          a.n5 += 1u;
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void write_rep_stats(fognet_rep_stats* S, const Acc& b) {
+  S->n_queued = (int64_t)b.n4;
+  S->n_started = (int64_t)b.n5;
+  S->last_tick = b.last;
+  S->queue_min_ticks = b.qmin;
+  S->queue_max_ticks = b.qmax;
+  S->resp_min_ticks = b.rmin;
+  S->resp_max_ticks = b.rmax;
+  S->queue_sum_lo = b.qs_lo;
+  S->queue_sum_hi = b.qs_hi;
+  S->queue_sq_lo = b.qq_lo;
+  S->queue_sq_hi = b.qq_hi;
+  S->resp_sum_lo = b.rs_lo;
+  S->resp_sum_hi = b.rs_hi;
+  S->resp_sq_lo = b.rq_lo;
+  S->resp_sq_hi = b.rq_hi;
+  S->busy_s = (int64_t)b.busy;
+  S->energy_j = 0.0;
+}
+
+// Builder-defined statistics of the north star, after the accumulation (and a
+// barrier): histogram counts added into the job histogram, and node energy
+// E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12) with IEEE-rounded
+// products and sums (no contraction), summed in node order by thread 0.
+// Per-node service seconds are integers, so only these final steps round.
+__device__ __forceinline__ void stats_finish(const ReplayArgs& A, int r, int64_t H, fognet_rep_stats* S,
+                                             const unsigned long long* s_busy, double* s_e, const uint32_t* s_hist,
+                                             int tid, int nth) {
+  const size_t nbase = (size_t)r * (size_t)A.node_stride;
+  if (A.hist) {
+    for (int h = tid; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += nth)
+      if (s_hist[h]) atomicAdd((unsigned long long*)&A.hist[h], (unsigned long long)s_hist[h]);
+  }
+  if (A.p_busy) {
+    for (int j = tid; j < A.N; j += nth) {
+      const int64_t B = (int64_t)s_busy[j];
+      const double eb = __dmul_rn(A.p_busy[nbase + j], (double)B);
+      const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
+      const double e = __dadd_rn(eb, __dmul_rn(A.p_idle[nbase + j], idle));
+      s_e[j] = e;
+      if (A.out_energy) A.out_energy[(size_t)r * (size_t)A.N + j] = e;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double sum = 0.0;
+      for (int j = 0; j < A.N; ++j) sum = __dadd_rn(sum, s_e[j]);
+      S->energy_j = sum;
+    }
+  }
+}
+
 template <int NPL, int POL>
 // 4 waves per SIMD (<= 128 VGPRs): 16 replications resident per CU, so the
 // 4096-replication sweep runs in a single wave of workgroups on 256 CUs.
@@ -877,53 +1058,36 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     S->resp_sum_lo = p_pk0;
 #endif
   }
-}
-
-// ---------------------------------------------------------------- statistics
-// Exact per-replication statistics from the replay outputs: queueTime
-// (ComputeBrokerApp3.cc:238) over queued tasks, response (done - publish
-// arrival) over all tasks.  128-bit integer sums: bit-identical for any
-// summation order.
-
-struct Acc {
-  uint64_t n4, n5, busy;
-  uint64_t qs_lo, qs_hi, qq_lo, qq_hi, rs_lo, rs_hi, rq_lo, rq_hi;
-  int64_t qmin, qmax, rmin, rmax, last;
-};
-
-__device__ __forceinline__ void add128(uint64_t& lo, uint64_t& hi, uint64_t vlo, uint64_t vhi) {
-  const uint64_t o = lo;
-  lo += vlo;
-  hi += vhi + (lo < o ? 1u : 0u);
-}
-
-__device__ __forceinline__ void add_moment(uint64_t& slo, uint64_t& shi, uint64_t& qlo, uint64_t& qhi,
-                                           uint64_t v) {
-  add128(slo, shi, v, 0u);
-  add128(qlo, qhi, v * v, __umul64hi(v, v));
-}
-
-__device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
-  a.n4 += b.n4;
-  a.n5 += b.n5;
-  a.busy += b.busy;
-  add128(a.qs_lo, a.qs_hi, b.qs_lo, b.qs_hi);
-  add128(a.qq_lo, a.qq_hi, b.qq_lo, b.qq_hi);
-  add128(a.rs_lo, a.rs_hi, b.rs_lo, b.rs_hi);
-  add128(a.rq_lo, a.rq_hi, b.rq_lo, b.rq_hi);
-  a.qmin = min(a.qmin, b.qmin);
-  a.qmax = max(a.qmax, b.qmax);
-  a.rmin = min(a.rmin, b.rmin);
-  a.rmax = max(a.rmax, b.rmax);
-  a.last = max(a.last, b.last);
+#if !defined(FOGNET_REPLAY_PROFILE) || FOGNET_REPLAY_PROFILE == 0
+  if (A.fuse_stats && A.out_stats) {
+    // ---- statistics epilogue (rep_stats_kernel's pass, fused).  The wave
+    // re-reads its own replication's outputs; task c0 + l was stored by lane
+    // l, and lane l reads tasks l, l + 64, ... (its own stores).  The loop's
+    // tail-state LDS is dead now and holds the pass's scratch.
+    unsigned long long* e_busy = reinterpret_cast<unsigned long long*>(s_tld);  // [NPL*64] u64
+    double* e_e = reinterpret_cast<double*>(s_ul);                              // [NPL*64] f64
+    uint32_t* e_hist = s_ch;                                                    // 192 >= 2*64 u32
+    static_assert(3 * kWave >= FOGNET_HIST_METRICS * FOGNET_HIST_BINS, "histogram fits the chunk stage");
+    if (A.p_busy)
+      for (int j = lane; j < NPL * kWave; j += kWave) e_busy[j] = 0ull;
+    if (A.hist)
+      for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) e_hist[h] = 0u;
+    __syncthreads();
+    Acc acc = acc_identity();
+    stats_accumulate<4>(A, tbase, (int)n_done, lane, kWave, acc, e_busy, e_hist, [&](int k) { return s_dl[k]; });
+    acc = wave_merge(acc);
+    __syncthreads();
+    fognet_rep_stats* S = A.out_stats + r;
+    if (lane == 0) write_rep_stats(S, acc);
+    stats_finish(A, r, n_done > 0 ? acc.last : 0, S, e_busy, e_e, e_hist, lane, kWave);
+  }
+#endif
 }
 
 constexpr int kStatThreads = 256;
 
-// Also the builder-defined statistics of the north star: latency histograms
-// (FOGNET_HIST_BINS, integer counts added into the job histogram) and node
-// energy (fognet_rep_stats.energy_j: per-node service seconds are integers,
-// so only the final per-node products and the index-ordered sum round).
+// Standalone statistics pass over the replay outputs (fognet_rep_stats_dev);
+// fognet_run_batch_dev fuses the same pass into replay_kernel instead.
 __global__ __launch_bounds__(kStatThreads) void rep_stats_kernel(ReplayArgs A) {
   const int r = blockIdx.x;
   __shared__ Acc s_acc[kStatThreads];
@@ -934,89 +1098,20 @@ __global__ __launch_bounds__(kStatThreads) void rep_stats_kernel(ReplayArgs A) {
   const int32_t n = (int32_t)S->n_tasks;  // written by replay_kernel
   const size_t tbase = (size_t)r * (size_t)A.T;
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
-  const bool energy = A.p_busy != nullptr;
-  const bool hist = A.hist != nullptr;
   for (int j = threadIdx.x; j < kWave * kMaxNodesPerLane; j += kStatThreads) s_busy[j] = 0ull;
   for (int h = threadIdx.x; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kStatThreads) s_hist[h] = 0u;
   __syncthreads();
-  Acc a = {};
-  a.qmin = a.rmin = INT64_MAX;
-  a.qmax = a.rmax = a.last = INT64_MIN;
-  for (int i = threadIdx.x; i < n; i += kStatThreads) {
-    const int64_t t = A.arrive[tbase + i];
-    const int32_t k = A.out_node[tbase + i];
-    const uint8_t stt = A.out_status[tbase + i];
-    const int64_t st0 = A.out_start[tbase + i];
-    const int64_t dn = A.out_done[tbase + i];
-    const int64_t resp = dn - t;
-    const uint64_t svc = (uint64_t)(dn - st0) / (uint64_t)kTicksPerSecond;  // whole seconds
-    a.busy += svc;
-    if (energy) atomicAdd(&s_busy[k], (unsigned long long)svc);
-    add_moment(a.rs_lo, a.rs_hi, a.rq_lo, a.rq_hi, (uint64_t)resp);
-    a.rmin = min(a.rmin, resp);
-    a.rmax = max(a.rmax, resp);
-    a.last = max(a.last, dn);
-    if (hist) atomicAdd(&s_hist[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
-    if (stt == 4) {
-      const int64_t q = st0 - (t + A.dl[nbase + k]);
-      a.n4 += 1u;
-      add_moment(a.qs_lo, a.qs_hi, a.qq_lo, a.qq_hi, (uint64_t)q);
-      a.qmin = min(a.qmin, q);
-      a.qmax = max(a.qmax, q);
-      if (hist) atomicAdd(&s_hist[hist_bin(q)], 1u);
-    } else {
-      a.n5 += 1u;
-    }
-  }
+  Acc a = acc_identity();
+  stats_accumulate<2>(A, tbase, n, threadIdx.x, kStatThreads, a, s_busy, s_hist,
+                      [&](int k) { return A.dl[nbase + k]; });
   s_acc[threadIdx.x] = a;
   __syncthreads();
   for (int w = kStatThreads / 2; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) acc_merge(s_acc[threadIdx.x], s_acc[threadIdx.x + w]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    const Acc& b = s_acc[0];
-    S->n_queued = (int64_t)b.n4;
-    S->n_started = (int64_t)b.n5;
-    S->last_tick = b.last;
-    S->queue_min_ticks = b.qmin;
-    S->queue_max_ticks = b.qmax;
-    S->resp_min_ticks = b.rmin;
-    S->resp_max_ticks = b.rmax;
-    S->queue_sum_lo = b.qs_lo;
-    S->queue_sum_hi = b.qs_hi;
-    S->queue_sq_lo = b.qq_lo;
-    S->queue_sq_hi = b.qq_hi;
-    S->resp_sum_lo = b.rs_lo;
-    S->resp_sum_hi = b.rs_hi;
-    S->resp_sq_lo = b.rq_lo;
-    S->resp_sq_hi = b.rq_hi;
-    S->busy_s = (int64_t)b.busy;
-    S->energy_j = 0.0;
-  }
-  if (hist) {
-    for (int h = threadIdx.x; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kStatThreads)
-      if (s_hist[h]) atomicAdd((unsigned long long*)&A.hist[h], (unsigned long long)s_hist[h]);
-  }
-  if (energy) {
-    // E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12), IEEE-rounded
-    // products and sums (no contraction), summed in node order by one thread.
-    const int64_t H = n > 0 ? s_acc[0].last : 0;
-    for (int j = threadIdx.x; j < A.N; j += kStatThreads) {
-      const int64_t B = (int64_t)s_busy[j];
-      const double eb = __dmul_rn(A.p_busy[nbase + j], (double)B);
-      const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
-      const double e = __dadd_rn(eb, __dmul_rn(A.p_idle[nbase + j], idle));
-      s_e[j] = e;
-      if (A.out_energy) A.out_energy[(size_t)r * (size_t)A.N + j] = e;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double sum = 0.0;
-      for (int j = 0; j < A.N; ++j) sum = __dadd_rn(sum, s_e[j]);
-      S->energy_j = sum;
-    }
-  }
+  if (threadIdx.x == 0) write_rep_stats(S, s_acc[0]);
+  stats_finish(A, r, n > 0 ? s_acc[0].last : 0, S, s_busy, s_e, s_hist, threadIdx.x, kStatThreads);
 }
 
 }  // namespace

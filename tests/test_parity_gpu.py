@@ -319,6 +319,27 @@ def test_energy_and_histograms_match_oracle(ctx, shared):
     np.testing.assert_allclose(float(job["energy_j"]), float(o["stats"]["energy_j"].sum()), rtol=1e-12)
 
 
+@pytest.mark.parametrize("N,T", [(7, 1500), (64, 1000), (130, 2111), (256, 3000)])
+def test_fused_statistics_equal_separate_pass(ctx, N, T):
+    """fognet_run_batch_dev runs the statistics pass as the replay kernel's
+    epilogue; fognet_replay_dev + fognet_rep_stats_dev run it as its own
+    kernel.  Same record, histogram and per-node energy, bit for bit."""
+    tr = tg.make_batch(0x5EED0077 + N, 5, N, T, sweep=True)
+    pb, pi = fa.power_model(tr["mips"])
+    tr = dict(tr, p_busy=pb, p_idle=pi)
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(tr, dev)
+    fused = fa.run_batch(ctx, d, hist=True)
+    sep = fa.allocate_outputs(5, T, dev, N=N, energy=True, hist=True)
+    fa.run_batch(ctx, d, out=sep, stage="replay")
+    fa.run_batch(ctx, d, out=sep, stage="stats")
+    torch.cuda.synchronize()
+    assert fused.stats.cpu().numpy().tobytes() == sep.stats.cpu().numpy().tobytes()
+    np.testing.assert_array_equal(fused.hist.cpu().numpy(), sep.hist.cpu().numpy())
+    np.testing.assert_array_equal(fused.node_energy.cpu().numpy(), sep.node_energy.cpu().numpy())
+    assert int(fused.hist.cpu().numpy()[1].sum()) == 5 * T
+
+
 def test_histogram_accumulates_across_calls(ctx):
     tr = tg.make_batch(3, 4, 32, 1000)
     dev = torch.device("cuda", ctx.device)
