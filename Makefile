@@ -4,9 +4,10 @@ ARCH ?= gfx950
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 SRC_DIR := fognetsimpp_amd/csrc
 SRCS := $(SRC_DIR)/capi.hip $(SRC_DIR)/replay.hip $(SRC_DIR)/decide.hip $(SRC_DIR)/tracegen.hip
-HDRS := include/fognet_hip.h $(SRC_DIR)/internal.h
+HDRS := include/fognet_hip.h include/fognet_io.h $(SRC_DIR)/internal.h
 OBJDIR := build/obj
-OBJS := $(patsubst $(SRC_DIR)/%.hip,$(OBJDIR)/%.o,$(SRCS))
+OBJS := $(patsubst $(SRC_DIR)/%.hip,$(OBJDIR)/%.o,$(SRCS)) $(OBJDIR)/io.o
+HOSTCXX ?= g++
 LIB := fognetsimpp_amd/libfognet_hip.so
 
 all: $(LIB) oracle
@@ -14,6 +15,10 @@ all: $(LIB) oracle
 $(OBJDIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o $@
+
+$(OBJDIR)/io.o: $(SRC_DIR)/io.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HOSTCXX) -O2 -std=c++17 -fPIC -Wall -Iinclude -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
@@ -36,8 +41,8 @@ clean:
 PROF_LIB := build/prof/libfognet_hip.so
 prof: $(SRCS) $(HDRS)
 	@mkdir -p build/prof
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DFOGNET_REPLAY_PROFILE=1 -Iinclude -shared -o $(PROF_LIB) $(SRCS)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DFOGNET_REPLAY_PROFILE=1 -Iinclude -shared -o $(PROF_LIB) $(SRCS) $(SRC_DIR)/io.cpp
 	@mkdir -p build/prof2
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DFOGNET_REPLAY_PROFILE=2 -Iinclude -shared -o build/prof2/libfognet_hip.so $(SRCS)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DFOGNET_REPLAY_PROFILE=2 -Iinclude -shared -o build/prof2/libfognet_hip.so $(SRCS) $(SRC_DIR)/io.cpp
 
 .PHONY: prof

@@ -26,7 +26,7 @@ FOGNET_ERR_UNSUPPORTED = 8
 FOGNET_POLICY_REF_V3 = 1
 FOGNET_POLICY_EXT_LAT = 16
 TICKS_PER_SECOND = 10**12
-ABI_VERSION = 2
+ABI_VERSION = 3
 HIST_METRICS = 2  # 0 queueTime, 1 response
 HIST_BINS = 64
 
@@ -101,7 +101,18 @@ class GenParams(C.Structure):
                 ("mean_gap_ticks", C.c_void_p), ("lat_scale", C.c_void_p)]
 
 
-# name -> (restype, argtypes); every function declared in include/fognet_hip.h
+TRACE_NOTE_BYTES = 160
+TRACE_FLAG_POWER = 1
+TRACE_FLAG_NODE_ID = 2
+
+
+class TraceInfo(C.Structure):
+    _fields_ = [("R", C.c_int32), ("T", C.c_int32), ("N", C.c_int32), ("node_stride", C.c_int32),
+                ("flags", C.c_uint32), ("version", C.c_uint32), ("payload_bytes", C.c_uint64),
+                ("checksum", C.c_uint64), ("note", C.c_char * TRACE_NOTE_BYTES)]
+
+
+# name -> (restype, argtypes); every function declared in include/*.h
 P = C.c_void_p
 SIGNATURES = {
     "fognet_abi_version": (C.c_int, []),
@@ -118,9 +129,19 @@ SIGNATURES = {
     "fognet_reduce_stats_dev": (C.c_int, [P, P, C.c_int32, P, P]),
     "fognet_job_stats_init": (None, [C.POINTER(JobStats)]),
     "fognet_job_stats_merge": (None, [C.POINTER(JobStats), C.POINTER(JobStats)]),
+    "fognet_job_stats_add_rep": (None, [C.POINTER(JobStats), C.POINTER(RepStats)]),
     "fognet_gen_trace_dev": (C.c_int, [P, C.POINTER(GenParams), C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                        P, P, P, P, P, P, P]),
     "fognet_sync": (C.c_int, [P]),
+    # include/fognet_io.h (host only, no context)
+    "fognet_io_last_error": (C.c_char_p, []),
+    "fognet_trace_write": (C.c_int, [C.c_char_p, C.POINTER(BatchIn), P, C.c_char_p]),
+    "fognet_trace_info_read": (C.c_int, [C.c_char_p, C.POINTER(TraceInfo)]),
+    "fognet_trace_read": (C.c_int, [C.c_char_p, C.POINTER(BatchIn), P]),
+    "fognet_write_sca": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(JobStats), P]),
+    "fognet_write_vec": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int32, C.c_int32, P, P, P, P, P, P]),
+    "fognet_gen_trace_mqtt": (C.c_int, [C.c_uint32, C.c_int32, P, P, P, P, C.c_int64, C.c_int32, C.c_int32,
+                                        C.c_int32, P, P, P, C.POINTER(C.c_int32)]),
 }
 
 _lib = None

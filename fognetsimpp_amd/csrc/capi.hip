@@ -380,6 +380,38 @@ void fognet_job_stats_merge(fognet_job_stats* a, const fognet_job_stats* b) {
   add192_host(a->resp_sq, b->resp_sq);
 }
 
+void fognet_job_stats_add_rep(fognet_job_stats* a, const fognet_rep_stats* s) {
+  if (!a || !s) return;
+  a->n_reps += 1;
+  if (s->status != FOGNET_OK) {
+    a->n_failed += 1;
+    return;
+  }
+  fognet_job_stats b;
+  fognet_job_stats_init(&b);
+  b.n_tasks = s->n_tasks;
+  b.n_queued = s->n_queued;
+  b.n_started = s->n_started;
+  b.events = s->events;
+  b.last_tick = s->last_tick;
+  b.queue_min_ticks = s->queue_min_ticks;
+  b.queue_max_ticks = s->queue_max_ticks;
+  b.resp_min_ticks = s->resp_min_ticks;
+  b.resp_max_ticks = s->resp_max_ticks;
+  b.max_pending = s->max_pending;
+  b.busy_s = s->busy_s;
+  b.energy_j = s->energy_j;
+  b.queue_sum[0] = s->queue_sum_lo;
+  b.queue_sum[1] = s->queue_sum_hi;
+  b.queue_sq[0] = s->queue_sq_lo;
+  b.queue_sq[1] = s->queue_sq_hi;
+  b.resp_sum[0] = s->resp_sum_lo;
+  b.resp_sum[1] = s->resp_sum_hi;
+  b.resp_sq[0] = s->resp_sq_lo;
+  b.resp_sq[1] = s->resp_sq_hi;
+  fognet_job_stats_merge(a, &b);
+}
+
 int fognet_gen_trace_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t r0, int32_t R, int32_t T, int32_t N,
                          int64_t* arrive_tick, int32_t* req_mips, int32_t* mips, int64_t* dl_tick, int64_t* ul_tick,
                          int64_t* init_adv_tick, void* stream) {

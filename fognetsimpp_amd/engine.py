@@ -220,6 +220,18 @@ def merge_job_stats(records) -> np.ndarray:
     return np.frombuffer(bytes(acc), dtype=_abi.JOB_STATS_DTYPE)[0]
 
 
+def job_from_reps(reps) -> np.ndarray:
+    """Exact host reduction of per-replication records (REP_STATS_DTYPE) into a
+    job record (fognet_job_stats_add_rep, the host twin of fognet_reduce_stats_dev)."""
+    lib = _abi.load()
+    acc = _abi.JobStats()
+    lib.fognet_job_stats_init(C.byref(acc))
+    for rec in np.atleast_1d(reps):
+        b = _abi.RepStats.from_buffer_copy(np.ascontiguousarray(rec).tobytes())
+        lib.fognet_job_stats_add_rep(C.byref(acc), C.byref(b))
+    return np.frombuffer(bytes(acc), dtype=_abi.JOB_STATS_DTYPE)[0]
+
+
 def _u192(limbs) -> int:
     return int(limbs[0]) | (int(limbs[1]) << 64) | (int(limbs[2]) << 128)
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FOGNET_ABI_VERSION 2
+#define FOGNET_ABI_VERSION 3
 #define FOGNET_TICKS_PER_SECOND 1000000000000LL
 
 /* Latency histograms (device-side statistics, summed over replications; the
@@ -195,6 +195,10 @@ int fognet_reduce_stats_dev(fognet_ctx *ctx, const fognet_rep_stats *stats, int3
  * *acc = *acc (+) *other.  fognet_job_stats_init() sets the identity. */
 void fognet_job_stats_init(fognet_job_stats *s);
 void fognet_job_stats_merge(fognet_job_stats *acc, const fognet_job_stats *other);
+/* Host-side exact accumulate of one replication (what fognet_reduce_stats_dev
+ * does per replication; energy is added in call order): for callers of the
+ * host-buffer fognet_run_batch. */
+void fognet_job_stats_add_rep(fognet_job_stats *acc, const fognet_rep_stats *rep);
 
 /* Device trace generator: fills arrive/req [R][T] and node params [R][N]
  * (replications r0 .. r0+R-1 of the recipe; r0 lets GPUs shard one job). */
