@@ -10,13 +10,18 @@ reduction; with N > 1 ranks also the all-gather of the job record and the
 RCCL all-reduce of histograms + energy.  Replications are sharded over ranks
 (weak scaling; no data-path collective).
 
+``--workload c5`` runs config C5 (large topology, BASELINE.json configs[4]):
+1024 replications in total x T = 10,000 x N = 10,000 fog nodes, sharded over
+the ranks (strong scaling), on the wide replay kernel (replay_wide.hip), with
+the builder-defined light-load recipe of ``fognetsimpp_amd.c5_params``.
+
 ``--workload c4`` runs config C4 (Monte Carlo what-if, BASELINE.json
 configs[3]): 1M replications x T = 10,000 x N = 256 in total, sharded over the
 ranks (strong scaling), traces generated on the device INSIDE the timed
 region in blocks of ``--block`` replications (the whole trace would be
 ~120 GB), only statistics kept.
 
-  python bench.py [--gpus N --steps K --warmup W] [--workload c3|c4]
+  python bench.py [--gpus N --steps K --warmup W] [--workload c3|c4|c5]
   torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -66,15 +71,23 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--policy", default="REF_V3", choices=("REF_V3", "EXT_LAT"))
-    ap.add_argument("--workload", default="c3", choices=("c3", "c4"))
-    ap.add_argument("--R-total", type=int, default=1_000_000, help="c4: replications over all ranks")
+    ap.add_argument("--workload", default="c3", choices=("c3", "c4", "c5"))
+    ap.add_argument("--R-total", type=int, default=None,
+                    help="c4/c5: replications over all ranks (default 1,000,000 / 1024)")
     ap.add_argument("--block", type=int, default=4096, help="c4: replications per device block")
     args = ap.parse_args()
-    if args.workload == "c4":
+    if args.workload in ("c4", "c5"):
         if args.T == 100_000:
             args.T = 10_000
         if args.seed == 0x5EED0003:
-            args.seed = 0x5EED0004
+            args.seed = 0x5EED0004 if args.workload == "c4" else 0x5EED0005
+        if args.R_total is None:
+            args.R_total = 1_000_000 if args.workload == "c4" else 1024
+    if args.workload == "c5":
+        if args.N == 256:
+            args.N = 10_000
+        if args.cpu_reps == 1024:
+            args.cpu_reps = 64
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -91,9 +104,15 @@ def main():
     ctx = fa.Context(local)
     if args.workload == "c4":
         return bench_c4(args, ctx, dev, dist, world, rank)
-    R, T, N = args.R, args.T, args.N
-    r0 = rank * R  # contiguous shard of the global replication index space
-    mg, sc = fa.sweep_params(np.arange(r0, r0 + R), N)
+    T, N = args.T, args.N
+    if args.workload == "c5":  # a fixed job split over the ranks
+        from fognetsimpp_amd.dist import shard
+        r0, R = shard(args.R_total, world, rank)
+        mg, sc = fa.c5_params(np.arange(r0, r0 + R), N)
+    else:  # C3: R replications per rank, contiguous blocks of the global index
+        R = args.R
+        r0 = rank * R
+        mg, sc = fa.sweep_params(np.arange(r0, r0 + R), N)
     t0 = time.time()
     trace = fa.generate_trace(ctx, args.seed, R, T, N, mg, sc, r0=r0)
     pb, pi = fa.power_model(trace["mips"].cpu().numpy())
@@ -156,7 +175,7 @@ def main():
     summary = fa.summarize(job)
     hist = out.hist.cpu().numpy()
 
-    decisions = world * R * T * args.steps
+    decisions = (args.R_total if args.workload == "c5" else world * R) * T * args.steps
     value = decisions / elapsed
     bpd = algorithmic_bytes_per_decision(T, N)
     achieved_gbs = R * T * bpd / replay_avg_s / 1e9
@@ -185,18 +204,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.workload == "c5" else "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (device-generated Philox traces, C3 policy-sweep recipe)",
-            "config": {"workload": "C3 policy sweep (BASELINE.json configs[2])", "R_per_gpu": R, "T": T, "N": N,
-                       "R_total": R * world, "ring_capacity": args.ring,
+            "data": "synthetic (device-generated Philox traces, "
+                    + ("C5 light-load recipe)" if args.workload == "c5" else "C3 policy-sweep recipe)"),
+            "config": {"workload": "C5 large topology (BASELINE.json configs[4])" if args.workload == "c5"
+                       else "C3 policy sweep (BASELINE.json configs[2])", "R_per_gpu": R, "T": T, "N": N,
+                       "R_total": args.R_total if args.workload == "c5" else R * world, "ring_capacity": args.ring,
                        "policy": "REF_V3 (BrokerBaseApp3)" if args.policy == "REF_V3" else
                        "EXT_LAT (north-star cost; not in the reference)",
                        "parallelism": f"replications sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "replay_kernel (statistics pass fused)", "kernel_avg_ms": replay_avg_s * 1e3,
+                         "kernel": ("replay_wide_kernel (statistics inline)" if N > 256
+                                    else "replay_kernel (statistics pass fused)"), "kernel_avg_ms": replay_avg_s * 1e3,
                          "bytes_per_decision": bpd},
             "cpu_baseline": cpu,
             "failed_replications": failed,

@@ -3,6 +3,7 @@
 // decision is evaluated on the device, and the library refuses to create a
 // context without a gfx950 GPU.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -58,8 +59,8 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   if (!in) return fail(c, FOGNET_ERR_ARG, "null batch");
   if (in->R < 0 || in->T < 0 || in->N < 0) return fail(c, FOGNET_ERR_ARG, "negative R/T/N");
   if (in->N == 0) return fail(c, FOGNET_ERR_NO_NODES, "N == 0 (BrokerBaseApp3.cc:268 reads brokers[0])");
-  if (in->N > fognet::kWave * fognet::kMaxNodesPerLane)
-    return fail(c, FOGNET_ERR_UNSUPPORTED, "N > 256 not supported by the register-resident replay kernel");
+  if (in->N > fognet::kWideMaxNodes)
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "N > 13568 (the wide replay kernel keeps 12 B per node in 160 KiB of LDS)");
   if (in->policy != FOGNET_POLICY_REF_V3 && in->policy != FOGNET_POLICY_EXT_LAT)
     return fail(c, FOGNET_ERR_UNSUPPORTED, "unknown policy");
   if ((in->p_busy_w == nullptr) != (in->p_idle_w == nullptr))
@@ -96,6 +97,14 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   a->p_busy = in->p_busy_w;
   a->p_idle = in->p_idle_w;
   return FOGNET_OK;
+}
+
+// N > 256 takes the wide replay kernel (replay_wide.hip); FOGNET_REPLAY_KERNEL=wide
+// forces it for any N (used by the parity tests to check both kernels).
+bool use_wide(int32_t N) {
+  if (N > fognet::kWave * fognet::kMaxNodesPerLane) return true;
+  const char* f = getenv("FOGNET_REPLAY_KERNEL");
+  return f != nullptr && strcmp(f, "wide") == 0;
 }
 
 }  // namespace
@@ -223,6 +232,16 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
   a.hist = out->hist;
   if (a.out_energy && !a.p_busy) return fail(c, FOGNET_ERR_ARG, "node_energy_j needs the power model (p_busy_w/p_idle_w)");
   hipError_t e = hipSuccess;
+  if (use_wide(a.N)) {
+    // the wide kernel accumulates the statistics while it replays, so the
+    // statistics-only stage has nothing left to do
+    if (!(which & 1)) return FOGNET_OK;
+    const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N);
+    rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ws, "wide replay workspace");
+    if (rc) return rc;
+    e = fognet::launch_replay_wide(a, c->ring, (hipStream_t)stream);
+    return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "wide replay launch");
+  }
   // both stages: the replay kernel runs the statistics pass as its epilogue
   a.fuse_stats = which == 3 ? 1 : 0;
   if (a.fuse_stats) which = 1;

@@ -184,6 +184,33 @@ __device__ __forceinline__ int hist_bin(int64_t ticks) {
   return b > FOGNET_HIST_BINS - 1 ? FOGNET_HIST_BINS - 1 : b;
 }
 
+// Wide replay (replay_wide.hip, N > 256): the pending-task chain of a node is
+// linked through per-task entries instead of a fixed per-node ring.
+struct WideEntry {
+  int64_t a;     // arrival tick at the node
+  int64_t done;  // completion (RELEASERESOURCE) tick
+  uint64_t C;    // cumulative service seconds assigned to the node, this task included
+  uint32_t S;    // service seconds, requiredMIPS / MIPS (int division)
+  int32_t prev;  // previous task on the same node (-1: none)
+  int32_t next;  // next task on the same node (valid while this one is pending)
+  int32_t pad;
+};
+static_assert(sizeof(WideEntry) == 40, "wide entry is 40 B");
+
+struct WideNode {
+  int32_t hd, tl;  // oldest pending / newest task of the node (-1: none yet)
+  int32_t npend;   // tasks whose completion advert has not reached the broker
+  int32_t pad;
+};
+
+// LDS of the wide kernel: 12 B per node (next advert tick, advertised busy)
+// + the histogram; a single workgroup may use all 160 KiB on gfx950.
+constexpr int kWideMaxNodes = 13568;
+size_t replay_wide_lds_bytes(int32_t N);
+// workspace: R*T WideEntry followed by R*N WideNode
+size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N);
+hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, hipStream_t s);
+
 hipError_t launch_replay(const ReplayArgs& a, hipStream_t s);
 hipError_t launch_rep_stats(const ReplayArgs& a, hipStream_t s);
 hipError_t launch_reduce_stats(const fognet_rep_stats* st, int32_t R, fognet_job_stats* out,

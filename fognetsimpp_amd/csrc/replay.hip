@@ -30,7 +30,7 @@
 // advert that could change the decision (run horizon), then pushes the whole
 // run (up to the 64 publishes of a trace chunk, one per lane) with a (max,+)
 // scan over the FIFO recurrence and coalesced ring and output stores.
-#include "internal.h"
+#include "replay_common.h"
 
 namespace fognet {
 
@@ -70,10 +70,6 @@ struct Slot {
 #endif
 
 constexpr uint32_t kNoKey = ~0u;
-constexpr int64_t kNever = INT64_MAX;
-// Simulated ticks are kept below 2^61 (26.7 days) and service times below
-// 2^16 s, so no intermediate of the run scan can overflow int64.
-constexpr int64_t kMaxTick = (int64_t)1 << 61;
 
 __device__ __forceinline__ uint32_t n_push(const Slot& st) { return st.cnt & 0xFFFFu; }
 __device__ __forceinline__ uint32_t n_head(const Slot& st) { return st.cnt >> 16; }
@@ -308,18 +304,6 @@ __device__ __forceinline__ void wait_vm(uint32_t m) {
       : "scc", "memory");
 }
 
-// S seconds in ticks: S * 1e12 = (S * 5^12) << 12, one v_mad_u64_u32 + shift.
-__device__ __forceinline__ int64_t ticks_of(uint32_t s) {
-  static_assert(kTicksPerSecond == 244140625ll << 12, "1e12 ticks per second");
-  return (int64_t)(((uint64_t)s * 244140625u) << 12);
-}
-
-// arrival at tick `a` happens before the completion at `done` of a task with
-// service S on a node with downlink latency dl (FES insertion-order rule).
-__device__ __forceinline__ bool arrives_before(int64_t a, int64_t done, int64_t dl, uint32_t S) {
-  return a < done || (a == done && dl >= (int64_t)S * kTicksPerSecond);
-}
-
 // Cumulative service of the tasks that reached the node before the
 // completion (tick `done`, service S) of pending entry head+d0; scans back
 // from the newest assignment.  c_self: cumulative service of that entry.
@@ -439,8 +423,6 @@ __device__ __forceinline__ uint32_t view_min(const Slot (&st)[NPL]) {
 // argmin over j of dl_j + (busy_j + min(req / mips_j, 2^20)) * 1e12 in uint64
 // ticks (dl_j < 2^50 and busy_j < 2^24 keep it below 2^64), ties -> lowest j.
 // The saturation never changes an admissible decision (service <= max_s < 2^16).
-constexpr uint32_t kExtSatS = 1u << 20;
-constexpr int64_t kExtMaxDl = (int64_t)1 << 50;
 
 template <int NPL>
 __device__ __forceinline__ uint32_t ext_argmin(const Slot (&st)[NPL], uint32_t req, const int32_t* s_mips,
@@ -477,83 +459,7 @@ __device__ __forceinline__ void run_scan_level(uint32_t& Cs, int64_t& Ac) {
 }
 
 // ---------------------------------------------------------------- statistics
-// Exact per-replication statistics from the replay outputs: queueTime
-// (ComputeBrokerApp3.cc:238) over queued tasks, response (done - publish
-// arrival) over all tasks.  128-bit integer sums are bit-identical for any
-// summation order, so the replay kernel's fused epilogue (one wave) and
-// rep_stats_kernel (256 threads) write the same record.
-
-struct Acc {
-  uint64_t n4, n5, busy;
-  uint64_t qs_lo, qs_hi, qq_lo, qq_hi, rs_lo, rs_hi, rq_lo, rq_hi;
-  int64_t qmin, qmax, rmin, rmax, last;
-};
-
-__device__ __forceinline__ Acc acc_identity() {
-  Acc a = {};
-  a.qmin = a.rmin = INT64_MAX;
-  a.qmax = a.rmax = a.last = INT64_MIN;
-  return a;
-}
-
-__device__ __forceinline__ void add128(uint64_t& lo, uint64_t& hi, uint64_t vlo, uint64_t vhi) {
-  const uint64_t o = lo;
-  lo += vlo;
-  hi += vhi + (lo < o ? 1u : 0u);
-}
-
-__device__ __forceinline__ void add_moment(uint64_t& slo, uint64_t& shi, uint64_t& qlo, uint64_t& qhi,
-                                           uint64_t v) {
-  add128(slo, shi, v, 0u);
-  add128(qlo, qhi, v * v, __umul64hi(v, v));
-}
-
-__device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
-  a.n4 += b.n4;
-  a.n5 += b.n5;
-  a.busy += b.busy;
-  add128(a.qs_lo, a.qs_hi, b.qs_lo, b.qs_hi);
-  add128(a.qq_lo, a.qq_hi, b.qq_lo, b.qq_hi);
-  add128(a.rs_lo, a.rs_hi, b.rs_lo, b.rs_hi);
-  add128(a.rq_lo, a.rq_hi, b.rq_lo, b.rq_hi);
-  a.qmin = min(a.qmin, b.qmin);
-  a.qmax = max(a.qmax, b.qmax);
-  a.rmin = min(a.rmin, b.rmin);
-  a.rmax = max(a.rmax, b.rmax);
-  a.last = max(a.last, b.last);
-}
-
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, kWave);
-  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, kWave);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// Butterfly merge over the 64 lanes of a wave: every lane ends with the total.
-__device__ __forceinline__ Acc wave_merge(Acc a) {
-#pragma unroll 1
-  for (int m = kWave / 2; m > 0; m >>= 1) {
-    Acc b;
-    b.n4 = shfl_xor_u64(a.n4, m);
-    b.n5 = shfl_xor_u64(a.n5, m);
-    b.busy = shfl_xor_u64(a.busy, m);
-    b.qs_lo = shfl_xor_u64(a.qs_lo, m);
-    b.qs_hi = shfl_xor_u64(a.qs_hi, m);
-    b.qq_lo = shfl_xor_u64(a.qq_lo, m);
-    b.qq_hi = shfl_xor_u64(a.qq_hi, m);
-    b.rs_lo = shfl_xor_u64(a.rs_lo, m);
-    b.rs_hi = shfl_xor_u64(a.rs_hi, m);
-    b.rq_lo = shfl_xor_u64(a.rq_lo, m);
-    b.rq_hi = shfl_xor_u64(a.rq_hi, m);
-    b.qmin = (int64_t)shfl_xor_u64((uint64_t)a.qmin, m);
-    b.qmax = (int64_t)shfl_xor_u64((uint64_t)a.qmax, m);
-    b.rmin = (int64_t)shfl_xor_u64((uint64_t)a.rmin, m);
-    b.rmax = (int64_t)shfl_xor_u64((uint64_t)a.rmax, m);
-    b.last = (int64_t)shfl_xor_u64((uint64_t)a.last, m);
-    acc_merge(a, b);
-  }
-  return a;
-}
+// The statistics pass over the replay outputs (Acc: replay_common.h).
 
 // Accumulate tasks i = i0, i0 + stride, ... < n of one replication into `a`
 // (plus the per-node service seconds s_busy and the histogram s_hist in LDS
@@ -604,26 +510,6 @@ __device__ __forceinline__ void stats_accumulate(const ReplayArgs& A, size_t tba
       }
     }
   }
-}
-
-__device__ __forceinline__ void write_rep_stats(fognet_rep_stats* S, const Acc& b) {
-  S->n_queued = (int64_t)b.n4;
-  S->n_started = (int64_t)b.n5;
-  S->last_tick = b.last;
-  S->queue_min_ticks = b.qmin;
-  S->queue_max_ticks = b.qmax;
-  S->resp_min_ticks = b.rmin;
-  S->resp_max_ticks = b.rmax;
-  S->queue_sum_lo = b.qs_lo;
-  S->queue_sum_hi = b.qs_hi;
-  S->queue_sq_lo = b.qq_lo;
-  S->queue_sq_hi = b.qq_hi;
-  S->resp_sum_lo = b.rs_lo;
-  S->resp_sum_hi = b.rs_hi;
-  S->resp_sq_lo = b.rq_lo;
-  S->resp_sq_hi = b.rq_hi;
-  S->busy_s = (int64_t)b.busy;
-  S->energy_j = 0.0;
 }
 
 // Builder-defined statistics of the north star, after the accumulation (and a

@@ -1,0 +1,153 @@
+// replay_common.h — device pieces shared by the two replay kernels:
+// replay.hip (N <= 256, node state in VGPRs) and replay_wide.hip (N <= 13,568,
+// node state in LDS + HBM).  Tick arithmetic, the FES same-tick rule and the
+// exact per-replication statistics accumulator.
+#pragma once
+
+#include "internal.h"
+
+namespace fognet {
+
+constexpr int64_t kNever = INT64_MAX;
+// Simulated ticks are kept below 2^61 (26.7 days) and service times below
+// 2^16 s, so no intermediate of the replay arithmetic can overflow int64.
+constexpr int64_t kMaxTick = (int64_t)1 << 61;
+
+// FOGNET_POLICY_EXT_LAT bounds (fognet_hip.h): service saturates at 2^20 s,
+// downlinks stay below 2^50 ticks.
+constexpr uint32_t kExtSatS = 1u << 20;
+constexpr int64_t kExtMaxDl = (int64_t)1 << 50;
+
+// S seconds in ticks: S * 1e12 = (S * 5^12) << 12, one v_mad_u64_u32 + shift.
+__device__ __forceinline__ int64_t ticks_of(uint32_t s) {
+  static_assert(kTicksPerSecond == 244140625ll << 12, "1e12 ticks per second");
+  return (int64_t)(((uint64_t)s * 244140625u) << 12);
+}
+
+// arrival at tick `a` happens before the completion at `done` of a task with
+// service S on a node with downlink latency dl (FES insertion-order rule,
+// DESIGN.md §3.3).
+__device__ __forceinline__ bool arrives_before(int64_t a, int64_t done, int64_t dl, uint32_t S) {
+  return a < done || (a == done && dl >= (int64_t)S * kTicksPerSecond);
+}
+
+// ---------------------------------------------------------------- statistics
+// Exact per-replication statistics: queueTime (ComputeBrokerApp3.cc:238) over
+// queued tasks, response (done - publish arrival) over all tasks.  128-bit
+// integer sums are bit-identical for any summation order, so every kernel that
+// accumulates them writes the same record.
+
+struct Acc {
+  uint64_t n4, n5, busy;
+  uint64_t qs_lo, qs_hi, qq_lo, qq_hi, rs_lo, rs_hi, rq_lo, rq_hi;
+  int64_t qmin, qmax, rmin, rmax, last;
+};
+
+__device__ __forceinline__ Acc acc_identity() {
+  Acc a = {};
+  a.qmin = a.rmin = INT64_MAX;
+  a.qmax = a.rmax = a.last = INT64_MIN;
+  return a;
+}
+
+__device__ __forceinline__ void add128(uint64_t& lo, uint64_t& hi, uint64_t vlo, uint64_t vhi) {
+  const uint64_t o = lo;
+  lo += vlo;
+  hi += vhi + (lo < o ? 1u : 0u);
+}
+
+__device__ __forceinline__ void add_moment(uint64_t& slo, uint64_t& shi, uint64_t& qlo, uint64_t& qhi,
+                                           uint64_t v) {
+  add128(slo, shi, v, 0u);
+  add128(qlo, qhi, v * v, __umul64hi(v, v));
+}
+
+__device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
+  a.n4 += b.n4;
+  a.n5 += b.n5;
+  a.busy += b.busy;
+  add128(a.qs_lo, a.qs_hi, b.qs_lo, b.qs_hi);
+  add128(a.qq_lo, a.qq_hi, b.qq_lo, b.qq_hi);
+  add128(a.rs_lo, a.rs_hi, b.rs_lo, b.rs_hi);
+  add128(a.rq_lo, a.rq_hi, b.rq_lo, b.rq_hi);
+  a.qmin = min(a.qmin, b.qmin);
+  a.qmax = max(a.qmax, b.qmax);
+  a.rmin = min(a.rmin, b.rmin);
+  a.rmax = max(a.rmax, b.rmax);
+  a.last = max(a.last, b.last);
+}
+
+// One task's contribution: response = done - publish tick t; queued tasks
+// (status 4) also their queueTime = start - arrival at the node a.
+__device__ __forceinline__ void acc_task(Acc& acc, int64_t t, int64_t a, int64_t start, int64_t done, uint32_t S,
+                                         uint32_t status) {
+  acc.busy += S;
+  const int64_t resp = done - t;
+  add_moment(acc.rs_lo, acc.rs_hi, acc.rq_lo, acc.rq_hi, (uint64_t)resp);
+  acc.rmin = min(acc.rmin, resp);
+  acc.rmax = max(acc.rmax, resp);
+  acc.last = max(acc.last, done);
+  if (status == 4u) {
+    const int64_t q = start - a;
+    acc.n4 += 1u;
+    add_moment(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, (uint64_t)q);
+    acc.qmin = min(acc.qmin, q);
+    acc.qmax = max(acc.qmax, q);
+  } else {
+    acc.n5 += 1u;
+  }
+}
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, kWave);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, kWave);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Butterfly merge over the 64 lanes of a wave: every lane ends with the total.
+__device__ __forceinline__ Acc wave_merge(Acc a) {
+#pragma unroll 1
+  for (int m = kWave / 2; m > 0; m >>= 1) {
+    Acc b;
+    b.n4 = shfl_xor_u64(a.n4, m);
+    b.n5 = shfl_xor_u64(a.n5, m);
+    b.busy = shfl_xor_u64(a.busy, m);
+    b.qs_lo = shfl_xor_u64(a.qs_lo, m);
+    b.qs_hi = shfl_xor_u64(a.qs_hi, m);
+    b.qq_lo = shfl_xor_u64(a.qq_lo, m);
+    b.qq_hi = shfl_xor_u64(a.qq_hi, m);
+    b.rs_lo = shfl_xor_u64(a.rs_lo, m);
+    b.rs_hi = shfl_xor_u64(a.rs_hi, m);
+    b.rq_lo = shfl_xor_u64(a.rq_lo, m);
+    b.rq_hi = shfl_xor_u64(a.rq_hi, m);
+    b.qmin = (int64_t)shfl_xor_u64((uint64_t)a.qmin, m);
+    b.qmax = (int64_t)shfl_xor_u64((uint64_t)a.qmax, m);
+    b.rmin = (int64_t)shfl_xor_u64((uint64_t)a.rmin, m);
+    b.rmax = (int64_t)shfl_xor_u64((uint64_t)a.rmax, m);
+    b.last = (int64_t)shfl_xor_u64((uint64_t)a.last, m);
+    acc_merge(a, b);
+  }
+  return a;
+}
+
+__device__ __forceinline__ void write_rep_stats(fognet_rep_stats* S, const Acc& b) {
+  S->n_queued = (int64_t)b.n4;
+  S->n_started = (int64_t)b.n5;
+  S->last_tick = b.last;
+  S->queue_min_ticks = b.qmin;
+  S->queue_max_ticks = b.qmax;
+  S->resp_min_ticks = b.rmin;
+  S->resp_max_ticks = b.rmax;
+  S->queue_sum_lo = b.qs_lo;
+  S->queue_sum_hi = b.qs_hi;
+  S->queue_sq_lo = b.qq_lo;
+  S->queue_sq_hi = b.qq_hi;
+  S->resp_sum_lo = b.rs_lo;
+  S->resp_sum_hi = b.rs_hi;
+  S->resp_sq_lo = b.rq_lo;
+  S->resp_sq_hi = b.rq_hi;
+  S->busy_s = (int64_t)b.busy;
+  S->energy_j = 0.0;
+}
+
+}  // namespace fognet

@@ -309,6 +309,21 @@ def sweep_params(r_global: np.ndarray, N: int, rho=None, lat_scale=None, req_lo=
     return mean_gap, sc
 
 
+def c5_params(r_global: np.ndarray, N: int, req_lo=1000, req_hi=64000):
+    """Per-replication (mean_gap_ticks, lat_scale) of the C5 large-topology
+    recipe (builder-defined: the reference has no C5 parameters):
+    rho = (0.002, 0.01, 0.05)[r % 3], latency x(1, 10, 100)[(r // 3) % 3].
+    Light loads: under REF_V3 the C3 loads herd all of T onto node 0 when N is
+    in the thousands (the stale view keeps every node at busy 0 until its first
+    completion advert), so C5 uses loads at which decisions spread over nodes."""
+    r_global = np.asarray(r_global, dtype=np.int64)
+    mg, sc = sweep_params(r_global, N, req_lo=req_lo, req_hi=req_hi)
+    rho = np.array((0.002, 0.01, 0.05))[r_global % 3]
+    mips = 1000.0 * (1 + (np.arange(N) % 4))
+    es = 0.5 * (req_lo + req_hi) * float(np.mean(1.0 / mips))
+    return es / (N * rho) * _abi.TICKS_PER_SECOND, sc
+
+
 def power_model(mips) -> tuple[np.ndarray, np.ndarray]:
     """Synthetic node power model for the a11 energy statistic (builder-defined;
     the reference has no fog-node energy model): busy power

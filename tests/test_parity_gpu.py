@@ -163,9 +163,10 @@ def test_ring_capacity_exceeded(ctx):
     assert_parity(tr, g, o)
 
 
+@pytest.mark.parametrize("N", [16, 300])  # register-resident and wide kernel
 @pytest.mark.parametrize("bad", ["unsorted", "neg_req", "mips0", "late_advert", "early_advert_send", "huge_service"])
-def test_precondition_errors(ctx, bad):
-    tr = tg.make_batch(5, 2, 16, 300)
+def test_precondition_errors(ctx, bad, N):
+    tr = tg.make_batch(5, 2, N, 300)
     tr = {k: v.copy() for k, v in tr.items()}
     if bad == "unsorted":
         tr["arrive"][1, 100] = tr["arrive"][1, 99] - 1
@@ -186,7 +187,7 @@ def test_precondition_errors(ctx, bad):
 
 
 def test_unsupported_sizes(ctx):
-    tr = tg.make_batch(5, 1, 257, 10)
+    tr = tg.make_batch(5, 1, 13569, 10)  # the wide kernel's LDS holds 12 B x 13,568 nodes
     with pytest.raises(fa.FognetError) as e:
         run_gpu(ctx, tr)
     assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED
@@ -319,7 +320,7 @@ def test_energy_and_histograms_match_oracle(ctx, shared):
     np.testing.assert_allclose(float(job["energy_j"]), float(o["stats"]["energy_j"].sum()), rtol=1e-12)
 
 
-@pytest.mark.parametrize("N,T", [(7, 1500), (64, 1000), (130, 2111), (256, 3000)])
+@pytest.mark.parametrize("N,T", [(7, 1500), (64, 1000), (130, 2111), (256, 3000), (300, 1500), (1000, 1200)])
 def test_fused_statistics_equal_separate_pass(ctx, N, T):
     """fognet_run_batch_dev runs the statistics pass as the replay kernel's
     epilogue; fognet_replay_dev + fognet_rep_stats_dev run it as its own
@@ -378,3 +379,92 @@ def test_ext_lat_latency_bound(ctx):
     tr["dl"][1, 2] = 2**50
     g = run_gpu_full(ctx, tr, policy="EXT_LAT")
     assert g["stats"]["status"][0] == 0 and g["stats"]["status"][1] == _abi.FOGNET_ERR_ARG
+
+
+# ------------------------------------------------------------------ wide replay kernel (N > 256, config C5)
+# replay_wide.hip restates the same closed form for node sets that do not fit
+# in registers; FOGNET_REPLAY_KERNEL=wide forces it for small N as well.
+
+# REF_V3 herds every publish onto the least-advertised node until its first
+# completion advert lands, so the C3 loads (rho 0.5..0.95) keep 10^3-10^4 nodes
+# on node 0 for the whole trace; light loads spread decisions over many nodes.
+@pytest.mark.parametrize("N,T,R,rho", [(257, 2000, 3, 0.8), (700, 3000, 3, 0.01), (4096, 4000, 2, 0.01),
+                                       (13568, 3000, 1, 0.002)])
+def test_wide_matches_oracle(ctx, N, T, R, rho):
+    tr = tg.make_batch(0x5EED0005 + N, R, N, T, rho=rho, lat_scale=10)
+    pb, pi = fa.power_model(tr["mips"])
+    tr = dict(tr, p_busy=pb, p_idle=pi)
+    g = run_gpu_full(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8,
+                     p_busy=pb, p_idle=pi, hist=True)
+    assert (o["stats"]["status"] == 0).all()
+    assert_parity(tr, g, o)
+    np.testing.assert_array_equal(g["energy"], o["node_energy"])
+    assert g["stats"].tobytes() == o["stats"].tobytes()
+    np.testing.assert_array_equal(g["hist"], o["hist"].sum(axis=0))
+
+
+@pytest.mark.parametrize("N", [1, 5, 64, 100, 256])
+def test_wide_kernel_forced_equals_register_kernel(ctx, monkeypatch, N):
+    tr = tg.make_batch(1000 + N, 3, N, 1500, rho=0.9)
+    narrow = run_gpu_full(ctx, tr, ring_capacity=4096)
+    monkeypatch.setenv("FOGNET_REPLAY_KERNEL", "wide")
+    wide = run_gpu_full(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=3, hist=True)
+    assert_parity(tr, wide, o)
+    assert wide["stats"].tobytes() == narrow["stats"].tobytes()
+    np.testing.assert_array_equal(wide["hist"], narrow["hist"])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_wide_tie_heavy(ctx, monkeypatch, seed):
+    tr = tie_heavy(seed, 8, 1 + 37 * seed, 2000)
+    monkeypatch.setenv("FOGNET_REPLAY_KERNEL", "wide")
+    g = run_gpu(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8)
+    assert_parity(tr, g, o)
+
+
+def test_wide_tie_heavy_many_nodes(ctx):
+    tr = tie_heavy(77, 4, 600, 3000)
+    g = run_gpu(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=4)
+    assert_parity(tr, g, o)
+
+
+@pytest.mark.parametrize("N", [300, 2000])
+def test_wide_ext_lat_matches_oracle(ctx, N):
+    tr = tg.make_batch(4343 + N, 3, N, 1500, sweep=True)
+    g = run_gpu_full(ctx, tr, policy="EXT_LAT")
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=3,
+                     policy=ol.POLICY_EXT_LAT, hist=True)
+    assert (o["stats"]["status"] == 0).all()
+    assert_parity(tr, g, o)
+    np.testing.assert_array_equal(g["hist"], o["hist"].sum(axis=0))
+
+
+def test_wide_ext_lat_forced_tie_heavy(ctx, monkeypatch):
+    tr = tie_heavy(123, 8, 41, 1500)
+    monkeypatch.setenv("FOGNET_REPLAY_KERNEL", "wide")
+    g = run_gpu_full(ctx, tr, policy="EXT_LAT")
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8,
+                     policy=ol.POLICY_EXT_LAT, hist=True)
+    assert_parity(tr, g, o)
+
+
+def test_c5_large_topology_sample(ctx):
+    """Config C5 shape (BASELINE.json configs[4]): N = 10,000 fog nodes,
+    T = 10,000 tasks, device-generated traces; every replication against the oracle."""
+    R, T, N = 4, 10_000, 10_000
+    mg, sc = fa.c5_params(np.arange(R), N)
+    d = fa.generate_trace(ctx, 0x5EED0005, R, T, N, mg, sc)
+    out = fa.run_batch(ctx, d)
+    torch.cuda.synchronize()
+    st = out.rep_stats()
+    assert (st["status"] == 0).all() and (st["n_tasks"] == T).all()
+    for r in range(R):
+        h = {k: d[k][r].cpu().numpy() for k in ("arrive", "req", "mips", "dl", "ul", "init")}
+        o = ol.run_batch(h["arrive"], h["req"], h["mips"], h["dl"], h["ul"], h["init"])
+        for k_gpu, k_ref in (("node", "node"), ("status", "status"), ("start_tick", "start"), ("done_tick", "done")):
+            np.testing.assert_array_equal(getattr(out, k_gpu)[r].cpu().numpy(), o[k_ref][0], err_msg=k_gpu)
+        assert st[r].tobytes() == o["stats"][0].tobytes()
