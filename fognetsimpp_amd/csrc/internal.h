@@ -197,15 +197,29 @@ struct WideEntry {
 };
 static_assert(sizeof(WideEntry) == 40, "wide entry is 40 B");
 
+// Per node: chain ends plus copies of the head's and tail's fields, so a push
+// or an advert starts from one 64-B record (one cache line) instead of
+// chasing entries.  The `next` of the head lives here (hd_next); the `next` of
+// every other pending task in its WideEntry.
 struct WideNode {
-  int32_t hd, tl;  // oldest pending / newest task of the node (-1: none yet)
-  int32_t npend;   // tasks whose completion advert has not reached the broker
-  int32_t pad;
+  int32_t hd, tl;   // oldest pending / newest task of the node (-1: none yet)
+  int32_t npend;    // tasks whose completion advert has not reached the broker
+  int32_t hd_next;  // task after the head (valid while npend >= 2)
+  int64_t hd_done;  // head: completion tick
+  uint64_t hd_C;    //       cumulative service
+  int64_t tl_a;     // tail: arrival tick
+  int64_t tl_done;  //       completion tick
+  uint64_t tl_C;    //       cumulative service (0: no task yet) = the node's service seconds so far
+  uint32_t hd_S, tl_S;
 };
+static_assert(sizeof(WideNode) == 64, "wide node record is one 64-B line");
 
-// LDS of the wide kernel: 12 B per node (next advert tick, advertised busy)
-// + the histogram; a single workgroup may use all 160 KiB on gfx950.
-constexpr int kWideMaxNodes = 13568;
+// LDS of the wide kernel per node: next advert tick (8 B) + advertised busy
+// (4 B); per lane and group of 16 of its nodes: earliest advert, its node and
+// the smallest view key (20 B); + the histogram.  N = 12,288 fills 160 KiB
+// (a single workgroup may use all of it on gfx950).
+constexpr int kWideGroupSlots = 16;
+constexpr int kWideMaxNodes = 12288;
 size_t replay_wide_lds_bytes(int32_t N);
 // workspace: R*T WideEntry followed by R*N WideNode
 size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N);

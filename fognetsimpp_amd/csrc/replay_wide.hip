@@ -1,5 +1,5 @@
 // replay_wide.hip — batched trace replay for large fog-node sets on gfx950
-// (BASELINE.json configs[4], C5: 10,000 fog nodes; here N <= 13,568).  Same
+// (BASELINE.json configs[4], C5: 10,000 fog nodes; here N <= 12,288).  Same
 // reference semantics and the same closed form as replay.hip,
 // restated for node sets that do not fit in registers:
 //   decision   BrokerBaseApp3::sendPubAck(status=false)   BrokerBaseApp3.cc:265-304
@@ -11,15 +11,14 @@
 // One wavefront replays one replication.  Node j belongs to lane j % 64 and
 // only that lane reads or writes node j's state, so the loop needs no
 // barriers:
-//   LDS    s_nxt[N]   i64  tick at which the advert of node j's head completion
+//   LDS    nxt[N]     i64  tick at which the advert of node j's head completion
 //                          reaches the broker (kNever: nothing pending)
-//          s_busy[N]  u32  the broker's advertised busyTime of node j (seconds)
-//   VGPRs  per lane: the minimum of s_nxt and of the view key (busy << 32 | j)
-//          over the lane's nodes, rescanned from LDS after the lane applies an
-//          advert
+//          busy[N]    u32  the broker's advertised busyTime of node j (seconds)
+//          per lane and group of 16 of its nodes: earliest advert, its node,
+//          smallest view key (busy << 32 | j); the lane's minima in VGPRs
 //   HBM    WideEntry [R][T]: per task its arrival, completion, cumulative
 //          service and the links of its node's pending chain;
-//          WideNode [R][N]: head, tail and pending count of each node.
+//          WideNode [R][N]: chain ends + copies of head and tail fields (64 B).
 // Publishes are decided one at a time in trace order: adverts that reached
 // the broker strictly before the publish are applied first (lane-parallel:
 // adverts of different nodes commute, those of one node come in completion
@@ -35,19 +34,62 @@ namespace {
 
 constexpr uint32_t kWideMaxS = 0xFFFFu;  // service seconds < 2^16 (kMaxTick arithmetic)
 
-// Lane-local rescan of the lane's nodes: earliest pending advert and smallest view key.
-__device__ __forceinline__ void lane_scan(const int64_t* s_nxt, const uint32_t* s_busy, int N, int lane,
-                                          int64_t& mn, int& mj, uint64_t& mk) {
+// Per-lane minima are kept in two levels: for each group of kWideGroupSlots
+// of the lane's nodes (node j is slot j / 64 of lane j % 64) the earliest
+// pending advert, its node and the smallest view key live in LDS
+// ([group][lane], conflict-free); the lane's overall minima in VGPRs.  An
+// applied advert rescans one group and the group minima.
+struct WideLds {
+  int64_t* nxt;     // [N]
+  uint32_t* busy;   // [N]
+  int64_t* g_nxt;   // [G][64]
+  int32_t* g_j;     // [G][64]
+  uint64_t* g_key;  // [G][64]
+  uint32_t* hist;   // [FOGNET_HIST_METRICS][FOGNET_HIST_BINS]
+  int G;
+};
+
+__host__ __device__ __forceinline__ int wide_groups(int N) {
+  return ((N + kWave - 1) / kWave + kWideGroupSlots - 1) / kWideGroupSlots;
+}
+
+// Recompute group g of this lane from the per-node arrays.
+__device__ __forceinline__ void group_scan(const WideLds& L, int N, int lane, int g) {
+  int64_t mn = kNever;
+  int mj = lane;
+  uint64_t mk = ~0ull;
+#pragma unroll
+  for (int i = 0; i < kWideGroupSlots; ++i) {
+    const int j = (g * kWideGroupSlots + i) * kWave + lane;
+    if (j < N) {
+      const int64_t x = L.nxt[j];
+      if (x < mn) {
+        mn = x;
+        mj = j;
+      }
+      const uint64_t key = ((uint64_t)L.busy[j] << 32) | (uint32_t)j;
+      mk = key < mk ? key : mk;
+    }
+  }
+  L.g_nxt[g * kWave + lane] = mn;
+  L.g_j[g * kWave + lane] = mj;
+  L.g_key[g * kWave + lane] = mk;
+}
+
+// The lane's minima over its groups (earliest advert: first group on ties).
+__device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn, int& mj, uint64_t& mk) {
   mn = kNever;
   mj = lane;
   mk = ~0ull;
-  for (int j = lane; j < N; j += kWave) {
-    const int64_t x = s_nxt[j];
+#pragma unroll 4
+  for (int g = 0; g < L.G; ++g) {
+    const int64_t x = L.g_nxt[g * kWave + lane];
+    const int jj = L.g_j[g * kWave + lane];
+    const uint64_t key = L.g_key[g * kWave + lane];
     if (x < mn) {
       mn = x;
-      mj = j;
+      mj = jj;
     }
-    const uint64_t key = ((uint64_t)s_busy[j] << 32) | (uint32_t)j;
     mk = key < mk ? key : mk;
   }
 }
@@ -58,26 +100,36 @@ __device__ __forceinline__ void lane_scan(const int64_t* s_nxt, const uint32_t* 
 // are not done yet, a difference of cumulative sums; the head advances.
 // Returns false when the advertised busy time does not fit 32 bits.
 __device__ __forceinline__ bool apply_advert(int j, WideNode* nd, const WideEntry* e, int64_t dl, int64_t ul,
-                                             int64_t* s_nxt, uint32_t* s_busy) {
+                                             const WideLds& L) {
   WideNode h = nd[j];
-  const WideEntry hd = e[h.hd];
-  uint64_t c_arrived = hd.C;            // only the completing task itself ...
-  for (int32_t x = h.tl; x != h.hd;) {  // ... unless a newer one arrived first
-    const WideEntry ex = e[x];
-    if (arrives_before(ex.a, hd.done, dl, hd.S)) {
-      c_arrived = ex.C;
-      break;
+  uint64_t c_arrived = h.hd_C;  // only the completing task itself ...
+  if (arrives_before(h.tl_a, h.hd_done, dl, h.hd_S)) {
+    c_arrived = h.tl_C;  // ... or everything up to the newest task (the common case)
+  } else {
+    for (int32_t x = e[h.tl].prev; x != h.hd;) {  // newest first
+      const WideEntry ex = e[x];
+      if (arrives_before(ex.a, h.hd_done, dl, h.hd_S)) {
+        c_arrived = ex.C;
+        break;
+      }
+      x = ex.prev;
     }
-    x = ex.prev;
   }
-  const uint64_t busy = c_arrived - hd.C;
-  s_busy[j] = (uint32_t)busy;
+  const uint64_t busy = c_arrived - h.hd_C;
+  L.busy[j] = (uint32_t)busy;
   h.npend -= 1;
   if (h.npend == 0) {
-    s_nxt[j] = kNever;
+    L.nxt[j] = kNever;
   } else {
-    h.hd = hd.next;
-    s_nxt[j] = e[hd.next].done + ul;  // FIFO: the next task started at max(arrival, this completion)
+    // FIFO: the next task started at max(arrival, this completion); its
+    // done tick was fixed when it was pushed
+    const WideEntry nx = e[h.hd_next];
+    h.hd = h.hd_next;
+    h.hd_done = nx.done;
+    h.hd_C = nx.C;
+    h.hd_S = nx.S;
+    h.hd_next = nx.next;  // valid while npend >= 2
+    L.nxt[j] = nx.done + ul;
   }
   nd[j] = h;
   return busy < 0xFFFFFFFFull;
@@ -90,9 +142,14 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
   const int T = A.T, N = A.N;
-  int64_t* const s_nxt = reinterpret_cast<int64_t*>(w_lds);
-  uint32_t* const s_busy = reinterpret_cast<uint32_t*>(s_nxt + N);
-  uint32_t* const s_hist = s_busy + N;  // [FOGNET_HIST_METRICS][FOGNET_HIST_BINS]
+  WideLds L;
+  L.G = wide_groups(N);
+  L.nxt = reinterpret_cast<int64_t*>(w_lds);
+  L.g_nxt = L.nxt + N;
+  L.g_key = reinterpret_cast<uint64_t*>(L.g_nxt + L.G * kWave);
+  L.busy = reinterpret_cast<uint32_t*>(L.g_key + L.G * kWave);
+  L.g_j = reinterpret_cast<int32_t*>(L.busy + N);
+  L.hist = reinterpret_cast<uint32_t*>(L.g_j + L.G * kWave);
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)T;
   WideEntry* const e = E + tbase;
@@ -108,18 +165,19 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
     const int64_t d = A.dl[nbase + j], u = A.ul[nbase + j], ia = A.init[nbase + j];
     bad |= (m <= 0) | (d < 0) | (u < 0) | (d > kMaxTick) | (u > kMaxTick) | (ia < u) | (ia >= arrive0);
     if constexpr (kExt) bad |= d >= kExtMaxDl;
-    s_nxt[j] = kNever;
-    s_busy[j] = 0u;
-    nd[j] = WideNode{-1, -1, 0, 0};
+    L.nxt[j] = kNever;
+    L.busy[j] = 0u;
+    nd[j] = WideNode{-1, -1, 0, -1, 0, 0u, 0, 0, 0u, 0u, 0u};
   }
-  for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) s_hist[h] = 0u;
+  for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) L.hist[h] = 0u;
+  for (int g = 0; g < L.G; ++g) group_scan(L, N, lane, g);  // lane-local: no barrier needed
   __syncthreads();
   uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
 
   int64_t mn;
   int mj;
   uint64_t mk;
-  lane_scan(s_nxt, s_busy, N, lane, mn, mj, mk);
+  lane_min(L, lane, mn, mj, mk);
   Acc acc = acc_identity();
   uint32_t max_pend = 0u;  // over this lane's nodes
   int64_t prev_t = INT64_MIN;
@@ -147,8 +205,9 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
       while (ballot(mn < t)) {
         if (mn < t) {
           const int j = mj;
-          lerr |= !apply_advert(j, nd, e, A.dl[nbase + j], A.ul[nbase + j], s_nxt, s_busy);
-          lane_scan(s_nxt, s_busy, N, lane, mn, mj, mk);
+          lerr |= !apply_advert(j, nd, e, A.dl[nbase + j], A.ul[nbase + j], L);
+          group_scan(L, N, lane, (j / kWave) / kWideGroupSlots);
+          lane_min(L, lane, mn, mj, mk);
         }
       }
       if (ballot(lerr)) {
@@ -164,7 +223,7 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
         uint32_t mjj = ~0u;
         for (int j = lane; j < N; j += kWave) {
           const uint32_t S = min(rq / (uint32_t)A.mips[nbase + j], kExtSatS);
-          const uint64_t c = (uint64_t)A.dl[nbase + j] + ((uint64_t)s_busy[j] + S) * (uint64_t)kTicksPerSecond;
+          const uint64_t c = (uint64_t)A.dl[nbase + j] + ((uint64_t)L.busy[j] + S) * (uint64_t)kTicksPerSecond;
           if (c < mc) {
             mc = c;
             mjj = (uint32_t)j;
@@ -185,15 +244,9 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
         const int64_t dl_k = A.dl[nbase + k], ul_k = A.ul[nbase + k];
         const uint32_t S = rq / (uint32_t)mips_k;  // double tskTime = requiredMIPS / MIPS (:276)
         const int64_t a = t + dl_k;
-        int64_t prev_done = INT64_MIN;
-        uint32_t prev_S = 0u;
-        uint64_t prev_C = 0u;
-        if (h.tl >= 0) {
-          const WideEntry p = e[h.tl];
-          prev_done = p.done;
-          prev_S = p.S;
-          prev_C = p.C;
-        }
+        // the previous task on node k is its tail (FIFO single server)
+        const int64_t prev_done = h.tl >= 0 ? h.tl_done : INT64_MIN;
+        const uint32_t prev_S = h.tl_S;
         const int64_t start = a > prev_done ? a : prev_done;
         const int64_t done = start + ticks_of(min(S, kWideMaxS));
         uint32_t status;
@@ -207,19 +260,34 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
         lerr = S > kWideMaxS || a > kMaxTick || done > kMaxTick;
         if (!lerr) {
           const int i = c0 + jp;
-          e[i] = WideEntry{a, done, prev_C + S, S, h.tl, -1, 0};
-          if (h.npend == 0) {
-            h.hd = i;  // its completion advert is the node's next one
+          const uint64_t C = h.tl_C + S;
+          e[i] = WideEntry{a, done, C, S, h.tl, -1, 0};
+          if (h.npend == 0) {  // its completion advert is the node's next one
+            h.hd = i;
+            h.hd_done = done;
+            h.hd_C = C;
+            h.hd_S = S;
             const int64_t x = done + ul_k;
-            s_nxt[k] = x;
+            const int g = ((int)k / kWave) / kWideGroupSlots;
+            L.nxt[k] = x;
+            if (x < L.g_nxt[g * kWave + lane]) {
+              L.g_nxt[g * kWave + lane] = x;
+              L.g_j[g * kWave + lane] = (int)k;
+            }
             if (x < mn) {
               mn = x;
               mj = (int)k;
             }
+          } else if (h.npend == 1) {
+            h.hd_next = i;  // the tail is the head
           } else {
             e[h.tl].next = i;
           }
           h.tl = i;
+          h.tl_a = a;
+          h.tl_done = done;
+          h.tl_C = C;
+          h.tl_S = S;
           h.npend += 1;
           nd[k] = h;
           max_pend = max(max_pend, (uint32_t)h.npend);
@@ -230,8 +298,8 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
           A.out_done[o] = done;
           acc_task(acc, t, a, start, done, S, status);
           if (hist) {
-            atomicAdd(&s_hist[FOGNET_HIST_BINS + hist_bin(done - t)], 1u);
-            if (status == 4u) atomicAdd(&s_hist[hist_bin(start - a)], 1u);
+            atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - t)], 1u);
+            if (status == 4u) atomicAdd(&L.hist[hist_bin(start - a)], 1u);
           }
         }
       }
@@ -258,10 +326,9 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
   // with B_j = node j's service seconds (its tail's cumulative sum), summed in node order
   if (A.p_busy && A.out_stats) {
     const int64_t H = n_done > 0 ? acc.last : 0;
-    double* const s_e = reinterpret_cast<double*>(s_nxt);  // dead now; lane j%64 wrote s_nxt[j]
+    double* const s_e = reinterpret_cast<double*>(L.nxt);  // dead now; lane j%64 wrote nxt[j]
     for (int j = lane; j < N; j += kWave) {
-      const int32_t tl = nd[j].tl;
-      const int64_t B = tl >= 0 ? (int64_t)e[tl].C : 0;
+      const int64_t B = (int64_t)nd[j].tl_C;
       const double eb = __dmul_rn(A.p_busy[nbase + j], (double)B);
       const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
       const double en = __dadd_rn(eb, __dmul_rn(A.p_idle[nbase + j], idle));
@@ -278,7 +345,7 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
   if (hist) {
     __syncthreads();
     for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave)
-      if (s_hist[h]) atomicAdd((unsigned long long*)&A.hist[h], (unsigned long long)s_hist[h]);
+      if (L.hist[h]) atomicAdd((unsigned long long*)&A.hist[h], (unsigned long long)L.hist[h]);
   }
 }
 
@@ -294,7 +361,10 @@ void launch_wide_pol(const ReplayArgs& a, WideEntry* e, WideNode* nd, size_t lds
 }  // namespace
 
 size_t replay_wide_lds_bytes(int32_t N) {
-  return (size_t)N * (sizeof(int64_t) + sizeof(uint32_t)) + FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t);
+  const size_t G = (size_t)wide_groups(N);
+  return (size_t)N * (sizeof(int64_t) + sizeof(uint32_t)) +
+         G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int32_t)) +
+         FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t);
 }
 
 size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N) {
