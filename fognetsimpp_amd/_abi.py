@@ -24,9 +24,12 @@ FOGNET_ERR_CAPACITY = 7
 FOGNET_ERR_UNSUPPORTED = 8
 
 FOGNET_POLICY_REF_V3 = 1
+FOGNET_POLICY_REF_V2 = 2
 FOGNET_POLICY_EXT_LAT = 16
 TICKS_PER_SECOND = 10**12
-ABI_VERSION = 3
+# fognet_v2_action (BrokerBaseApp2 decision outcome)
+V2_LOCAL, V2_FORWARD, V2_DROPPED, V2_NO_NODES = 3, 4, 5, 6
+ABI_VERSION = 4
 HIST_METRICS = 2  # 0 queueTime, 1 response
 HIST_BINS = 64
 
@@ -122,6 +125,9 @@ SIGNATURES = {
     "fognet_last_error": (C.c_char_p, [P]),
     "fognet_decide": (C.c_int, [P, C.c_int, C.c_int32, P, P, C.c_int32, C.POINTER(C.c_int32)]),
     "fognet_decide_batch_dev": (C.c_int, [P, C.c_int, C.c_int64, C.c_int32, P, P, P, P, P, P]),
+    "fognet_decide_v2": (C.c_int, [P, C.c_int32, P, C.c_int32, C.c_int32, C.POINTER(C.c_int32),
+                                   C.POINTER(C.c_int32)]),
+    "fognet_decide_v2_batch_dev": (C.c_int, [P, C.c_int64, C.c_int32, P, P, P, P, P, P]),
     "fognet_run_batch_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P]),
     "fognet_run_batch": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut)]),
     "fognet_replay_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P]),

@@ -212,6 +212,47 @@ int fognet_decide(fognet_ctx* c, int policy, int32_t n, const double* adv_busy, 
   return FOGNET_OK;
 }
 
+int fognet_decide_v2_batch_dev(fognet_ctx* c, int64_t m, int32_t n, const int32_t* adv_mips, const int32_t* local_mips,
+                               const int32_t* req, int32_t* out_node, int32_t* out_action, void* stream) {
+  if (!c) return FOGNET_ERR_ARG;
+  if (m < 0 || n < 0) return fail(c, FOGNET_ERR_ARG, "m < 0 or n < 0");
+  if (m > 0 && (!out_node || !out_action || !local_mips || !req || (n > 0 && !adv_mips)))
+    return fail(c, FOGNET_ERR_ARG, "null pointer");
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipError_t e = fognet::launch_decide_v2(m, n, adv_mips, local_mips, req, out_node, out_action, (hipStream_t)stream);
+  return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "decide_v2 launch");
+}
+
+int fognet_decide_v2(fognet_ctx* c, int32_t n, const int32_t* adv_mips, int32_t local_mips, int32_t req_mips,
+                     int32_t* out_node, int32_t* out_action) {
+  if (!c || !out_node || !out_action) return FOGNET_ERR_ARG;
+  if (n < 0) return fail(c, FOGNET_ERR_ARG, "n < 0");
+  if (n > 0 && !adv_mips) return fail(c, FOGNET_ERR_ARG, "null view");
+  int rc = set_device(c);
+  if (rc) return rc;
+  const size_t nm = (size_t)n * sizeof(int32_t);
+  const size_t off_s = (nm + 255) & ~(size_t)255, off_o = off_s + 256, total = off_o + 256;
+  rc = ensure(c, &c->scratch, &c->scratch_bytes, total, "decide scratch");
+  if (rc) return rc;
+  char* s = (char*)c->scratch;
+  const int32_t scal[2] = {local_mips, req_mips};
+  hipError_t e;
+  if ((n > 0 && (e = hipMemcpyAsync(s, adv_mips, nm, hipMemcpyHostToDevice, c->stream)) != hipSuccess) ||
+      (e = hipMemcpyAsync(s + off_s, scal, sizeof scal, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return hip_fail(c, e, "decide_v2 copy-in");
+  e = fognet::launch_decide_v2(1, n, (const int32_t*)s, (const int32_t*)(s + off_s), (const int32_t*)(s + off_s) + 1,
+                               (int32_t*)(s + off_o), (int32_t*)(s + off_o) + 1, c->stream);
+  if (e != hipSuccess) return hip_fail(c, e, "decide_v2 launch");
+  int32_t res[2] = {-1, 0};
+  if ((e = hipMemcpyAsync(res, s + off_o, sizeof res, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+    return hip_fail(c, e, "decide_v2 copy-out");
+  *out_node = res[0];
+  *out_action = res[1];
+  return FOGNET_OK;
+}
+
 static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out, void* stream, int which) {
   if (!c || !out) return FOGNET_ERR_ARG;
   fognet::ReplayArgs a;

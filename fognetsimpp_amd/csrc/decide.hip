@@ -1,5 +1,6 @@
-// decide.hip — M independent broker decisions, BrokerBaseApp3.cc:265-281,
-// evaluated with the reference's exact arithmetic:
+// decide.hip — M independent broker decisions: BrokerBaseApp3.cc:265-281
+// (decide_kernel) and BrokerBaseApp2.cc:180-192/235-286 (decide_v2_kernel).
+// The v3 core is evaluated with the reference's exact arithmetic:
 //   tskTime = req / brokers[0].MIPS           (int / int, then double)
 //   tempp   = busy[0] + tskTime
 //   for j in 0..n-1: if busy[j] + tskTime < tempp: tempp = ..., k = j   (strict '<')
@@ -77,7 +78,48 @@ __global__ __launch_bounds__(kDecideThreads) void decide_kernel(int64_t m, int32
   }
 }
 
+// BrokerBaseApp2 (BrokerBaseApp2.cc:180-192, 235-286): one wavefront per
+// query.  The reference's loop takes index i+1 whenever brokers[i+1].MIPS >
+// brokers[0].MIPS (temp is never updated), i.e. the LAST such index; the lanes
+// scan strided candidates and a wave max keeps the largest qualifying index.
+__global__ __launch_bounds__(kDecideThreads) void decide_v2_kernel(int64_t m, int32_t n, const int32_t* mips,
+                                                                    const int32_t* local, const int32_t* req,
+                                                                    int32_t* node, int32_t* action) {
+  const int64_t q = (int64_t)blockIdx.x * (kDecideThreads / kWave) + threadIdx.x / kWave;
+  const int lane = threadIdx.x % kWave;
+  if (q >= m) return;  // whole wave exits together
+  const int32_t rq = req[q];
+  int32_t out = -1, act;
+  if (rq < local[q]) {
+    act = FOGNET_V2_LOCAL;  // :181
+  } else if (n <= 0) {
+    act = FOGNET_V2_NO_NODES;  // :273-285
+  } else {
+    const int32_t* v = mips + q * (int64_t)n;
+    const int32_t temp = v[0];  // :241
+    uint32_t last = 0u;         // currentGoodBroker = 0 (:237)
+    for (int32_t j = 1 + lane; j < n; j += kWave)
+      if (v[j] > temp) last = (uint32_t)j;  // ascending per lane: keeps the lane's largest
+    out = (int32_t)~wave_min_u32(~last);
+    act = rq < v[out] ? FOGNET_V2_FORWARD : FOGNET_V2_DROPPED;  // :262
+  }
+  if (lane == 0) {
+    node[q] = out;
+    action[q] = act;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_decide_v2(int64_t m, int32_t n, const int32_t* mips, const int32_t* local, const int32_t* req,
+                            int32_t* node, int32_t* action, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  const int per = kDecideThreads / kWave;
+  const int64_t blocks = (m + per - 1) / per;
+  hipLaunchKernelGGL(decide_v2_kernel, dim3((unsigned)blocks), dim3(kDecideThreads), 0, s, m, n, mips, local, req,
+                     node, action);
+  return hipGetLastError();
+}
 
 hipError_t launch_decide(int64_t m, int32_t n, const double* busy, const int32_t* mips, const int32_t* req,
                          int32_t* node, int32_t* status, hipStream_t s) {

@@ -8,6 +8,8 @@ decision, node update and statistic is computed by the gfx950 kernels in
   (``simple BrokerBaseApp3 like IUDPApp``, src/mqttapp/BrokerBaseApp3.ned:20);
   :meth:`BrokerBaseApp3.sendPubAck` is the decision core of
   ``BrokerBaseApp3::sendPubAck(..., status=false)`` (BrokerBaseApp3.cc:265-281).
+* :class:`BrokerBaseApp2` — the v2 broker's local-first / "max-MIPS" forward
+  (BrokerBaseApp2.cc:180-192, 235-286).
 * :class:`Context` + :func:`run_batch` — R independent trace replays of the
   broker/fog-node loop (BrokerBaseApp3.cc:123-158, ComputeBrokerApp3.cc:205-320).
 """
@@ -117,6 +119,43 @@ class BrokerBaseApp3:
             _ptr(node), _ptr(status), _stream_ptr(adv_busy.device))
         self.ctx.check(rc, "decide_batch")
         return node, status
+
+
+class BrokerBaseApp2:
+    """Allocation policy of BrokerBaseApp2 (src/mqttapp/BrokerBaseApp2.cc, the
+    module simulations/example/wirelessNet.ini:56 selects).
+
+    Serves a task itself when MIPSRequired < its own remaining MIPS
+    (``local_mips``: par MIPS minus its reservations, :181, :211); otherwise
+    forwards to the LAST node whose advertised MIPS exceeds node 0's (the
+    reference's "best broker" loop never updates its threshold, :241-248),
+    and only if MIPSRequired < that node's MIPS (:262).
+    """
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def sendPubAck(self, adv_mips, local_mips: int, MIPSRequired: int) -> tuple[int, int]:  # noqa: N802,N803
+        """(action, node): action is _abi.V2_LOCAL / V2_FORWARD / V2_DROPPED /
+        V2_NO_NODES; node is -1 for LOCAL and NO_NODES."""
+        mips = np.ascontiguousarray(adv_mips, dtype=np.int32).reshape(-1)
+        node, act = C.c_int32(-1), C.c_int32(0)
+        rc = self.ctx._lib.fognet_decide_v2(self.ctx.handle, len(mips), mips.ctypes.data_as(C.c_void_p),
+                                            int(local_mips), int(MIPSRequired), C.byref(node), C.byref(act))
+        self.ctx.check(rc, "sendPubAck(v2)")
+        return act.value, node.value
+
+    def sendPubAck_batch(self, adv_mips: torch.Tensor, local_mips: torch.Tensor, req: torch.Tensor):  # noqa: N802
+        """M independent decisions on device tensors adv_mips [M, n], local_mips [M],
+        req [M]; returns (action, node) int32 [M]."""
+        m, n = adv_mips.shape
+        node = torch.empty(m, dtype=torch.int32, device=adv_mips.device)
+        act = torch.empty(m, dtype=torch.int32, device=adv_mips.device)
+        rc = self.ctx._lib.fognet_decide_v2_batch_dev(
+            self.ctx.handle, m, n, _ptr(adv_mips.contiguous()), _ptr(local_mips.contiguous()), _ptr(req.contiguous()),
+            _ptr(node), _ptr(act), _stream_ptr(adv_mips.device))
+        self.ctx.check(rc, "decide_v2_batch")
+        return act, node
 
 
 @dataclass

@@ -6,6 +6,8 @@
  *   - the broker's allocation argmin, BrokerBaseApp3::sendPubAck(status=false),
  *     src/mqttapp/BrokerBaseApp3.cc:265-304 (decision core :267-281)
  *       -> fognet_decide / fognet_decide_batch_dev;
+ *   - the v2 broker's local-first / "max-MIPS" forward, BrokerBaseApp2.cc:180-192
+ *     and :235-286 -> fognet_decide_v2 / fognet_decide_v2_batch_dev;
  *   - the fog node's task arrival, ComputeBrokerApp3::processPacket,
  *     src/mqttapp/ComputeBrokerApp3.cc:269-320, its completion + advertisement,
  *     ComputeBrokerApp3::releaseResource / advertiseMIPS, :224-256 / :205-222,
@@ -36,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FOGNET_ABI_VERSION 3
+#define FOGNET_ABI_VERSION 4
 #define FOGNET_TICKS_PER_SECOND 1000000000000LL
 
 /* Latency histograms (device-side statistics, summed over replications; the
@@ -64,6 +66,9 @@ typedef enum fognet_status {
 } fognet_status;
 
 typedef enum fognet_policy {
+    FOGNET_POLICY_REF_V2 = 2,   /* BrokerBaseApp2: local-first, then the LAST node whose advertised MIPS
+                                   exceeds node 0's, forwarded only if MIPSRequired < its MIPS
+                                   (fognet_decide_v2; needs the broker's own MIPS)                 */
     FOGNET_POLICY_REF_V3 = 1,   /* BrokerBaseApp3: argmin(busy_j + req / mips_0), int division,
                                    strict '<' (ties -> lowest index), stale advertised view      */
     FOGNET_POLICY_EXT_LAT = 16  /* north-star cost, NOT in the reference (parity vs the oracle's
@@ -72,6 +77,14 @@ typedef enum fognet_policy {
                                    (int division by the node's OWN MIPS, exact int64 ticks,
                                    ties -> lowest index); same stale view and node model      */
 } fognet_policy;
+
+/* Outcome of one BrokerBaseApp2 decision (BrokerBaseApp2.cc:180-192, 235-286). */
+typedef enum fognet_v2_action {
+    FOGNET_V2_LOCAL = 3,     /* MIPSRequired < the broker's own MIPS: served locally (pubAck status 3)  */
+    FOGNET_V2_FORWARD = 4,   /* pubAck status 4 + FognetMsgTask to *out_node                            */
+    FOGNET_V2_DROPPED = 5,   /* pubAck status 4, MIPSRequired >= the chosen node's MIPS: no task sent   */
+    FOGNET_V2_NO_NODES = 6   /* no compute broker registered: "no compute resource available" puback   */
+} fognet_v2_action;
 
 /* Per-replication statistics.  Times are kept in exact ticks; 128-bit sums are
  * split into (lo, hi) uint64 halves so results are bit-reproducible. */
@@ -170,6 +183,21 @@ int fognet_decide(fognet_ctx *ctx, int policy, int32_t n, const double *adv_busy
 int fognet_decide_batch_dev(fognet_ctx *ctx, int policy, int64_t m, int32_t n,
                             const double *adv_busy, const int32_t *adv_mips, const int32_t *req,
                             int32_t *out_node, int32_t *out_status, void *hip_stream);
+
+/* Drop-in for the v2 broker's allocation (BrokerBaseApp2.cc:180-192 and
+ * sendPubAck(status=false) :235-286): host arrays of the advertised MIPS view
+ * adv_mips[n] (Broker::MIPS, updated by adverts :128-136), the broker's own
+ * remaining MIPS (par MIPS minus local reservations) and MIPSRequired.
+ * *out_action: fognet_v2_action; *out_node: chosen node, -1 for LOCAL/NO_NODES.
+ * Evaluated on the device. */
+int fognet_decide_v2(fognet_ctx *ctx, int32_t n, const int32_t *adv_mips, int32_t local_mips,
+                     int32_t req_mips, int32_t *out_node, int32_t *out_action);
+
+/* M independent v2 decisions, device pointers: adv_mips [M][n], local_mips [M],
+ * req [M], out_node [M], out_action [M]. */
+int fognet_decide_v2_batch_dev(fognet_ctx *ctx, int64_t m, int32_t n, const int32_t *adv_mips,
+                               const int32_t *local_mips, const int32_t *req, int32_t *out_node,
+                               int32_t *out_action, void *hip_stream);
 
 /* Batched replay engine.  *_dev: every pointer in in/out is a device pointer
  * (the structs themselves are host memory).  Returns FOGNET_OK once enqueued;

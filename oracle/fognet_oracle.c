@@ -305,6 +305,33 @@ int orc_decide_ext_lat(int32_t n, const double *adv_busy, const int32_t *mips, c
     return ORC_OK;
 }
 
+int orc_decide_v2(int32_t n, const int32_t *adv_mips, int32_t local_mips, int32_t req, int32_t *out_node,
+                  int32_t *out_action) {
+    /* BrokerBaseApp2::handleMessageWhenUp, MqttMsgPublish branch (BrokerBaseApp2.cc:180-192) */
+    if (req < local_mips) { /* :181 */
+        *out_node = -1;
+        *out_action = ORC_V2_LOCAL;
+        return ORC_OK;
+    }
+    /* sendPubAck(..., false), :235-286 */
+    if (n <= 0) { /* :239, :273-285 */
+        *out_node = -1;
+        *out_action = ORC_V2_NO_NODES;
+        return ORC_OK;
+    }
+    int32_t currentGoodBroker = 0;      /* :237 */
+    int32_t temp = adv_mips[0];         /* :241 */
+    for (int32_t i = 0; i < n; i++) {   /* :242 */
+        if (i + 1 < n) {                /* :243 */
+            if (adv_mips[i + 1] > temp) /* :244, temp never updated */
+                currentGoodBroker = i + 1;
+        }
+    }
+    *out_node = currentGoodBroker;
+    *out_action = req < adv_mips[currentGoodBroker] ? ORC_V2_FORWARD : ORC_V2_DROPPED; /* :262 */
+    return ORC_OK;
+}
+
 /* BrokerBaseApp3::handleMessageWhenUp, MqttMsgPublish branch (:138-158) + sendPubAck(false). */
 static int broker_publish(sim_t *s, int64_t t) {
     /* QoS==1 in every trace publish; the status-4 pubAck to the user (:145-150) and the

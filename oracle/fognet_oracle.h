@@ -93,6 +93,22 @@ int orc_decide_v3(int32_t n, const double *adv_busy, const int32_t *adv_mips, in
 int orc_decide_ext_lat(int32_t n, const double *adv_busy, const int32_t *mips, const int64_t *dl, int32_t req,
                        int32_t *out_node);
 
+/* BrokerBaseApp2 (v2 policy) decision, BrokerBaseApp2.cc:180-192 (publish
+ * branch) + 235-270 (sendPubAck(status=false)): served by the broker itself if
+ * MIPSRequired < its own MIPS; otherwise the node is the LAST index i >= 1
+ * whose advertised MIPS exceeds node 0's (temp is never updated, :241-248),
+ * else 0, and the task is sent only if MIPSRequired < that node's MIPS.
+ * *out_action: ORC_V2_* below; *out_node: the chosen node (-1 for LOCAL and
+ * NO_NODES). */
+enum {
+    ORC_V2_LOCAL = 3,    /* pubAck status 3, the broker reserves its own MIPS (:181-182, :209-232) */
+    ORC_V2_FORWARD = 4,  /* pubAck status 4 + FognetMsgTask to the node (:186-192, :262-270)        */
+    ORC_V2_DROPPED = 5,  /* pubAck status 4 but MIPSRequired >= the node's MIPS: no task (:262)      */
+    ORC_V2_NO_NODES = 6  /* "no compute resource available" (:273-285)                             */
+};
+int orc_decide_v2(int32_t n, const int32_t *adv_mips, int32_t local_mips, int32_t req, int32_t *out_node,
+                  int32_t *out_action);
+
 /* Histogram bin of a duration in ticks (fognet_hip.h FOGNET_HIST_BINS rule). */
 int orc_hist_bin(int64_t ticks);
 

@@ -30,3 +30,9 @@ def replay_cases():
                   ul=np.array(c["ul"], np.int64), init=np.array(c["init"], np.int64))
         out.append((c["name"], tr, c["expect"]))
     return out
+
+
+def decide_v2_cases():
+    d = json.load(open(os.path.join(GOLDEN, "kat_decide_v2.json")))
+    return [(c["name"], np.array(c["mips"], dtype=np.int32), int(c["local"]), int(c["req"]), int(c["action"]),
+             int(c["node"])) for c in d["cases"]]

@@ -60,6 +60,8 @@ def lib():
         _lib.orc_hist_bin.restype = C.c_int
         _lib.orc_decide_v3.argtypes = [C.c_int32, p, p, C.c_int32, C.POINTER(C.c_int32)]
         _lib.orc_decide_v3.restype = C.c_int
+        _lib.orc_decide_v2.argtypes = [C.c_int32, p, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        _lib.orc_decide_v2.restype = C.c_int
     return _lib
 
 
@@ -73,6 +75,18 @@ def decide_v3(adv_busy, adv_mips, req):
     out = C.c_int32(-7)
     rc = lib().orc_decide_v3(len(adv_busy), _ptr(adv_busy), _ptr(adv_mips), int(req), C.byref(out))
     return rc, out.value
+
+
+def decide_v2(adv_mips, local_mips, req):
+    """BrokerBaseApp2 decision: (action ORC_V2_*, node)."""
+    adv_mips = np.ascontiguousarray(adv_mips, dtype=np.int32)
+    node, act = C.c_int32(-7), C.c_int32(-7)
+    lib().orc_decide_v2(len(adv_mips), _ptr(adv_mips) if len(adv_mips) else None, int(local_mips), int(req),
+                        C.byref(node), C.byref(act))
+    return act.value, node.value
+
+
+V2_LOCAL, V2_FORWARD, V2_DROPPED, V2_NO_NODES = 3, 4, 5, 6
 
 
 def decide_ext_lat(adv_busy, mips, dl, req):

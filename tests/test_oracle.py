@@ -183,3 +183,10 @@ def test_ext_lat_replay_invariants():
     # spreads load (the reference policy herds onto one node between adverts)
     assert all(len(np.unique(o["node"][r])) > 8 for r in range(4))
     check_fifo_invariants(tr, o)
+
+
+@pytest.mark.parametrize("case", golden_io.decide_v2_cases(), ids=lambda c: c[0])
+def test_decide_v2_known_answers(case):
+    """Oracle restatement of BrokerBaseApp2's decision pinned by hand-traced vectors."""
+    name, mips, local, req, action, node = case
+    assert ol.decide_v2(mips, local, req) == (action, node)

@@ -70,6 +70,28 @@ def test_decide_batch_matches_oracle(ctx):
                 assert node[q] == k, (n, q)
 
 
+@pytest.mark.parametrize("case", golden_io.decide_v2_cases(), ids=lambda c: c[0])
+def test_v2_sendPubAck_known_answers(ctx, case):
+    name, mips, local, req, action, node = case
+    assert fa.BrokerBaseApp2(ctx).sendPubAck(mips, local, req) == (action, node)
+
+
+def test_decide_v2_batch_matches_oracle(ctx):
+    rng = np.random.default_rng(17)
+    dev = torch.device("cuda", ctx.device)
+    for n in (0, 1, 2, 5, 64, 65, 300, 5000):
+        m = 1500
+        mips = rng.choice([0, 500, 999, 1000, 1001, 2000, 4000], size=(m, max(n, 1))).astype(np.int32)[:, :n]
+        mips = np.ascontiguousarray(mips)
+        local = rng.integers(-100, 3000, size=m).astype(np.int32)
+        req = rng.integers(0, 4500, size=m).astype(np.int32)
+        act, node = fa.BrokerBaseApp2(ctx).sendPubAck_batch(
+            torch.from_numpy(mips).to(dev), torch.from_numpy(local).to(dev), torch.from_numpy(req).to(dev))
+        act, node = act.cpu().numpy(), node.cpu().numpy()
+        for q in range(m):
+            assert (act[q], node[q]) == ol.decide_v2(mips[q], local[q], req[q]), (n, q)
+
+
 # ------------------------------------------------------------------ replay engine
 
 @pytest.mark.parametrize("case", golden_io.replay_cases(), ids=lambda c: c[0])
