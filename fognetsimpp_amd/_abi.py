@@ -83,6 +83,24 @@ class JobStats(C.Structure):
 JOB_STATS_DTYPE = _np_dtype(JobStats)
 
 
+class Moments(C.Structure):
+    _fields_ = [("count", C.c_int64), ("min_ticks", C.c_int64), ("max_ticks", C.c_int64),
+                ("sum_lo", C.c_uint64), ("sum_hi", C.c_uint64), ("sq_lo", C.c_uint64), ("sq_hi", C.c_uint64),
+                ("pad", C.c_int64)]
+
+
+USER_SIGNALS = ("delay", "latency", "latencyH1", "taskTime")
+
+
+class UserStats(C.Structure):
+    _fields_ = [(n, Moments) for n in USER_SIGNALS]
+
+
+MOMENTS_DTYPE = _np_dtype(Moments)
+USER_STATS_DTYPE = np.dtype([(n, MOMENTS_DTYPE) for n in USER_SIGNALS])
+assert USER_STATS_DTYPE.itemsize == C.sizeof(UserStats)
+
+
 class BatchIn(C.Structure):
     _fields_ = [
         ("R", C.c_int32), ("T", C.c_int32), ("N", C.c_int32), ("policy", C.c_int32),
@@ -132,6 +150,7 @@ SIGNATURES = {
     "fognet_run_batch": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut)]),
     "fognet_replay_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P]),
     "fognet_rep_stats_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P]),
+    "fognet_user_stats_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P, P, C.c_int32, P, P]),
     "fognet_reduce_stats_dev": (C.c_int, [P, P, C.c_int32, P, P]),
     "fognet_job_stats_init": (None, [C.POINTER(JobStats)]),
     "fognet_job_stats_merge": (None, [C.POINTER(JobStats), C.POINTER(JobStats)]),

@@ -394,6 +394,26 @@ int fognet_run_batch(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out*
   return FOGNET_OK;
 }
 
+int fognet_user_stats_dev(fognet_ctx* c, const fognet_batch_in* in, const fognet_batch_out* out, const int64_t* user_ul,
+                          const int64_t* user_dl, int32_t user_per_task, fognet_user_stats* user_stats, void* stream) {
+  if (!c || !out) return FOGNET_ERR_ARG;
+  fognet::ReplayArgs a;
+  int rc = prepare(c, in, &a);
+  if (rc) return rc;
+  if (user_per_task != 0 && user_per_task != 1) return fail(c, FOGNET_ERR_ARG, "user_per_task must be 0 or 1");
+  if (a.R == 0) return FOGNET_OK;
+  if (!user_ul || !user_dl || !user_stats || !out->stats || (a.T > 0 && (!out->node || !out->status || !out->done_tick)))
+    return fail(c, FOGNET_ERR_ARG, "null pointer");
+  rc = set_device(c);
+  if (rc) return rc;
+  a.out_node = out->node;
+  a.out_status = out->status;
+  a.out_done = out->done_tick;
+  a.out_stats = out->stats;
+  hipError_t e = fognet::launch_user_stats(a, user_ul, user_dl, user_per_task, user_stats, (hipStream_t)stream);
+  return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "user stats launch");
+}
+
 int fognet_reduce_stats_dev(fognet_ctx* c, const fognet_rep_stats* stats, int32_t R, fognet_job_stats* out,
                             void* stream) {
   if (!c || !out || (R > 0 && !stats) || R < 0) return FOGNET_ERR_ARG;

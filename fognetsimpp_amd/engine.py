@@ -240,6 +240,50 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
     return out
 
 
+def user_stats(ctx: Context, trace: dict, out: BatchResult, user_ul, user_dl) -> np.ndarray:
+    """User-side signals (fognet_user_stats_dev) of a finished replay: broker
+    ``delay`` and mqttApp2's ``latency`` / ``latencyH1`` / ``taskTime`` as exact
+    tick moments per replication (USER_STATS_DTYPE [R]).  ``user_ul`` /
+    ``user_dl``: the publishing user's links, [R] (one user per replication)
+    or [R, T] (per task), host arrays or device tensors."""
+    arrive = trace["arrive"]
+    R, T = arrive.shape
+    dev = arrive.device
+    uu = torch.as_tensor(np.asarray(user_ul) if not isinstance(user_ul, torch.Tensor) else user_ul,
+                         dtype=torch.int64).to(dev).contiguous()
+    ud = torch.as_tensor(np.asarray(user_dl) if not isinstance(user_dl, torch.Tensor) else user_dl,
+                         dtype=torch.int64).to(dev).contiguous()
+    per_task = 1 if uu.dim() == 2 else 0
+    want = (R, T) if per_task else (R,)
+    if tuple(uu.shape) != want or tuple(ud.shape) != want:
+        raise FognetError(_abi.FOGNET_ERR_ARG, f"user links must both have shape [R] or [R, T], got "
+                                               f"{tuple(uu.shape)} / {tuple(ud.shape)}")
+    mips = trace["mips"]
+    N = mips.shape[-1]
+    res = torch.zeros(R * _abi.USER_STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    bi = _abi.BatchIn(R, T, N, _abi.FOGNET_POLICY_REF_V3, N if mips.dim() == 2 else 0, 0,
+                      _ptr(arrive), _ptr(trace["req"]), _ptr(mips), _ptr(trace["dl"]), _ptr(trace["ul"]),
+                      _ptr(trace["init"]), None, None)
+    bo = _abi.BatchOut(_ptr(out.node), _ptr(out.status), _ptr(out.start_tick), _ptr(out.done_tick),
+                       _ptr(out.stats), None, None)
+    ctx.check(ctx._lib.fognet_user_stats_dev(ctx.handle, C.byref(bi), C.byref(bo), _ptr(uu), _ptr(ud), per_task,
+                                             _ptr(res), _stream_ptr(dev)), "user_stats")
+    return res.cpu().numpy().view(_abi.USER_STATS_DTYPE)
+
+
+def summarize_moments(m) -> dict:
+    """count/mean/stddev/sum/sqrsum/min/max in ms (the reference's signal unit) of one
+    tick-moments record, like cStdDev's `.sca` fields."""
+    n = int(m["count"])
+    if n == 0:
+        return dict(count=0)
+    s = int(m["sum_lo"]) | (int(m["sum_hi"]) << 64)
+    q = int(m["sq_lo"]) | (int(m["sq_hi"]) << 64)
+    var = (q - s * s / n) / (n - 1) if n > 1 else 0.0
+    return dict(count=n, mean=s / n / 1e9, stddev=max(var, 0.0) ** 0.5 / 1e9, sum=s / 1e9, sqrsum=q / 1e18,
+                min=int(m["min_ticks"]) / 1e9, max=int(m["max_ticks"]) / 1e9)
+
+
 def reduce_stats(ctx: Context, stats: torch.Tensor, R: int) -> np.ndarray:
     """Exact job-level reduction on the device; returns a JOB_STATS_DTYPE record."""
     out = torch.zeros(_abi.JOB_STATS_DTYPE.itemsize, dtype=torch.uint8, device=stats.device)

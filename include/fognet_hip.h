@@ -15,7 +15,9 @@
  *     BrokerBaseApp3.cc:123-130 -> fognet_run_batch[_dev] (R independent
  *     trace replays of the whole decide -> queue -> complete -> advertise loop);
  *   - the queueTime statistic (ComputeBrokerApp3.cc:238, ComputeBrokerApp3.ned:45-46)
- *     -> fognet_rep_stats, reduced on the device (fognet_reduce_stats_dev).
+ *     -> fognet_rep_stats, reduced on the device (fognet_reduce_stats_dev);
+ *   - the ack relay and the users' latency signals (BrokerBaseApp3.cc:143,
+ *     164-198; mqttApp2.cc:252-291) -> fognet_user_stats_dev.
  *
  * Conventions
  *   - Every entry point returns a fognet_status; no exception crosses the ABI.
@@ -155,6 +157,31 @@ typedef struct fognet_batch_out {
                                  (the caller zeroes it; nullable)                                 */
 } fognet_batch_out;
 
+/* count / min / max / exact 128-bit sum and sum of squares of values in ticks
+ * (min_ticks = INT64_MAX, max_ticks = INT64_MIN when count == 0). */
+typedef struct fognet_moments {
+    int64_t count, min_ticks, max_ticks;
+    uint64_t sum_lo, sum_hi, sq_lo, sq_hi;
+    int64_t pad;
+} fognet_moments;
+
+/* User-side signals of one replication, in ticks
+ * (the reference emits (simTime() - created) * 1000 ms, i.e. ticks / 1e9):
+ *   delay      broker `delay` (BrokerBaseApp3.cc:143): publish arrival at the
+ *              broker - creation at the user, every publish
+ *   latency    mqttApp2 on the relayed status-5 ack ("task assigned",
+ *              mqttApp2.cc:257-265)
+ *   latencyH1  on status-4 acks (mqttApp2.cc:269-277): the broker's own pubAck
+ *              (BrokerBaseApp3.cc:145-150) for every publish, plus the node's
+ *              relayed "task queued" ack
+ *   taskTime   on the relayed status-6 ack ("performed", mqttApp2.cc:279-291)
+ * Acks travel node -> broker (ul_k), are relayed to the request's user
+ * (BrokerBaseApp3.cc:164-198) and arrive one user downlink later.  Message
+ * ids are assumed unique (the reference matches them with strcmp). */
+typedef struct fognet_user_stats {
+    fognet_moments delay, latency, latencyH1, taskTime;
+} fognet_user_stats;
+
 /* Synthetic trace recipe, generated on the device.
  * Replication r uses Philox4x32-10 key (seed, r); see DESIGN.md §Trace generator. */
 typedef struct fognet_gen_params {
@@ -213,6 +240,16 @@ int fognet_rep_stats_dev(fognet_ctx *ctx, const fognet_batch_in *in, fognet_batc
 /* Host-buffer variant: copies in, replays, copies out, synchronises.  Returns
  * the first non-OK replication status, if any. */
 int fognet_run_batch(fognet_ctx *ctx, const fognet_batch_in *in, fognet_batch_out *out);
+
+/* User-side signals from a finished replay (fognet_replay_dev or
+ * fognet_run_batch_dev on the same stream): device pointers in `in` (trace,
+ * node parameters) and `out` (node, status, done_tick, stats) plus the
+ * publishing users' links user_ul_tick (user -> broker) and user_dl_tick
+ * (broker -> user): [R] (one user per replication, user_per_task = 0) or
+ * [R][T] (per task, = 1).  Writes user_stats [R] (device). */
+int fognet_user_stats_dev(fognet_ctx *ctx, const fognet_batch_in *in, const fognet_batch_out *out,
+                          const int64_t *user_ul_tick, const int64_t *user_dl_tick, int32_t user_per_task,
+                          fognet_user_stats *user_stats, void *hip_stream);
 
 /* Exact reduction of R per-replication stats (device pointers) into one job
  * record (device pointer).  Replications with status != OK count in n_failed

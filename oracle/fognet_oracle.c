@@ -23,7 +23,7 @@
 
 #define TICKS_PER_SECOND 1000000000000LL /* simtime scale 1e-12 (no simtime-scale in any ini) */
 
-enum { EV_PUBLISH = 0, EV_ADVERT = 1, EV_TASK = 2, EV_SELF = 3 };
+enum { EV_PUBLISH = 0, EV_ADVERT = 1, EV_TASK = 2, EV_SELF = 3, EV_ACK_AT_BROKER = 4, EV_ACK_AT_USER = 5 };
 enum { KIND_ADVERTISEMIPS = 1, KIND_RELEASERESOURCE = 2 }; /* ComputeBrokerApp3.h selfMsg kinds */
 
 typedef struct {
@@ -32,7 +32,7 @@ typedef struct {
     int32_t type;
     int32_t node;
     int64_t task;
-    int32_t mips;    /* EV_ADVERT payload: FognetMsgAdvertiseMIPS.MIPS     */
+    int32_t mips;    /* EV_ADVERT payload: FognetMsgAdvertiseMIPS.MIPS; EV_ACK_*: MqttMsgPuback.status */
     uint32_t gen;    /* EV_SELF: selfMsg generation (cancelEvent support)  */
     double busy;     /* EV_ADVERT payload: FognetMsgAdvertiseMIPS.busyTime */
 } ev_t;
@@ -146,6 +146,44 @@ static int schedule(sim_t *s, ev_t *e) {
     return heap_push(&s->fes, e);
 }
 
+/* ---- user side (only when the trace carries user links) */
+
+static int64_t user_ul(const sim_t *s, int64_t t) { return s->in->user_ul_tick[s->in->user_per_task ? t : 0]; }
+static int64_t user_dl(const sim_t *s, int64_t t) { return s->in->user_dl_tick[s->in->user_per_task ? t : 0]; }
+
+static void moment_add(orc_moments *m, int64_t v) {
+    m->count++;
+    if (v < m->min_ticks) m->min_ticks = v;
+    if (v > m->max_ticks) m->max_ticks = v;
+    acc_moment(&m->sum_lo, &m->sum_hi, &m->sq_lo, &m->sq_hi, v);
+}
+
+/* socket.sendTo(MqttMsgPuback{status}) towards task t's user: from the broker
+ * (one user downlink later at the user) or from node k (one uplink later at the
+ * broker, which relays it, BrokerBaseApp3.cc:164-198). */
+static int send_ack(sim_t *s, int at_broker, int32_t k, int64_t t, int32_t status) {
+    if (!s->in->user_ul_tick || !s->out->user) return ORC_OK;
+    ev_t e;
+    memset(&e, 0, sizeof e);
+    e.tick = s->now + (at_broker ? user_dl(s, t) : s->in->ul_tick[k]);
+    e.type = at_broker ? EV_ACK_AT_USER : EV_ACK_AT_BROKER;
+    e.node = k;
+    e.task = t;
+    e.mips = status;
+    return schedule(s, &e);
+}
+
+/* mqttApp2::processPacket, MqttMsgPuback branch (mqttApp2.cc:252-291): the
+ * signal is (simTime() - timeCreated) * 1000 ms, kept in exact ticks here. */
+static void user_ack(sim_t *s, const ev_t *e) {
+    orc_user_stats *u = s->out->user;
+    int64_t created = s->in->arrive_tick[e->task] - user_ul(s, e->task); /* sendMqttData: created at the user */
+    int64_t v = s->now - created;
+    if (e->mips == 5) moment_add(&u->latency, v);        /* :257-265 */
+    else if (e->mips == 4) moment_add(&u->latencyH1, v); /* :269-277 */
+    else if (e->mips == 6) moment_add(&u->taskTime, v);  /* :279-291 */
+}
+
 /* cSimpleModule::scheduleAt for a node's selfMsg. */
 static int node_schedule_self(sim_t *s, int32_t k, int64_t tick, int kind) {
     node_t *nd = &s->nodes[k];
@@ -190,6 +228,8 @@ static int node_release(sim_t *s, int32_t k) {
     node_t *nd = &s->nodes[k];
     int64_t t = nd->currentTask.task;
     /* ack status 6 to the broker (:228-233) -- relay only, no decision effect */
+    int rc0 = send_ack(s, 0, k, t, 6);
+    if (rc0) return rc0;
     nd->busyTime = nd->busyTime - nd->currentTask.required_time; /* :232 */
     nd->resourceStatus = 0;                                      /* :234 */
     nd->served_s += (int64_t)nd->currentTask.required_time;
@@ -234,6 +274,8 @@ static int node_task(sim_t *s, int32_t k, int64_t t) {
     if (nd->resourceStatus == 0) {             /* :282 */
         nd->resourceStatus = 1;
         if (s->out->status) s->out->status[t] = 5; /* "task assigned" (:285-289) */
+        int rc5 = send_ack(s, 0, k, t, 5);
+        if (rc5) return rc5;
         nd->currentTask.task = t;
         nd->currentTask.required_time = tskTime; /* :292-296 */
         nd->currentTask.qstart_tick = s->now;
@@ -260,7 +302,7 @@ static int node_task(sim_t *s, int32_t k, int64_t t) {
     nd->qn++;
     if (s->out->status) s->out->status[t] = 4;
     s->st.n_queued++;
-    return ORC_OK;
+    return send_ack(s, 0, k, t, 4);
 }
 
 int orc_decide_v3(int32_t n, const double *adv_busy, const int32_t *adv_mips, int32_t req, int32_t *out_node) {
@@ -338,6 +380,11 @@ static int broker_publish(sim_t *s, int64_t t) {
      * `delay` emit (:143) do not influence the decision. */
     int32_t k;
     int rc;
+    if (s->in->user_ul_tick && s->out->user) {
+        moment_add(&s->out->user->delay, user_ul(s, t)); /* emit(delaySignal, simTime() - creationTime) (:143) */
+        rc = send_ack(s, 1, -1, t, 4);                    /* pubAck status 4 (:145-150) */
+        if (rc) return rc;
+    }
     if (s->in->policy == ORC_POLICY_EXT_LAT)
         rc = orc_decide_ext_lat(s->in->n_nodes, s->adv_busy, s->in->mips, s->in->dl_tick, s->in->req_mips[t], &k);
     else
@@ -366,6 +413,12 @@ static void broker_advert(sim_t *s, const ev_t *e) {
 
 static int dispatch(sim_t *s, const ev_t *e) {
     s->now = e->tick;
+    if (e->type == EV_ACK_AT_BROKER) /* relay to the request's user (BrokerBaseApp3.cc:164-198) */
+        return send_ack(s, 1, e->node, e->task, e->mips);
+    if (e->type == EV_ACK_AT_USER) {
+        user_ack(s, e);
+        return ORC_OK;
+    }
     s->st.events++;
     switch (e->type) {
     case EV_PUBLISH:
@@ -411,6 +464,14 @@ int orc_run_rep(const orc_rep_in *in, orc_rep_out *out) {
     s.st.queue_max_ticks = INT64_MIN;
     s.st.resp_max_ticks = INT64_MIN;
     s.st.last_tick = INT64_MIN;
+    if (out->user) {
+        orc_moments *ms[4] = {&out->user->delay, &out->user->latency, &out->user->latencyH1, &out->user->taskTime};
+        for (int i = 0; i < 4; i++) {
+            memset(ms[i], 0, sizeof *ms[i]);
+            ms[i]->min_ticks = INT64_MAX;
+            ms[i]->max_ticks = INT64_MIN;
+        }
+    }
     int rc = ORC_OK;
     if (out->node)
         for (int64_t t = 0; t < T; t++) out->node[t] = -1;
@@ -523,12 +584,15 @@ typedef struct {
     const int32_t *req_mips, *mips;
     const int64_t *dl, *ul, *init_adv;
     const double *p_busy, *p_idle;
+    const int64_t *user_ul, *user_dl;
+    int32_t user_per_task;
     int32_t *node;
     uint8_t *status;
     int64_t *start_tick, *done_tick;
     orc_rep_stats *stats;
     double *node_energy;
     int64_t *hist;
+    orc_user_stats *user;
     int64_t next; /* work counter */
     pthread_mutex_t mu;
 } batch_t;
@@ -541,14 +605,17 @@ static void *batch_worker(void *arg) {
         pthread_mutex_unlock(&b->mu);
         if (r >= b->R) break;
         size_t to = (size_t)r * (size_t)b->T, no = (size_t)r * (size_t)b->node_stride;
+        size_t uo = b->user_per_task ? to : (size_t)r;
         orc_rep_in in = {b->N, b->T, b->arrive_tick + to, b->req_mips + to, b->mips + no,
                          b->dl + no, b->ul + no, b->init_adv + no,
-                         b->p_busy ? b->p_busy + no : 0, b->p_idle ? b->p_idle + no : 0, b->policy};
+                         b->p_busy ? b->p_busy + no : 0, b->p_idle ? b->p_idle + no : 0, b->policy,
+                         b->user_ul ? b->user_ul + uo : 0, b->user_dl ? b->user_dl + uo : 0, b->user_per_task};
         orc_rep_out out = {b->node ? b->node + to : 0, b->status ? b->status + to : 0,
                            b->start_tick ? b->start_tick + to : 0, b->done_tick ? b->done_tick + to : 0,
                            0, b->stats ? b->stats + r : 0,
                            b->node_energy ? b->node_energy + (size_t)r * (size_t)b->N : 0,
-                           b->hist ? b->hist + (size_t)r * ORC_HIST_METRICS * ORC_HIST_BINS : 0};
+                           b->hist ? b->hist + (size_t)r * ORC_HIST_METRICS * ORC_HIST_BINS : 0,
+                           b->user ? b->user + r : 0};
         orc_run_rep(&in, &out);
     }
     return 0;
@@ -569,8 +636,22 @@ int orc_run_batch2(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t
                    const double *p_busy_w, const double *p_idle_w,
                    int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
                    orc_rep_stats *stats, double *node_energy_j, int64_t *hist, int threads) {
+    return orc_run_batch3(R, T, N, node_stride, policy, arrive_tick, req_mips, mips, dl, ul, init_adv, p_busy_w,
+                          p_idle_w, 0, 0, 0, node, status, start_tick, done_tick, stats, node_energy_j, hist, 0,
+                          threads);
+}
+
+int orc_run_batch3(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
+                   const int64_t *arrive_tick, const int32_t *req_mips,
+                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                   const double *p_busy_w, const double *p_idle_w,
+                   const int64_t *user_ul, const int64_t *user_dl, int32_t user_per_task,
+                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                   orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
+                   int threads) {
     batch_t b = {R, N, node_stride, policy, T, arrive_tick, req_mips, mips, dl, ul, init_adv, p_busy_w, p_idle_w,
-                 node, status, start_tick, done_tick, stats, node_energy_j, hist, 0};
+                 user_ul, user_dl, user_per_task, node, status, start_tick, done_tick, stats, node_energy_j, hist,
+                 user_stats, 0};
     pthread_mutex_init(&b.mu, 0);
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;

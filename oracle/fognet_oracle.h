@@ -56,7 +56,28 @@ typedef struct {
     const double *p_busy_w;       /* [N] power while serving, W (nullable: no energy)  */
     const double *p_idle_w;       /* [N] power while idle, W                           */
     int32_t policy;               /* ORC_POLICY_*; 0 means REF_V3                      */
+    /* User side (nullable: not modelled).  The publishing user's links: user ->
+     * broker (the publish; created = arrive - user_ul) and broker -> user (the
+     * pubacks), per task ([T], user_per_task = 1) or one user ([1]). */
+    const int64_t *user_ul_tick;
+    const int64_t *user_dl_tick;
+    int32_t user_per_task;
 } orc_rep_in;
+
+/* count / min / max / exact 128-bit sum and sum of squares of values in ticks */
+typedef struct {
+    int64_t count, min_ticks, max_ticks;
+    uint64_t sum_lo, sum_hi, sq_lo, sq_hi;
+    int64_t pad;
+} orc_moments;
+
+/* The user-side signals of the offload loop: broker `delay` (BrokerBaseApp3.cc:143)
+ * and mqttApp2's `latency` (status 5, mqttApp2.cc:257-265), `latencyH1`
+ * (status 4: the broker's own ack and the node's "queued" relay, :269-277)
+ * and `taskTime` (status 6, :279-291). */
+typedef struct {
+    orc_moments delay, latency, latencyH1, taskTime;
+} orc_user_stats;
 
 typedef struct {
     int64_t n_tasks, n_queued, n_started;
@@ -81,6 +102,7 @@ typedef struct {
     orc_rep_stats *stats;
     double *node_energy_j;   /* [N] per-node energy (nullable)                         */
     int64_t *hist;           /* [2][64] histogram counts, ADDED to (nullable)          */
+    orc_user_stats *user;    /* user-side signals (needs user_ul/dl_tick; nullable)    */
 } orc_rep_out;
 
 int orc_run_rep(const orc_rep_in *in, orc_rep_out *out);
@@ -122,6 +144,17 @@ int orc_run_batch(int32_t R, int64_t T, int32_t N, int32_t node_stride,
 
 /* The same with a policy, an optional power model ([R|1][N], node_stride) and
  * optional per-node energy [R][N] and per-replication histograms [R][2][64]. */
+/* orc_run_batch2 + the user side: user_ul/user_dl [R][T] (user_per_task) or
+ * [R] (one user per replication); user_stats [R] (nullable). */
+int orc_run_batch3(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
+                   const int64_t *arrive_tick, const int32_t *req_mips,
+                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                   const double *p_busy_w, const double *p_idle_w,
+                   const int64_t *user_ul, const int64_t *user_dl, int32_t user_per_task,
+                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                   orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
+                   int threads);
+
 int orc_run_batch2(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
                    const int64_t *arrive_tick, const int32_t *req_mips,
                    const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,

@@ -33,6 +33,11 @@ class OrcRepStats(C.Structure):
 _NP = {C.c_int64: np.int64, C.c_uint64: np.uint64, C.c_int32: np.int32, C.c_double: np.float64}
 ORC_STATS_DTYPE = np.dtype([(n, _NP[t]) for n, t in OrcRepStats._fields_])
 assert ORC_STATS_DTYPE.itemsize == C.sizeof(OrcRepStats)
+MOMENTS_DTYPE = np.dtype([("count", np.int64), ("min_ticks", np.int64), ("max_ticks", np.int64),
+                          ("sum_lo", np.uint64), ("sum_hi", np.uint64), ("sq_lo", np.uint64), ("sq_hi", np.uint64),
+                          ("pad", np.int64)])
+USER_SIGNALS = ("delay", "latency", "latencyH1", "taskTime")
+USER_STATS_DTYPE = np.dtype([(n, MOMENTS_DTYPE) for n in USER_SIGNALS])
 POLICY_REF_V3, POLICY_EXT_LAT = 1, 16
 
 _lib = None
@@ -54,6 +59,9 @@ def lib():
         _lib.orc_run_batch.restype = C.c_int
         _lib.orc_run_batch2.argtypes = [C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [p] * 15 + [C.c_int]
         _lib.orc_run_batch2.restype = C.c_int
+        _lib.orc_run_batch3.argtypes = ([C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [p] * 10 +
+                                        [C.c_int32] + [p] * 8 + [C.c_int])
+        _lib.orc_run_batch3.restype = C.c_int
         _lib.orc_decide_ext_lat.argtypes = [C.c_int32, p, p, p, C.c_int32, C.POINTER(C.c_int32)]
         _lib.orc_decide_ext_lat.restype = C.c_int
         _lib.orc_hist_bin.argtypes = [C.c_int64]
@@ -99,10 +107,12 @@ def decide_ext_lat(adv_busy, mips, dl, req):
 
 
 def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool = True, policy: int = 1,
-              p_busy=None, p_idle=None, hist: bool = False):
+              p_busy=None, p_idle=None, hist: bool = False, user_ul=None, user_dl=None):
     """Replay R replications.  arrive/req: [R,T]; node params [R,N] or [N] (shared).
     ``p_busy``/``p_idle`` (same shape as mips) enable the energy model; ``hist``
-    returns per-replication histograms [R, 2, 64]."""
+    returns per-replication histograms [R, 2, 64]; ``user_ul``/``user_dl``
+    ([R] one user per replication, or [R, T] per task) model the publishing
+    users' links and return the user-side signals as ``user`` [R] (USER_STATS_DTYPE)."""
     arrive = np.ascontiguousarray(np.atleast_2d(arrive), dtype=np.int64)
     req = np.ascontiguousarray(np.atleast_2d(req), dtype=np.int32)
     R, T = arrive.shape
@@ -120,9 +130,17 @@ def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool =
     pi = np.ascontiguousarray(p_idle, dtype=np.float64) if p_idle is not None else None
     energy = np.zeros((R, N), np.float64) if pb is not None else None
     h = np.zeros((R, 2, 64), np.int64) if hist else None
+    uu = ud = user = None
+    per_task = 0
+    if user_ul is not None:
+        uu = np.ascontiguousarray(user_ul, dtype=np.int64)
+        ud = np.ascontiguousarray(user_dl, dtype=np.int64)
+        per_task = 1 if uu.ndim == 2 else 0
+        user = np.zeros(R, USER_STATS_DTYPE)
     stats = (OrcRepStats * R)()
-    lib().orc_run_batch2(R, T, N, stride, policy, _ptr(arrive), _ptr(req), _ptr(mips), _ptr(dl), _ptr(ul),
-                         _ptr(init), _ptr(pb), _ptr(pi), _ptr(node), _ptr(status), _ptr(start), _ptr(done),
-                         C.cast(stats, C.c_void_p), _ptr(energy), _ptr(h), threads)
+    lib().orc_run_batch3(R, T, N, stride, policy, _ptr(arrive), _ptr(req), _ptr(mips), _ptr(dl), _ptr(ul),
+                         _ptr(init), _ptr(pb), _ptr(pi), _ptr(uu), _ptr(ud), per_task, _ptr(node), _ptr(status),
+                         _ptr(start), _ptr(done), C.cast(stats, C.c_void_p), _ptr(energy), _ptr(h), _ptr(user),
+                         threads)
     st = np.frombuffer(stats, dtype=ORC_STATS_DTYPE, count=R).copy()
-    return dict(node=node, status=status, start=start, done=done, stats=st, node_energy=energy, hist=h)
+    return dict(node=node, status=status, start=start, done=done, stats=st, node_energy=energy, hist=h, user=user)

@@ -190,3 +190,38 @@ def test_decide_v2_known_answers(case):
     """Oracle restatement of BrokerBaseApp2's decision pinned by hand-traced vectors."""
     name, mips, local, req, action, node = case
     assert ol.decide_v2(mips, local, req) == (action, node)
+
+
+def test_user_side_known_answer():
+    """One publish at tick 100, node 0 (MIPS 1000, dl 3, ul 5), MIPSRequired 2000
+    (S = 2 s), user uplink 7 / downlink 11 ticks.  Hand-traced: broker `delay` =
+    7 (BrokerBaseApp3.cc:143); its status-4 pubAck reaches the user at 111,
+    created at 93 -> latencyH1 18; the node's status-5 ack leaves at 103,
+    reaches the broker at 108, the user at 119 -> latency 26; status 6 leaves
+    at 103 + 2e12 -> taskTime 2e12 + 26 (mqttApp2.cc:257-291)."""
+    tr = dict(arrive=np.array([[100]], np.int64), req=np.array([[2000]], np.int32), mips=np.array([1000], np.int32),
+              dl=np.array([3], np.int64), ul=np.array([5], np.int64), init=np.array([5], np.int64))
+    o = ol.run_batch(**tr, user_ul=np.array([7]), user_dl=np.array([11]))
+    u = o["user"][0]
+    got = {n: (int(u[n]["count"]), int(u[n]["min_ticks"]), int(u[n]["max_ticks"])) for n in ol.USER_SIGNALS}
+    assert got == {"delay": (1, 7, 7), "latencyH1": (1, 18, 18), "latency": (1, 26, 26),
+                   "taskTime": (1, 2 * 10**12 + 26, 2 * 10**12 + 26)}
+
+
+def test_user_side_events_do_not_change_decisions():
+    """The ack relay is modelled as real FES events; they carry no state back
+    into the decision loop, so every output and record is unchanged."""
+    tr = tg.make_batch(7, 3, 16, 2000, rho=0.9)
+    a = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=3)
+    rng = np.random.default_rng(3)
+    uu, ud = rng.integers(0, 10**9, (2, 3, 2000))
+    b = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=3, user_ul=uu,
+                     user_dl=ud)
+    for k in ("node", "status", "start", "done"):
+        np.testing.assert_array_equal(a[k], b[k])
+    assert a["stats"].tobytes() == b["stats"].tobytes()
+    u = b["user"]
+    np.testing.assert_array_equal(u["delay"]["count"], 2000)
+    np.testing.assert_array_equal(u["taskTime"]["count"], 2000)
+    np.testing.assert_array_equal(u["latency"]["count"], b["stats"]["n_started"])
+    np.testing.assert_array_equal(u["latencyH1"]["count"], 2000 + b["stats"]["n_queued"])

@@ -490,3 +490,62 @@ def test_c5_large_topology_sample(ctx):
         for k_gpu, k_ref in (("node", "node"), ("status", "status"), ("start_tick", "start"), ("done_tick", "done")):
             np.testing.assert_array_equal(getattr(out, k_gpu)[r].cpu().numpy(), o[k_ref][0], err_msg=k_gpu)
         assert st[r].tobytes() == o["stats"][0].tobytes()
+
+
+# ------------------------------------------------------------------ user-side signals (ack relay)
+# fognet_user_stats_dev (closed form over the replay outputs) against the
+# oracle's event-level restatement (acks as FES events relayed by the broker).
+
+def assert_user_parity(g_user, o_user):
+    for n in ol.USER_SIGNALS:
+        for f in ("count", "min_ticks", "max_ticks", "sum_lo", "sum_hi", "sq_lo", "sq_hi"):
+            np.testing.assert_array_equal(g_user[n][f], o_user[n][f], err_msg=f"{n}.{f}")
+
+
+@pytest.mark.parametrize("kind", ["one_user", "per_task", "tie_heavy", "wide"])
+def test_user_stats_match_oracle(ctx, kind):
+    rng = np.random.default_rng(31)
+    if kind == "tie_heavy":
+        tr = tie_heavy(5, 6, 37, 1500)
+    elif kind == "wide":
+        tr = tg.make_batch(0x5EED0005, 3, 400, 2000, rho=0.01, lat_scale=10)
+    else:
+        tr = tg.make_batch(0x5EED0003, 6, 64, 2000, sweep=True)
+    R, T = tr["arrive"].shape
+    shape = (R, T) if kind == "per_task" else (R,)
+    uu = rng.integers(0, 5 * 10**9, shape).astype(np.int64)
+    ud = rng.integers(0, 5 * 10**9, shape).astype(np.int64)
+    if kind == "tie_heavy":
+        uu[:] = 0
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(tr, dev)
+    out = fa.run_batch(ctx, d, ring_capacity=4096)
+    g = fa.user_stats(ctx, d, out, uu, ud)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=6, user_ul=uu,
+                     user_dl=ud)
+    assert (o["stats"]["status"] == 0).all()
+    assert_user_parity(g, o["user"])
+
+
+def test_user_stats_with_reference_task_source(ctx):
+    """Several users publishing through mqttApp2's timer chain and glibc rand()
+    stream (fognet_gen_trace_mqtt); per-task user links from the user index."""
+    from fognetsimpp_amd import formats
+    MS = 10**9
+    U = 6
+    up = np.array([2, 3, 5, 7, 11, 13], np.int64) * MS
+    dn = np.array([1, 4, 6, 8, 9, 10], np.int64) * MS
+    g = formats.gen_trace_mqtt(1, np.arange(U) * 7 * MS, np.full(U, 20_000 * MS), up, dn, 2000 * 10**12,
+                               req_base=1000, req_span=30000)
+    n = 8
+    tr = dict(arrive=g["arrive"][None], req=g["req"][None], mips=(1000 * (1 + np.arange(n) % 4)).astype(np.int32),
+              dl=np.full(n, 3 * MS, np.int64), ul=np.full(n, 4 * MS, np.int64), init=np.full(n, 4 * MS, np.int64))
+    uu, ud = up[g["user"]][None], dn[g["user"]][None]
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(tr, dev)
+    out = fa.run_batch(ctx, d)
+    gu = fa.user_stats(ctx, d, out, uu, ud)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], user_ul=uu, user_dl=ud)
+    assert o["stats"]["status"][0] == 0 and int(o["stats"]["n_tasks"][0]) == g["arrive"].size
+    np.testing.assert_array_equal(out.node.cpu().numpy(), o["node"])
+    assert_user_parity(gu, o["user"])
