@@ -94,14 +94,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU; FOGNET_BENCH_SHARE_GPU=1 lets ranks share devices (a
+    # multi-rank rehearsal on a 1-GPU box, with FOGNET_BENCH_BACKEND=gloo)
+    gpu = local % torch.cuda.device_count() if os.environ.get("FOGNET_BENCH_SHARE_GPU") == "1" else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("FOGNET_BENCH_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
-    ctx = fa.Context(local)
+    ctx = fa.Context(gpu)
     if args.workload == "c4":
         return bench_c4(args, ctx, dev, dist, world, rank)
     T, N = args.T, args.N
