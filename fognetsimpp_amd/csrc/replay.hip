@@ -448,14 +448,18 @@ __device__ __forceinline__ uint32_t ext_argmin(const Slot (&st)[NPL], uint32_t r
   return 0u;
 }
 
-// One level of the run scan: combine with the element kCtrl names on the left.
+// One level of the run's inclusive u32 prefix sum (the element kCtrl names on
+// the left; invalid sources read 0).
 template <int kCtrl, int kRowMask>
-__device__ __forceinline__ void run_scan_level(uint32_t& Cs, int64_t& Ac) {
-  const uint32_t Cl = dpp_or_u32<kCtrl, kRowMask>(0u, Cs);
-  const int64_t Al = dpp_or_i64<kCtrl, kRowMask>(INT64_MIN, Ac);
-  const int64_t aa = (int64_t)((uint64_t)Al + (uint64_t)ticks_of(Cs));  // no signed-overflow UB on rejected lanes
-  Ac = aa > Ac ? aa : Ac;
-  Cs = Cl + Cs;
+__device__ __forceinline__ uint32_t scan_add_level(uint32_t v) {
+  return v + dpp_or_u32<kCtrl, kRowMask>(0u, v);
+}
+
+// One level of the run's inclusive i64 prefix maximum (invalid sources read INT64_MIN).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int64_t scan_max_level(int64_t v) {
+  const int64_t l = dpp_or_i64<kCtrl, kRowMask>(INT64_MIN, v);
+  return l > v ? l : v;
 }
 
 // ---------------------------------------------------------------- statistics
@@ -786,12 +790,9 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
       const int L = __popcll(run_mask);
       const int jq = jp + L;
 
-      // 5) FIFO recurrence over the run: done_m = max(a_m, done_{m-1}) + S_m,
-      //    as an inclusive scan of g_m(x) = max(x + S_m 1e12, A_m) with
-      //    A_m = a_m + S_m 1e12, composed left to right:
-      //    (Cs_l, A_l) then (Cs_r, A_r) = (Cs_l + Cs_r, max(A_l + Cs_r 1e12, A_r)).
-      //    Non-run lanes carry the identity (0, INT64_MIN); DPP row shifts
-      //    and row broadcasts fill invalid sources with it.
+      // 5) FIFO recurrence over the run: done_m = max(a_m, done_{m-1}) + S_m.
+      //    Non-run lanes carry the identities (S = 0, X = INT64_MIN); DPP row
+      //    shifts and row broadcasts fill invalid sources with them.
       uint32_t S = 0u;
       int64_t a = 0, dd = 0;
       bool lerr = false;
@@ -801,17 +802,27 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
         dd = (int64_t)S * kTicksPerSecond;
         lerr = S > A.max_s || a > kMaxTick;
       }
-      int64_t Ac = in_run ? a + dd : INT64_MIN;
+      //    Unrolled: with P_m = sum_{i<=m} S_i 1e12 (a prefix sum) and
+      //    X_m = a_m - P_{m-1},  done_m = max(done_before_run, max_{i<=m} X_i) + P_m,
+      //    i.e. one u32 prefix sum and one i64 prefix max over the wave.
+      //    Unsigned arithmetic: rejected lanes (lerr) may wrap, never UB.
       uint32_t Cs = S;
-      run_scan_level<0x111, 0xF>(Cs, Ac);  // row_shr:1
-      run_scan_level<0x112, 0xF>(Cs, Ac);  // row_shr:2
-      run_scan_level<0x114, 0xF>(Cs, Ac);  // row_shr:4
-      run_scan_level<0x118, 0xF>(Cs, Ac);  // row_shr:8
-      run_scan_level<0x142, 0xA>(Cs, Ac);  // row_bcast:15
-      run_scan_level<0x143, 0xC>(Cs, Ac);  // row_bcast:31
+      Cs = scan_add_level<0x111, 0xF>(Cs);  // row_shr:1
+      Cs = scan_add_level<0x112, 0xF>(Cs);  // row_shr:2
+      Cs = scan_add_level<0x114, 0xF>(Cs);  // row_shr:4
+      Cs = scan_add_level<0x118, 0xF>(Cs);  // row_shr:8
+      Cs = scan_add_level<0x142, 0xA>(Cs);  // row_bcast:15
+      Cs = scan_add_level<0x143, 0xC>(Cs);  // row_bcast:31
+      int64_t X = in_run ? (int64_t)((uint64_t)a - (uint64_t)ticks_of(Cs - S)) : INT64_MIN;
+      X = scan_max_level<0x111, 0xF>(X);
+      X = scan_max_level<0x112, 0xF>(X);
+      X = scan_max_level<0x114, 0xF>(X);
+      X = scan_max_level<0x118, 0xF>(X);
+      X = scan_max_level<0x142, 0xA>(X);
+      X = scan_max_level<0x143, 0xC>(X);
       const int64_t base_done = tld_k;  // INT64_MIN when k never ran a task
-      const int64_t via = base_done + ticks_of(Cs);
-      const int64_t done = via > Ac ? via : Ac;
+      const int64_t dmax = base_done > X ? base_done : X;
+      const int64_t done = (int64_t)((uint64_t)dmax + (uint64_t)ticks_of(Cs));
       // previous task on node k: the run's previous lane, or k's tail
       const int64_t done_up = dpp_or_i64<kDppWaveShr1>(0, done);
       const uint32_t S_up = dpp_or_u32<kDppWaveShr1>(0u, S);
