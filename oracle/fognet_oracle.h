@@ -131,6 +131,66 @@ enum {
 int orc_decide_v2(int32_t n, const int32_t *adv_mips, int32_t local_mips, int32_t req, int32_t *out_node,
                   int32_t *out_action);
 
+/* ---- v2 model replay (fognet_oracle_v2.c): BrokerBaseApp2 + ComputeBrokerApp2 */
+
+/* per-task outcome */
+enum {
+    ORC_V2_ST_LOCAL = 3,      /* reserved in the broker's own pool (pubAck 3)                  */
+    ORC_V2_ST_FORWARDED = 4,  /* FognetMsgTask sent, not yet at the node when the run stopped  */
+    ORC_V2_ST_DROPPED = 5,    /* pubAck 4 but MIPSRequired >= the chosen node's advertised MIPS */
+    ORC_V2_ST_NO_NODES = 6,   /* no compute broker registered                                  */
+    ORC_V2_ST_ACCEPTED = 7,   /* reserved at the node (TaskAck true, ComputeBrokerApp2.cc:269)  */
+    ORC_V2_ST_REJECTED = 8    /* MIPSRequired >= the node's remaining MIPS (TaskAck false)      */
+};
+
+typedef struct {
+    int32_t n_nodes;
+    int64_t n_tasks;
+    const int64_t *arrive_tick;    /* [T] publish arrival at the broker, nondecreasing          */
+    const int32_t *req_mips;       /* [T] MqttMsgPublish.MIPSRequired                            */
+    double required_time;          /* MqttMsgPublish.requiredTime, s (mqttApp2.cc:372: 0.01)     */
+    int32_t broker_mips;           /* BrokerBaseApp2 par("MIPS") (wirelessNet.ini:58)            */
+    const int32_t *mips;           /* [N] ComputeBrokerApp2 par("MIPS") (wirelessNet.ini:64)     */
+    const int64_t *dl_tick;        /* [N] broker -> node latency                                 */
+    const int64_t *ul_tick;        /* [N] node -> broker latency                                 */
+    const int64_t *first_adv_tick; /* [N] first ADVERTISEMIPS firing at the node                 */
+    int64_t stop_tick;             /* sim-time-limit: events at ticks >= stop are not processed  */
+} orc_v2_in;
+
+typedef struct {
+    int64_t n_tasks, n_local, n_forwarded, n_accepted, n_rejected, n_dropped, n_no_nodes;
+    int64_t n_released_broker;  /* broker RELEASERESOURCE releases (BrokerBaseApp2.cc:382-406)     */
+    int64_t n_inflated;         /* ... of them forwarded requests credited to the broker's pool    */
+    int64_t n_released_node;    /* node releases (ComputeBrokerApp2.cc:222-245)                   */
+    int64_t n_relayed;          /* status-6 acks that found their request at the broker (:143-154) */
+    int64_t events;             /* events processed (cancelled timers excluded)                    */
+    int64_t node_mips_final_sum;
+    int32_t broker_mips_final;
+    int32_t status;
+} orc_v2_stats;
+
+typedef struct {
+    int32_t *node;        /* [T] chosen node, -1: served locally / no node (nullable)   */
+    uint8_t *status;      /* [T] ORC_V2_ST_* (0: not published before the stop)         */
+    int64_t *start_tick;  /* [T] reservation tick, -1 if never reserved                 */
+    int64_t *done_tick;   /* [T] release tick of its reservation, -1 if not released    */
+    orc_v2_stats *stats;
+} orc_v2_out;
+
+int orc_run_v2_rep(const orc_v2_in *in, orc_v2_out *out);
+
+typedef struct {
+    int32_t R, N, node_stride;
+    int64_t T;
+    const int64_t *arrive_tick; const int32_t *req_mips;            /* [R][T] */
+    const double *required_time; const int32_t *broker_mips;        /* [R]    */
+    const int64_t *stop_tick;                                       /* [R]    */
+    const int32_t *mips; const int64_t *dl_tick, *ul_tick, *first_adv_tick; /* [R|1][N] */
+    int32_t *node; uint8_t *status; int64_t *start_tick, *done_tick; /* [R][T] (nullable) */
+    orc_v2_stats *stats;                                            /* [R]    */
+} orc_v2_batch;
+int orc_run_v2_batch(const orc_v2_batch *b, int threads);
+
 /* Histogram bin of a duration in ticks (fognet_hip.h FOGNET_HIST_BINS rule). */
 int orc_hist_bin(int64_t ticks);
 

@@ -36,3 +36,19 @@ def decide_v2_cases():
     d = json.load(open(os.path.join(GOLDEN, "kat_decide_v2.json")))
     return [(c["name"], np.array(c["mips"], dtype=np.int32), int(c["local"]), int(c["req"]), int(c["action"]),
              int(c["node"])) for c in d["cases"]]
+
+
+def replay_v2_cases():
+    d = json.load(open(os.path.join(GOLDEN, "kat_replay_v2.json")))
+    ms = d["ms"]
+    out = []
+    for c in d["cases"]:
+        tr = dict(arrive=np.array(c["arrive_ms"], np.int64)[None] * ms, req=np.array(c["req"], np.int32)[None],
+                  broker_mips=int(c["broker_mips"]), mips=np.array(c["mips"], np.int32),
+                  dl=np.array(c["dl_ms"], np.int64) * ms, ul=np.array(c["ul_ms"], np.int64) * ms,
+                  first_adv=np.array(c["first_adv_ms"], np.int64) * ms, stop=int(c["stop_ms"]) * ms)
+        e = dict(c["expect"])
+        e["start"] = [x * ms if x >= 0 else -1 for x in e.pop("start_ms")]
+        e["done"] = [x * ms if x >= 0 else -1 for x in e.pop("done_ms")]
+        out.append((c["name"], tr, e))
+    return out

@@ -70,6 +70,8 @@ def lib():
         _lib.orc_decide_v3.restype = C.c_int
         _lib.orc_decide_v2.argtypes = [C.c_int32, p, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         _lib.orc_decide_v2.restype = C.c_int
+        _lib.orc_run_v2_batch.argtypes = [p, C.c_int]
+        _lib.orc_run_v2_batch.restype = C.c_int
     return _lib
 
 
@@ -144,3 +146,53 @@ def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool =
                          threads)
     st = np.frombuffer(stats, dtype=ORC_STATS_DTYPE, count=R).copy()
     return dict(node=node, status=status, start=start, done=done, stats=st, node_energy=energy, hist=h, user=user)
+
+
+# ---------------------------------------------------------------- v2 model (fognet_oracle_v2.c)
+
+V2_ST_LOCAL, V2_ST_FORWARDED, V2_ST_DROPPED, V2_ST_NO_NODES, V2_ST_ACCEPTED, V2_ST_REJECTED = 3, 4, 5, 6, 7, 8
+
+
+class OrcV2Stats(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("n_tasks", "n_local", "n_forwarded", "n_accepted", "n_rejected",
+                                         "n_dropped", "n_no_nodes", "n_released_broker", "n_inflated",
+                                         "n_released_node", "n_relayed", "events", "node_mips_final_sum")] + \
+               [("broker_mips_final", C.c_int32), ("status", C.c_int32)]
+
+
+V2_STATS_DTYPE = np.dtype([(n, _NP[t]) for n, t in OrcV2Stats._fields_])
+assert V2_STATS_DTYPE.itemsize == C.sizeof(OrcV2Stats)
+
+
+class OrcV2Batch(C.Structure):
+    _fields_ = [("R", C.c_int32), ("N", C.c_int32), ("node_stride", C.c_int32), ("T", C.c_int64),
+                ("arrive_tick", C.c_void_p), ("req_mips", C.c_void_p), ("required_time", C.c_void_p),
+                ("broker_mips", C.c_void_p), ("stop_tick", C.c_void_p), ("mips", C.c_void_p), ("dl_tick", C.c_void_p),
+                ("ul_tick", C.c_void_p), ("first_adv_tick", C.c_void_p), ("node", C.c_void_p), ("status", C.c_void_p),
+                ("start_tick", C.c_void_p), ("done_tick", C.c_void_p), ("stats", C.c_void_p)]
+
+
+def run_v2(arrive, req, broker_mips, mips, dl, ul, first_adv, stop_tick, required_time=0.01, threads: int = 1):
+    """Replay the v2 model (BrokerBaseApp2 + ComputeBrokerApp2).  arrive/req
+    [R,T]; broker_mips, stop_tick, required_time scalars or [R]; node params
+    [R,N] or [N] (shared).  Returns node/status/start/done [R,T] and stats [R]."""
+    arrive = np.ascontiguousarray(np.atleast_2d(arrive), dtype=np.int64)
+    req = np.ascontiguousarray(np.atleast_2d(req), dtype=np.int32)
+    R, T = arrive.shape
+    mips = np.ascontiguousarray(mips, dtype=np.int32)
+    N = mips.shape[-1]
+    stride = N if mips.ndim == 2 else 0
+    dl, ul, fa = (np.ascontiguousarray(x, dtype=np.int64) for x in (dl, ul, first_adv))
+    bm = np.ascontiguousarray(np.broadcast_to(broker_mips, (R,)), dtype=np.int32)
+    st_ = np.ascontiguousarray(np.broadcast_to(stop_tick, (R,)), dtype=np.int64)
+    rt = np.ascontiguousarray(np.broadcast_to(required_time, (R,)), dtype=np.float64)
+    node = np.empty((R, T), np.int32)
+    status = np.empty((R, T), np.uint8)
+    start = np.empty((R, T), np.int64)
+    done = np.empty((R, T), np.int64)
+    stats = (OrcV2Stats * R)()
+    b = OrcV2Batch(R, N, stride, T, _ptr(arrive), _ptr(req), _ptr(rt), _ptr(bm), _ptr(st_), _ptr(mips), _ptr(dl),
+                   _ptr(ul), _ptr(fa), _ptr(node), _ptr(status), _ptr(start), _ptr(done), C.cast(stats, C.c_void_p))
+    lib().orc_run_v2_batch(C.byref(b), threads)
+    return dict(node=node, status=status, start=start, done=done,
+                stats=np.frombuffer(stats, dtype=V2_STATS_DTYPE, count=R).copy())

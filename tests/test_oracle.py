@@ -225,3 +225,42 @@ def test_user_side_events_do_not_change_decisions():
     np.testing.assert_array_equal(u["taskTime"]["count"], 2000)
     np.testing.assert_array_equal(u["latency"]["count"], b["stats"]["n_started"])
     np.testing.assert_array_equal(u["latencyH1"]["count"], 2000 + b["stats"]["n_queued"])
+
+
+@pytest.mark.parametrize("case", golden_io.replay_v2_cases(), ids=lambda c: c[0])
+def test_v2_replay_known_answers(case):
+    """The v2 model restatement (oracle/fognet_oracle_v2.c) on hand-traced traces."""
+    name, tr, e = case
+    o = ol.run_v2(tr["arrive"], tr["req"], tr["broker_mips"], tr["mips"], tr["dl"], tr["ul"], tr["first_adv"],
+                  tr["stop"])
+    assert o["node"][0].tolist() == e["node"]
+    assert o["status"][0].tolist() == e["status"]
+    assert o["start"][0].tolist() == e["start"]
+    assert o["done"][0].tolist() == e["done"]
+    st = o["stats"][0]
+    assert int(st["status"]) == e.get("rep_status", 0)
+    for k, v in e.items():
+        if k.startswith("n_") or k.endswith("_final") or k.endswith("_sum"):
+            assert int(st[k]) == v, k
+
+
+def test_v2_c1_example_run_has_rounding_forwards():
+    """C1 as shipped (wirelessNet.ini: 1 user, 50-ms interval, MIPSRequired 200 + rand() % 701,
+    broker and 5 nodes at 1000 MIPS).  The broker's single timer fails to release a
+    local reservation when dbl(t) + 0.01 > dbl(t + 0.01 s) (IEEE rounding); only a
+    new local task re-arms it, and once the pool is below 200 MIPS no task is local
+    again: the pool stays stuck and every later publish is forwarded -- to node 0,
+    the only outcome of the v2 forward rule with equal MIPS (the General-0.sca fact
+    that ComputeBroker1 received all forwarded tasks)."""
+    from fognetsimpp_amd import formats
+    MS = 10**9
+    g = formats.gen_trace_mqtt(1, [0], [50 * MS], [MS], [-1], 1000 * 10**12)
+    n = 5
+    o = ol.run_v2(g["arrive"], g["req"], 1000, np.full(n, 1000, np.int32), np.full(n, MS), np.full(n, MS),
+                  np.full(n, 20 * MS), 1000 * 10**12)
+    st = o["stats"][0]
+    assert int(st["status"]) == 0 and int(st["n_tasks"]) == 19999
+    assert (int(st["n_local"]), int(st["n_forwarded"]), int(st["broker_mips_final"])) == (9, 19990, 101)
+    assert int(st["n_accepted"]) == int(st["n_relayed"]) == 19990
+    fw = o["node"][0][o["status"][0] != 3]
+    assert (fw == 0).all()
