@@ -122,6 +122,33 @@ class GenParams(C.Structure):
                 ("mean_gap_ticks", C.c_void_p), ("lat_scale", C.c_void_p)]
 
 
+V2_MAX_NODES = 64
+V2_ST_LOCAL, V2_ST_FORWARDED, V2_ST_DROPPED, V2_ST_NO_NODES, V2_ST_ACCEPTED, V2_ST_REJECTED = 3, 4, 5, 6, 7, 8
+
+
+class V2In(C.Structure):
+    _fields_ = [("R", C.c_int32), ("T", C.c_int32), ("N", C.c_int32), ("node_stride", C.c_int32),
+                ("queue_capacity", C.c_int32), ("pad", C.c_int32),
+                ("arrive_tick", C.c_void_p), ("req_mips", C.c_void_p), ("broker_mips", C.c_void_p),
+                ("required_time_s", C.c_void_p), ("stop_tick", C.c_void_p), ("mips", C.c_void_p),
+                ("dl_tick", C.c_void_p), ("ul_tick", C.c_void_p), ("first_adv_tick", C.c_void_p)]
+
+
+class V2Stats(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("n_tasks", "n_local", "n_forwarded", "n_accepted", "n_rejected",
+                                         "n_dropped", "n_no_nodes", "n_released_broker", "n_inflated",
+                                         "n_released_node", "n_relayed", "events", "node_mips_final_sum")] + \
+               [("broker_mips_final", C.c_int32), ("status", C.c_int32)]
+
+
+V2_STATS_DTYPE = _np_dtype(V2Stats)
+
+
+class V2Out(C.Structure):
+    _fields_ = [("node", C.c_void_p), ("status", C.c_void_p), ("start_tick", C.c_void_p), ("done_tick", C.c_void_p),
+                ("stats", C.c_void_p)]
+
+
 TRACE_NOTE_BYTES = 160
 TRACE_FLAG_POWER = 1
 TRACE_FLAG_NODE_ID = 2
@@ -151,6 +178,7 @@ SIGNATURES = {
     "fognet_replay_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P]),
     "fognet_rep_stats_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P]),
     "fognet_user_stats_dev": (C.c_int, [P, C.POINTER(BatchIn), C.POINTER(BatchOut), P, P, C.c_int32, P, P]),
+    "fognet_run_v2_dev": (C.c_int, [P, C.POINTER(V2In), C.POINTER(V2Out), P]),
     "fognet_reduce_stats_dev": (C.c_int, [P, P, C.c_int32, P, P]),
     "fognet_job_stats_init": (None, [C.POINTER(JobStats)]),
     "fognet_job_stats_merge": (None, [C.POINTER(JobStats), C.POINTER(JobStats)]),

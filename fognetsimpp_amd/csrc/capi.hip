@@ -414,6 +414,30 @@ int fognet_user_stats_dev(fognet_ctx* c, const fognet_batch_in* in, const fognet
   return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "user stats launch");
 }
 
+int fognet_run_v2_dev(fognet_ctx* c, const fognet_v2_in* in, fognet_v2_out* out, void* stream) {
+  if (!c || !in || !out) return FOGNET_ERR_ARG;
+  if (in->R < 0 || in->T < 0 || in->N < 0) return fail(c, FOGNET_ERR_ARG, "negative R/T/N");
+  if (in->N > FOGNET_V2_MAX_NODES) return fail(c, FOGNET_ERR_UNSUPPORTED, "the v2 replay keeps node j on lane j: N <= 64");
+  if (in->node_stride != 0 && in->node_stride != in->N) return fail(c, FOGNET_ERR_ARG, "node_stride must be 0 or N");
+  const int q = in->queue_capacity ? in->queue_capacity : 256;
+  if (q < 2 || (q & (q - 1)) != 0 || q > (1 << 16)) return fail(c, FOGNET_ERR_ARG, "queue_capacity must be a power of two in [2, 2^16]");
+  int qlog = 0;
+  while ((1 << qlog) < q) ++qlog;
+  if (in->R == 0) return FOGNET_OK;
+  if (!in->broker_mips || !in->required_time_s || !in->stop_tick || (in->T > 0 && (!in->arrive_tick || !in->req_mips)) ||
+      (in->N > 0 && (!in->mips || !in->dl_tick || !in->ul_tick || !in->first_adv_tick)))
+    return fail(c, FOGNET_ERR_ARG, "null input array");
+  if (!out->stats || (in->T > 0 && (!out->node || !out->status || !out->start_tick || !out->done_tick)))
+    return fail(c, FOGNET_ERR_ARG, "null output array");
+  int rc = set_device(c);
+  if (rc) return rc;
+  rc = ensure(c, (void**)&c->ring, &c->ring_bytes, fognet::replay_v2_workspace_bytes(in->R, in->T, qlog),
+              "v2 replay workspace");
+  if (rc) return rc;
+  hipError_t e = fognet::launch_replay_v2(*in, *out, c->ring, qlog, (hipStream_t)stream);
+  return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "v2 replay launch");
+}
+
 int fognet_reduce_stats_dev(fognet_ctx* c, const fognet_rep_stats* stats, int32_t R, fognet_job_stats* out,
                             void* stream) {
   if (!c || !out || (R > 0 && !stats) || R < 0) return FOGNET_ERR_ARG;

@@ -532,16 +532,16 @@ __device__ __forceinline__ void stats_finish(const ReplayArgs& A, int r, int64_t
   if (A.p_busy) {
     for (int j = tid; j < A.N; j += nth) {
       const int64_t B = (int64_t)s_busy[j];
-      const double eb = __dmul_rn(A.p_busy[nbase + j], (double)B);
+      const double eb = mul_rn(A.p_busy[nbase + j], (double)B);
       const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
-      const double e = __dadd_rn(eb, __dmul_rn(A.p_idle[nbase + j], idle));
+      const double e = add_rn(eb, mul_rn(A.p_idle[nbase + j], idle));
       s_e[j] = e;
       if (A.out_energy) A.out_energy[(size_t)r * (size_t)A.N + j] = e;
     }
     __syncthreads();
     if (tid == 0) {
       double sum = 0.0;
-      for (int j = 0; j < A.N; ++j) sum = __dadd_rn(sum, s_e[j]);
+      for (int j = 0; j < A.N; ++j) sum = add_rn(sum, s_e[j]);
       S->energy_j = sum;
     }
   }

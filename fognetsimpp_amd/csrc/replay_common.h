@@ -1,5 +1,5 @@
 // replay_common.h — device pieces shared by the two replay kernels:
-// replay.hip (N <= 256, node state in VGPRs) and replay_wide.hip (N <= 13,568,
+// replay.hip (N <= 256, node state in VGPRs) and replay_wide.hip (N <= 12,288,
 // node state in LDS + HBM).  Tick arithmetic, the FES same-tick rule and the
 // exact per-replication statistics accumulator.
 #pragma once
@@ -29,6 +29,18 @@ __device__ __forceinline__ int64_t ticks_of(uint32_t s) {
 // DESIGN.md §3.3).
 __device__ __forceinline__ bool arrives_before(int64_t a, int64_t done, int64_t dl, uint32_t S) {
   return a < done || (a == done && dl >= (int64_t)S * kTicksPerSecond);
+}
+
+// Separately rounded IEEE double operations.  hipcc contracts a*b+c into an
+// FMA by default, and __dmul_rn/__dadd_rn are plain * and + in a header, so
+// they fuse too; these carry the pragma themselves.
+__device__ __forceinline__ double mul_rn(double a, double b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ double add_rn(double a, double b) {
+#pragma clang fp contract(off)
+  return a + b;
 }
 
 // ---------------------------------------------------------------- statistics

@@ -1,0 +1,415 @@
+// replay_v2.hip — batched replay of FogNetSim++'s v2 offload model on gfx950
+// (SURVEY.md §8(f) row 2): the modules simulations/example/wirelessNet.ini:56,62
+// select,
+//   broker  BrokerBaseApp2::handleMessageWhenUp/sendPubAck/releaseResource
+//           BrokerBaseApp2.cc:62-203, 205-287, 382-406
+//   node    ComputeBrokerApp2::advertiseMIPS/releaseResource/processPacket
+//           ComputeBrokerApp2.cc:202-220, 222-245, 247-324
+// The v2 model has periodic 10-ms node timers whose phase every accepted task
+// resets, a broker timer that only local tasks re-arm, and double-valued
+// deadlines whose rounding decides releases, so it is replayed as a
+// discrete-event simulation in OMNeT++'s future-event order (tick, then
+// insertion sequence) rather than in closed form.
+//
+// One wavefront replays one replication; node j lives on lane j (N <= 64):
+// its remaining MIPS, the broker's advertised view of it, its self-message
+// (tick, sequence, kind) and the heads of its two message queues in VGPRs
+// (broker -> node tasks and node -> broker adverts/acks; latencies are fixed
+// per node, so each queue is FIFO), the queue bodies and its reservation list
+// in HBM.  Each step takes the earliest (tick, sequence) over the 64 lanes (two
+// wave minima) and over the broker's own sources (the next trace publish,
+// whose pre-insertion sequence is N + index, and the broker timer), then runs
+// that one handler.  Broker state is wave-uniform; per-task outputs and the
+// broker's request list are written by lane 0 only and a node's queues by its
+// own lane only, so every memory location has one writer in program order.
+#include "replay_common.h"
+
+namespace fognet {
+
+namespace {
+
+constexpr int64_t kAdvertPeriod = 10000000000LL;  // scheduleAt(simTime() + 0.01) (ComputeBrokerApp2.cc:219)
+constexpr int64_t kMaxV2Tick = (int64_t)1 << 53;  // ticks convert to double exactly
+constexpr uint32_t kKindAdvertise = 1u, kKindRelease = 2u;
+constexpr int32_t kMsgAdvert = 1, kMsgAck6 = 2;
+constexpr uint8_t kListNone = 0, kListLocal = 1, kListForwarded = 2;
+
+struct V2Msg {  // a message in flight: arrival tick, insertion sequence, payload
+  int64_t tick;
+  uint64_t seq;
+  int32_t kind;  // node -> broker: kMsgAdvert / kMsgAck6
+  int32_t val;   // task index, or the advertised MIPS
+};
+
+struct V2Res {  // a reservation at a node: Request{requiredTime = now.dbl() + requiredTime}
+  int32_t task;
+  int32_t pad;
+  double deadline;
+};
+
+// SimTime::dbl() of OMNeT++ 4.6: ticks times the double scale 1e-12.
+__device__ __forceinline__ double dbl(int64_t t) { return mul_rn((double)t, 1e-12); }
+
+__device__ __forceinline__ bool earlier(int64_t t, uint64_t s, int64_t t2, uint64_t s2) {
+  return t < t2 || (t == t2 && s < s2);
+}
+
+struct V2Args {
+  fognet_v2_in in;
+  fognet_v2_out out;
+  V2Msg* inq;     // [R][64][Q]
+  V2Msg* outq;    // [R][64][Q]
+  V2Res* res;     // [R][64][Q]
+  uint8_t* list;  // [R][T] broker request list membership (kList*)
+  int32_t q_log2;
+};
+
+__global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
+  const fognet_v2_in& A = P.in;
+  const fognet_v2_out& O = P.out;
+  const int r = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = A.N, T = A.T;
+  const bool own = lane < N;
+  const uint32_t Q = 1u << P.q_log2, qm = Q - 1u;
+  const size_t nbase = (size_t)r * (size_t)A.node_stride;
+  const size_t tbase = (size_t)r * (size_t)T;
+  const size_t qbase = ((size_t)r * (size_t)FOGNET_V2_MAX_NODES + (size_t)lane) << P.q_log2;
+  V2Msg* const inq = P.inq + qbase;
+  V2Msg* const outq = P.outq + qbase;
+  V2Res* const res = P.res + qbase;
+  uint8_t* const list = P.list + tbase;
+  const int64_t* const arrive = A.arrive_tick + tbase;
+  const int32_t* const reqs = A.req_mips + tbase;
+
+  const double rt = A.required_time_s[r];
+  const double rtx = mul_rn(rt, 1e12);  // SimTime + double: the double in ticks
+  const int64_t rt_ticks = (int64_t)add_rn(rtx, rtx >= 0.0 ? 0.5 : -0.5);
+  const int64_t stop = A.stop_tick[r];
+
+  // ---- node j on lane j
+  int32_t mips = 0, view = 0;  // the broker's Broker record starts at MIPS 0 (BrokerBaseApp2.cc:105)
+  int64_t dl = 0, ul = 0;
+  bool t_sched = false;  // selfMsg->isScheduled()
+  int64_t t_tick = kNever;
+  uint64_t t_seq = ~0ull;
+  uint32_t t_kind = kKindAdvertise;
+  bool bad = !(stop <= kMaxV2Tick) || !(rtx >= 0.0) || rt_ticks > kMaxV2Tick;
+  if (own) {
+    mips = A.mips[nbase + lane];
+    dl = A.dl_tick[nbase + lane];
+    ul = A.ul_tick[nbase + lane];
+    const int64_t fa = A.first_adv_tick[nbase + lane];
+    bad |= dl < 0 || ul < 0 || fa < 0 || dl > kMaxV2Tick || ul > kMaxV2Tick || fa > kMaxV2Tick;
+    t_sched = true;  // the first ADVERTISEMIPS firing, pre-inserted in node order
+    t_tick = fa;
+    t_seq = (uint64_t)lane;
+  }
+  uint32_t in_h = 0u, in_n = 0u, out_h = 0u, out_n = 0u, rs_h = 0u, rs_n = 0u;
+  V2Msg in_hd = {kNever, ~0ull, 0, 0}, out_hd = {kNever, ~0ull, 0, 0};
+
+  // ---- broker (wave-uniform)
+  int32_t pool = A.broker_mips[r];
+  bool b_sched = false;
+  int64_t b_tick = kNever;
+  uint64_t b_seq = ~0ull;
+  uint64_t seq = (uint64_t)N + (uint64_t)T;  // the publishes hold N .. N+T-1
+  int next = 0, list_h = 0;
+  int64_t prev_pub = INT64_MIN;
+  fognet_v2_stats st = {};
+  uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
+  bad = false;
+
+  while (err == FOGNET_OK) {
+    // ---- the earliest event: the lanes' own sources, then the broker's
+    int64_t ct = kNever;
+    uint64_t cs = ~0ull;
+    int src = 0;  // 1 self-message, 2 task arrival, 3 message at the broker
+    if (t_sched) {
+      ct = t_tick;
+      cs = t_seq;
+      src = 1;
+    }
+    if (in_n && earlier(in_hd.tick, in_hd.seq, ct, cs)) {
+      ct = in_hd.tick;
+      cs = in_hd.seq;
+      src = 2;
+    }
+    if (out_n && earlier(out_hd.tick, out_hd.seq, ct, cs)) {
+      ct = out_hd.tick;
+      cs = out_hd.seq;
+      src = 3;
+    }
+    const int64_t m_tick = (int64_t)wave_min_u64((uint64_t)ct);
+    const uint64_t m_seq = wave_min_u64(ct == m_tick ? cs : ~0ull);
+    const uint64_t wmask = ballot(src != 0 && ct == m_tick && cs == m_seq);
+    const int w = wmask ? (int)__builtin_ctzll(wmask) : 0;
+    int kind = wmask ? 1 : 0;  // 1 node-side event of lane w, 2 publish, 3 broker timer
+    int64_t e_tick = wmask ? m_tick : kNever;
+    uint64_t e_seq = wmask ? m_seq : ~0ull;
+    int64_t p_tick = kNever;
+    if (next < T) {
+      p_tick = arrive[next];
+      if (earlier(p_tick, (uint64_t)N + (uint64_t)next, e_tick, e_seq)) {
+        e_tick = p_tick;
+        e_seq = (uint64_t)N + (uint64_t)next;
+        kind = 2;
+      }
+    }
+    if (b_sched && earlier(b_tick, b_seq, e_tick, e_seq)) {
+      e_tick = b_tick;
+      e_seq = b_seq;
+      kind = 3;
+    }
+    if (kind == 0 || e_tick >= stop) break;  // nothing left, or the sim-time-limit
+    const int64_t now = e_tick;
+    ++st.events;
+
+    if (kind == 2) {
+      // ---- publish: BrokerBaseApp2.cc:176-195 + sendPubAck(:205-287)
+      const int t = next++;
+      if (p_tick < prev_pub || p_tick > kMaxV2Tick) {
+        err = FOGNET_ERR_ARG;  // trace not sorted / out of range
+        break;
+      }
+      prev_pub = p_tick;
+      const int32_t req = reqs[t];
+      ++st.n_tasks;
+      int32_t k = -1;
+      uint32_t status;
+      int64_t start = -1;
+      uint8_t lmark = kListNone;
+      if (req < pool) {  // :181 -> sendPubAck(true), :209-232
+        pool -= req;
+        lmark = kListLocal;
+        status = FOGNET_V2_ST_LOCAL;
+        start = now;
+        ++st.n_local;
+        b_sched = true;  // cancelEvent + scheduleAt(now + requiredTime) (:226-229)
+        b_tick = now + rt_ticks;
+        b_seq = seq++;
+      } else if (N == 0) {  // :273-285: scheduleAt without cancelEvent
+        status = FOGNET_V2_ST_NO_NODES;
+        ++st.n_no_nodes;
+        if (b_sched) {
+          err = FOGNET_ERR_STATE;  // "scheduleAt(): message already scheduled"
+        } else {
+          b_sched = true;
+          b_tick = now + rt_ticks;
+          b_seq = seq++;
+        }
+      } else {
+        // the LAST node whose advertised MIPS exceeds node 0's (:241-248), else node 0
+        const int32_t v0 = (int32_t)readlane_u32((uint32_t)view, 0);
+        k = (int32_t)~wave_min_u32(~((own && lane >= 1 && view > v0) ? (uint32_t)lane : 0u));
+        const int32_t vk = (int32_t)readlane_u32((uint32_t)view, k);
+        lmark = kListForwarded;  // :255-260, before the MIPS check
+        if (req < vk) {          // :262-270: FognetMsgTask to node k
+          status = FOGNET_V2_ST_FORWARDED;
+          ++st.n_forwarded;
+          if (lane == k) {
+            const V2Msg m = {now + dl, seq, 0, t};
+            if (in_n == Q) {
+              bad = true;
+            } else {
+              inq[(in_h + in_n) & qm] = m;
+              if (in_n == 0u) in_hd = m;
+              ++in_n;
+            }
+          }
+          ++seq;
+          if (ballot(bad)) err = FOGNET_ERR_CAPACITY;
+        } else {
+          status = FOGNET_V2_ST_DROPPED;
+          ++st.n_dropped;
+        }
+      }
+      if (lane == 0) {
+        list[t] = lmark;
+        O.node[tbase + t] = k;
+        O.status[tbase + t] = (uint8_t)status;
+        O.start_tick[tbase + t] = start;
+        O.done_tick[tbase + t] = -1;
+      }
+    } else if (kind == 3) {
+      // ---- broker RELEASERESOURCE: BrokerBaseApp2::releaseResource (:382-406), the
+      // first request with deadline <= now (the oldest live one: deadlines follow
+      // the list order), local or forwarded
+      b_sched = false;
+      int rel = -1;
+      uint32_t mark = kListNone;
+      if (lane == 0) {
+        while (list_h < next && list[list_h] == kListNone) ++list_h;
+        if (list_h < next) {
+          const double deadline = add_rn(dbl(arrive[list_h]), rt);
+          if (deadline <= dbl(now)) {
+            rel = list_h;
+            mark = list[list_h];
+            list[list_h] = kListNone;
+            if (mark == kListLocal) O.done_tick[tbase + list_h] = now;
+          }
+        }
+      }
+      list_h = __builtin_amdgcn_readfirstlane(list_h);
+      rel = __builtin_amdgcn_readfirstlane(rel);
+      mark = __builtin_amdgcn_readfirstlane(mark);
+      if (rel >= 0) {
+        pool += reqs[rel];  // :386
+        ++st.n_released_broker;
+        if (mark == kListForwarded) ++st.n_inflated;
+      }
+    } else {
+      // ---- an event of node w
+      const int wsrc = (int)readlane_u32((uint32_t)src, w);
+      if (wsrc == 3) {
+        // a node -> broker message reaches the broker (BrokerBaseApp2.cc:128-154)
+        const int32_t mk = (int32_t)readlane_u32((uint32_t)out_hd.kind, w);
+        const int32_t mv = (int32_t)readlane_u32((uint32_t)out_hd.val, w);
+        if (lane == w) {
+          ++out_h;
+          --out_n;
+          if (out_n) out_hd = outq[out_h & qm];
+          if (mk == kMsgAdvert) view = mv;  // setMips (:132)
+        }
+        if (mk == kMsgAck6) {  // relay and erase the request if it is still listed (:145-153)
+          bool relayed = false;
+          if (lane == 0 && list[mv] == kListForwarded) {
+            list[mv] = kListNone;
+            relayed = true;
+          }
+          if (ballot(relayed)) ++st.n_relayed;
+        }
+      } else {
+        // the node's own events: its self-message or a task arrival.  The owner
+        // lane runs the handler; sequence numbers and per-task results are
+        // broadcast afterwards (lane 0 writes the outputs).
+        int32_t o_task = -1;        // task whose result changed
+        uint32_t o_what = 0u;       // 1 released, 2 accepted, 3 rejected
+        bool released = false;
+        uint64_t my_seq = seq;
+        if (lane == w) {
+          if (wsrc == 1) {
+            t_sched = false;
+            if (t_kind == kKindRelease && rs_n) {
+              // ComputeBrokerApp2::releaseResource (:222-245): the first reservation
+              // with deadline < now (the oldest: deadlines follow arrival order)
+              const V2Res h = res[rs_h & qm];
+              if (h.deadline < dbl(now)) {
+                mips += reqs[h.task];  // :226
+                ++rs_h;
+                --rs_n;
+                released = true;
+                o_task = h.task;
+                o_what = 1u;
+                const V2Msg m = {now + ul, my_seq++, kMsgAck6, h.task};  // puback 6 (:231-235)
+                if (out_n == Q) bad = true;
+                else {
+                  outq[(out_h + out_n) & qm] = m;
+                  if (out_n == 0u) out_hd = m;
+                  ++out_n;
+                }
+              }
+            }
+            // advertiseMIPS (:202-220): advert, then the self-message again 0.01 s later
+            const V2Msg m = {now + ul, my_seq++, kMsgAdvert, mips};
+            if (out_n == Q) bad = true;
+            else {
+              outq[(out_h + out_n) & qm] = m;
+              if (out_n == 0u) out_hd = m;
+              ++out_n;
+            }
+            t_sched = true;
+            t_tick = now + kAdvertPeriod;
+            t_seq = my_seq++;
+          } else {
+            // ComputeBrokerApp2::processPacket, FognetMsgTask (:258-318)
+            const int32_t t = in_hd.val;
+            ++in_h;
+            --in_n;
+            if (in_n) in_hd = inq[in_h & qm];
+            o_task = t;
+            const int32_t req = reqs[t];
+            if (req < mips) {  // :269
+              mips -= req;     // :272
+              o_what = 2u;
+              if (rs_n == Q) bad = true;
+              else {
+                res[(rs_h + rs_n) & qm] = V2Res{t, 0, add_rn(dbl(now), rt)};  // :274
+                ++rs_n;
+              }
+              // cancelEvent + RELEASERESOURCE at now + requiredTime (:292-295)
+              t_kind = kKindRelease;
+              t_sched = true;
+              t_tick = now + rt_ticks;
+              t_seq = my_seq++;
+            } else {
+              o_what = 3u;  // TaskAck(false) (:299-306)
+            }
+          }
+        }
+        if (ballot(bad)) {
+          err = FOGNET_ERR_CAPACITY;
+          break;
+        }
+        seq = ((uint64_t)readlane_u32((uint32_t)(my_seq >> 32), w) << 32) | readlane_u32((uint32_t)my_seq, w);
+        o_task = (int32_t)readlane_u32((uint32_t)o_task, w);
+        o_what = readlane_u32(o_what, w);
+        if (o_what == 1u) {
+          ++st.n_released_node;
+          if (lane == 0) O.done_tick[tbase + o_task] = now;
+        } else if (o_what == 2u) {
+          ++st.n_accepted;
+          if (lane == 0) {
+            O.status[tbase + o_task] = FOGNET_V2_ST_ACCEPTED;
+            O.start_tick[tbase + o_task] = now;
+          }
+        } else if (o_what == 3u) {
+          ++st.n_rejected;
+          if (lane == 0) O.status[tbase + o_task] = FOGNET_V2_ST_REJECTED;
+        }
+        (void)released;
+      }
+    }
+  }
+
+  // ---- tasks not published before the stop (or the error), and the record
+  for (int t = next + lane; t < T; t += kWave) {
+    O.node[tbase + t] = -1;
+    O.status[tbase + t] = 0;
+    O.start_tick[tbase + t] = -1;
+    O.done_tick[tbase + t] = -1;
+  }
+  int64_t msum = own ? (int64_t)mips : 0;
+  for (int m = kWave / 2; m > 0; m >>= 1) msum += (int64_t)shfl_xor_u64((uint64_t)msum, m);
+  if (lane == 0) {
+    st.node_mips_final_sum = msum;
+    st.broker_mips_final = pool;
+    st.status = (int32_t)err;
+    O.stats[r] = st;
+  }
+}
+
+}  // namespace
+
+size_t replay_v2_workspace_bytes(int32_t R, int32_t T, int32_t q_log2) {
+  const size_t q = (size_t)R * FOGNET_V2_MAX_NODES << q_log2;
+  return q * (2 * sizeof(V2Msg) + sizeof(V2Res)) + (size_t)R * (size_t)T;
+}
+
+hipError_t launch_replay_v2(const fognet_v2_in& in, const fognet_v2_out& out, void* ws, int32_t q_log2,
+                            hipStream_t s) {
+  if (in.R <= 0) return hipSuccess;
+  V2Args a;
+  a.in = in;
+  a.out = out;
+  a.q_log2 = q_log2;
+  const size_t q = (size_t)in.R * FOGNET_V2_MAX_NODES << q_log2;
+  a.inq = reinterpret_cast<V2Msg*>(ws);
+  a.outq = a.inq + q;
+  a.res = reinterpret_cast<V2Res*>(a.outq + q);
+  a.list = reinterpret_cast<uint8_t*>(a.res + q);
+  hipLaunchKernelGGL(replay_v2_kernel, dim3(in.R), dim3(kWave), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace fognet

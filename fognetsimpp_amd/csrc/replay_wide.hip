@@ -329,16 +329,16 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
     double* const s_e = reinterpret_cast<double*>(L.nxt);  // dead now; lane j%64 wrote nxt[j]
     for (int j = lane; j < N; j += kWave) {
       const int64_t B = (int64_t)nd[j].tl_C;
-      const double eb = __dmul_rn(A.p_busy[nbase + j], (double)B);
+      const double eb = mul_rn(A.p_busy[nbase + j], (double)B);
       const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
-      const double en = __dadd_rn(eb, __dmul_rn(A.p_idle[nbase + j], idle));
+      const double en = add_rn(eb, mul_rn(A.p_idle[nbase + j], idle));
       s_e[j] = en;
       if (A.out_energy) A.out_energy[(size_t)r * (size_t)N + j] = en;
     }
     __syncthreads();
     if (lane == 0) {
       double sum = 0.0;
-      for (int j = 0; j < N; ++j) sum = __dadd_rn(sum, s_e[j]);
+      for (int j = 0; j < N; ++j) sum = add_rn(sum, s_e[j]);
       S->energy_j = sum;
     }
   }

@@ -10,6 +10,7 @@ decision, node update and statistic is computed by the gfx950 kernels in
   ``BrokerBaseApp3::sendPubAck(..., status=false)`` (BrokerBaseApp3.cc:265-281).
 * :class:`BrokerBaseApp2` — the v2 broker's local-first / "max-MIPS" forward
   (BrokerBaseApp2.cc:180-192, 235-286).
+* :func:`run_v2` — replays of the v2 model (BrokerBaseApp2 + ComputeBrokerApp2).
 * :class:`Context` + :func:`run_batch` — R independent trace replays of the
   broker/fog-node loop (BrokerBaseApp3.cc:123-158, ComputeBrokerApp3.cc:205-320).
 """
@@ -26,7 +27,7 @@ from ._abi import FognetError
 
 _TENSOR_DTYPES = {
     "arrive": torch.int64, "req": torch.int32, "mips": torch.int32,
-    "dl": torch.int64, "ul": torch.int64, "init": torch.int64,
+    "dl": torch.int64, "ul": torch.int64, "init": torch.int64, "first_adv": torch.int64,
     "p_busy": torch.float64, "p_idle": torch.float64,  # optional power model (a11)
 }
 POLICIES = {"REF_V3": _abi.FOGNET_POLICY_REF_V3, "EXT_LAT": _abi.FOGNET_POLICY_EXT_LAT}
@@ -269,6 +270,47 @@ def user_stats(ctx: Context, trace: dict, out: BatchResult, user_ul, user_dl) ->
     ctx.check(ctx._lib.fognet_user_stats_dev(ctx.handle, C.byref(bi), C.byref(bo), _ptr(uu), _ptr(ud), per_task,
                                              _ptr(res), _stream_ptr(dev)), "user_stats")
     return res.cpu().numpy().view(_abi.USER_STATS_DTYPE)
+
+
+@dataclass
+class V2Result:
+    node: torch.Tensor        # [R, T] int32 (-1: served by the broker / no node)
+    status: torch.Tensor      # [R, T] uint8 (_abi.V2_ST_*; 0: not published before the stop)
+    start_tick: torch.Tensor  # [R, T] int64 reservation tick (-1: never reserved)
+    done_tick: torch.Tensor   # [R, T] int64 release tick (-1: not released)
+    stats: torch.Tensor       # [R * sizeof(fognet_v2_stats)] uint8
+
+    def rep_stats(self) -> np.ndarray:
+        return self.stats.cpu().numpy().view(_abi.V2_STATS_DTYPE)
+
+
+def run_v2(ctx: Context, trace: dict, broker_mips, stop_tick, required_time_s=0.01, queue_capacity: int = 0,
+           stream=None) -> V2Result:
+    """R replays of the v2 model (BrokerBaseApp2 + ComputeBrokerApp2, the modules
+    simulations/example/wirelessNet.ini:56,62 select) on the device
+    (fognet_run_v2_dev).  ``trace``: device tensors arrive/req [R, T], node
+    parameters mips/dl/ul and first_adv (first ADVERTISEMIPS firing) [R, N] or
+    [N]; ``broker_mips``, ``stop_tick``, ``required_time_s``: scalars or [R]."""
+    arrive, req = trace["arrive"], trace["req"]
+    R, T = arrive.shape
+    dev = arrive.device
+    mips = trace["mips"]
+    N = mips.shape[-1]
+    for k in ("dl", "ul", "first_adv"):
+        if tuple(trace[k].shape) != tuple(mips.shape):
+            raise FognetError(_abi.FOGNET_ERR_ARG, f"{k} has shape {tuple(trace[k].shape)}, mips {tuple(mips.shape)}")
+    per = lambda v, dt: torch.as_tensor(np.array(np.broadcast_to(np.asarray(v), (R,))), dtype=dt).to(dev)
+    bm, st_, rt = per(broker_mips, torch.int32), per(stop_tick, torch.int64), per(required_time_s, torch.float64)
+    out = V2Result(torch.empty((R, T), dtype=torch.int32, device=dev), torch.empty((R, T), dtype=torch.uint8, device=dev),
+                   torch.empty((R, T), dtype=torch.int64, device=dev), torch.empty((R, T), dtype=torch.int64, device=dev),
+                   torch.zeros(R * _abi.V2_STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev))
+    vi = _abi.V2In(R, T, N, N if mips.dim() == 2 else 0, queue_capacity, 0, _ptr(arrive), _ptr(req), _ptr(bm), _ptr(rt),
+                   _ptr(st_), _ptr(mips), _ptr(trace["dl"]), _ptr(trace["ul"]), _ptr(trace["first_adv"]))
+    vo = _abi.V2Out(_ptr(out.node), _ptr(out.status), _ptr(out.start_tick), _ptr(out.done_tick), _ptr(out.stats))
+    s = C.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(dev)
+    ctx.check(ctx._lib.fognet_run_v2_dev(ctx.handle, C.byref(vi), C.byref(vo), s), "run_v2")
+    out._keep = (bm, st_, rt)
+    return out
 
 
 def summarize_moments(m) -> dict:

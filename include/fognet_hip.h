@@ -182,6 +182,65 @@ typedef struct fognet_user_stats {
     fognet_moments delay, latency, latencyH1, taskTime;
 } fognet_user_stats;
 
+/* ---- v2 model replay: BrokerBaseApp2 + ComputeBrokerApp2,
+ * the modules simulations/example/wirelessNet.ini:56,62 select.  The broker
+ * keeps its own MIPS pool with a single RELEASERESOURCE timer
+ * (BrokerBaseApp2.cc:205-233, 382-406) and forwards to the LAST node whose
+ * advertised MIPS exceeds node 0's (:235-271); a node reserves MIPS for
+ * requiredTime and runs a 10-ms advert/release timer (ComputeBrokerApp2.cc:
+ * 202-318).  Deadlines are doubles compared with simTime().dbl() = ticks *
+ * 1e-12, exactly as the reference does (their rounding decides releases). */
+#define FOGNET_V2_MAX_NODES 64
+
+typedef enum fognet_v2_task_status {
+    FOGNET_V2_ST_LOCAL = 3,      /* reserved in the broker's own pool (pubAck 3)                   */
+    FOGNET_V2_ST_FORWARDED = 4,  /* task sent, still in flight when the run stopped                */
+    FOGNET_V2_ST_DROPPED = 5,    /* MIPSRequired >= the chosen node's advertised MIPS: no task sent */
+    FOGNET_V2_ST_NO_NODES = 6,   /* no compute broker registered                                   */
+    FOGNET_V2_ST_ACCEPTED = 7,   /* reserved at the node (ComputeBrokerApp2.cc:269-295)             */
+    FOGNET_V2_ST_REJECTED = 8    /* MIPSRequired >= the node's remaining MIPS (:299-306)            */
+} fognet_v2_task_status;
+
+typedef struct fognet_v2_in {
+    int32_t R, T, N;              /* N <= FOGNET_V2_MAX_NODES                                      */
+    int32_t node_stride;          /* 0: node parameters shared; N: one row per replication         */
+    int32_t queue_capacity;       /* per-node capacity of each message queue and of the
+                                     reservation list, power of two (0 = default 256)              */
+    int32_t pad;
+    const int64_t *arrive_tick;   /* [R][T] publish arrival at the broker, nondecreasing           */
+    const int32_t *req_mips;      /* [R][T] MIPSRequired                                           */
+    const int32_t *broker_mips;   /* [R] BrokerBaseApp2 par("MIPS")                                */
+    const double *required_time_s;/* [R] MqttMsgPublish.requiredTime (mqttApp2.cc:372: 0.01)      */
+    const int64_t *stop_tick;     /* [R] sim-time-limit: events at >= stop are not run (<= 2^53)   */
+    const int32_t *mips;          /* [R|1][N] ComputeBrokerApp2 par("MIPS")                        */
+    const int64_t *dl_tick;       /* [R|1][N] broker -> node latency                               */
+    const int64_t *ul_tick;       /* [R|1][N] node -> broker latency                               */
+    const int64_t *first_adv_tick;/* [R|1][N] first ADVERTISEMIPS firing (CONNACK + 0.01 s)        */
+} fognet_v2_in;
+
+typedef struct fognet_v2_stats {
+    int64_t n_tasks, n_local, n_forwarded, n_accepted, n_rejected, n_dropped, n_no_nodes;
+    int64_t n_released_broker;    /* broker timer releases (BrokerBaseApp2.cc:382-406)            */
+    int64_t n_inflated;           /* ... of forwarded requests, credited to the broker's own pool  */
+    int64_t n_released_node;      /* node releases (ComputeBrokerApp2.cc:222-245)                 */
+    int64_t n_relayed;            /* status-6 acks that found their request at the broker         */
+    int64_t events;               /* events processed (cancelled timers excluded)                  */
+    int64_t node_mips_final_sum;
+    int32_t broker_mips_final;
+    int32_t status;               /* fognet_status of the replication                              */
+} fognet_v2_stats;
+
+typedef struct fognet_v2_out {
+    int32_t *node;                /* [R][T] chosen node, -1: served locally / no node              */
+    uint8_t *status;              /* [R][T] fognet_v2_task_status (0: not published before stop)  */
+    int64_t *start_tick;          /* [R][T] reservation tick, -1 if never reserved                 */
+    int64_t *done_tick;           /* [R][T] release tick of the reservation, -1 if not released    */
+    fognet_v2_stats *stats;       /* [R]                                                           */
+} fognet_v2_out;
+
+/* R v2 replays on the device (device pointers; enqueued on hip_stream). */
+int fognet_run_v2_dev(fognet_ctx *ctx, const fognet_v2_in *in, fognet_v2_out *out, void *hip_stream);
+
 /* Synthetic trace recipe, generated on the device.
  * Replication r uses Philox4x32-10 key (seed, r); see DESIGN.md §Trace generator. */
 typedef struct fognet_gen_params {

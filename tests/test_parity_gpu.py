@@ -549,3 +549,102 @@ def test_user_stats_with_reference_task_source(ctx):
     assert o["stats"]["status"][0] == 0 and int(o["stats"]["n_tasks"][0]) == g["arrive"].size
     np.testing.assert_array_equal(out.node.cpu().numpy(), o["node"])
     assert_user_parity(gu, o["user"])
+
+
+# ------------------------------------------------------------------ v2 model replay
+# replay_v2.hip (lane-parallel FES per replication) against the oracle's
+# heap-ordered DES restatement (oracle/fognet_oracle_v2.c).
+
+V2_FIELDS = ("n_tasks", "n_local", "n_forwarded", "n_accepted", "n_rejected", "n_dropped", "n_no_nodes",
+             "n_released_broker", "n_inflated", "n_released_node", "n_relayed", "events", "node_mips_final_sum",
+             "broker_mips_final", "status")
+
+
+def run_v2_gpu(ctx, tr, broker_mips, stop, rt=0.01, qcap=0):
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace({k: tr[k] for k in ("arrive", "req", "mips", "dl", "ul", "first_adv")}, dev)
+    out = fa.run_v2(ctx, d, broker_mips, stop, rt, queue_capacity=qcap)
+    torch.cuda.synchronize()
+    return dict(node=out.node.cpu().numpy(), status=out.status.cpu().numpy(), start=out.start_tick.cpu().numpy(),
+                done=out.done_tick.cpu().numpy(), stats=out.rep_stats())
+
+
+def assert_v2_parity(g, o):
+    for k in ("node", "status", "start", "done"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+    for f in V2_FIELDS:
+        np.testing.assert_array_equal(g["stats"][f], o["stats"][f], err_msg=f)
+
+
+@pytest.mark.parametrize("case", golden_io.replay_v2_cases(), ids=lambda c: c[0])
+def test_v2_replay_known_answers_gpu(ctx, case):
+    name, tr, e = case
+    g = run_v2_gpu(ctx, tr, tr["broker_mips"], tr["stop"])
+    assert g["node"][0].tolist() == e["node"] and g["status"][0].tolist() == e["status"]
+    assert g["start"][0].tolist() == e["start"] and g["done"][0].tolist() == e["done"]
+    assert int(g["stats"]["status"][0]) == e.get("rep_status", 0)
+    o = ol.run_v2(tr["arrive"], tr["req"], tr["broker_mips"], tr["mips"], tr["dl"], tr["ul"], tr["first_adv"],
+                  tr["stop"])
+    assert_v2_parity(g, o)
+
+
+def v2_random(seed, R, N, T):
+    """Coarse millisecond grids so arrivals, timer firings and messages share
+    ticks often (the FES insertion-order rule decides), per-replication broker
+    pools, requiredTime values and stop times; shared node parameters."""
+    rng = np.random.default_rng(seed)
+    MS = 10**9
+    gaps = rng.choice([0, 1, 2, 5, 10, 50], size=(R, T)) * MS
+    arrive = (rng.integers(0, 30, size=(R, 1)) * MS + np.cumsum(gaps, axis=1)).astype(np.int64)
+    req = rng.integers(0, 1600, size=(R, T)).astype(np.int32)
+    mips = rng.choice([500, 1000, 1500], size=(R, N)).astype(np.int32)
+    dl = rng.choice([0, 1, 2, 10, 20], size=(R, N)).astype(np.int64) * MS
+    ul = rng.choice([0, 1, 2, 10, 20], size=(R, N)).astype(np.int64) * MS
+    first = rng.integers(0, 21, size=(R, N)).astype(np.int64) * MS
+    broker = rng.choice([0, 300, 1000, 2500], size=R).astype(np.int32)
+    rt = rng.choice([0.01, 0.005, 0.02], size=R)
+    stop = arrive[:, -1] + rng.integers(0, 200, size=R) * MS
+    return dict(arrive=arrive, req=req, mips=mips, dl=dl, ul=ul, first_adv=first), broker, stop, rt
+
+
+@pytest.mark.parametrize("seed,N", [(0, 1), (1, 2), (2, 5), (3, 13), (4, 64), (5, 5)])
+def test_v2_random_matches_oracle(ctx, seed, N):
+    tr, broker, stop, rt = v2_random(seed, 16, N, 3000)
+    g = run_v2_gpu(ctx, tr, broker, stop, rt, qcap=4096)
+    o = ol.run_v2(tr["arrive"], tr["req"], broker, tr["mips"], tr["dl"], tr["ul"], tr["first_adv"], stop, rt,
+                  threads=8)
+    assert (o["stats"]["status"] == 0).all()
+    assert_v2_parity(g, o)
+
+
+def test_v2_c1_as_shipped(ctx):
+    """Config C1 (BASELINE.json configs[0]) with the modules its ini names:
+    one user (mqttApp2's timer chain + glibc rand()), broker and 5 nodes at 1000
+    MIPS, 1000 s.  Bit-exact with the oracle, including the rounding-stuck pool."""
+    from fognetsimpp_amd import formats
+    MS = 10**9
+    g0 = formats.gen_trace_mqtt(1, [0], [50 * MS], [MS], [-1], 1000 * 10**12)
+    n = 5
+    tr = dict(arrive=g0["arrive"][None], req=g0["req"][None], mips=np.full(n, 1000, np.int32), dl=np.full(n, MS),
+              ul=np.full(n, MS), first_adv=np.full(n, 20 * MS))
+    g = run_v2_gpu(ctx, tr, 1000, 1000 * 10**12)
+    o = ol.run_v2(tr["arrive"], tr["req"], 1000, tr["mips"], tr["dl"], tr["ul"], tr["first_adv"], 1000 * 10**12)
+    assert_v2_parity(g, o)
+    assert (int(g["stats"]["n_local"][0]), int(g["stats"]["n_forwarded"][0])) == (9, 19990)
+
+
+def test_v2_errors(ctx):
+    MS = 10**9
+    tr = dict(arrive=np.array([[10 * MS, 12 * MS]]), req=np.array([[150, 150]], np.int32),
+              mips=np.zeros(0, np.int32), dl=np.zeros(0, np.int64), ul=np.zeros(0, np.int64),
+              first_adv=np.zeros(0, np.int64))
+    g = run_v2_gpu(ctx, tr, 100, 100 * MS)
+    assert int(g["stats"]["status"][0]) == _abi.FOGNET_ERR_STATE
+    big = dict(arrive=np.array([[10 * MS]]), req=np.array([[1]], np.int32), mips=np.full(65, 1000, np.int32),
+               dl=np.ones(65, np.int64), ul=np.ones(65, np.int64), first_adv=np.ones(65, np.int64))
+    with pytest.raises(fa.FognetError) as e:
+        run_v2_gpu(ctx, big, 100, 100 * MS)
+    assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED
+    tr2, broker, stop, rt = v2_random(9, 2, 3, 500)
+    g = run_v2_gpu(ctx, tr2, broker, np.full(2, 2**53 + 1), rt)
+    assert (g["stats"]["status"] == _abi.FOGNET_ERR_ARG).all()
