@@ -15,13 +15,21 @@ RCCL all-reduce of histograms + energy.  Replications are sharded over ranks
 the ranks (strong scaling), on the wide replay kernel (replay_wide.hip), with
 the builder-defined light-load recipe of ``fognetsimpp_amd.c5_params``.
 
+``--workload c1`` runs config C1 (the reference's example General run,
+BASELINE.json configs[0]) with the modules its ini names (BrokerBaseApp2 +
+ComputeBrokerApp2, the v2 model): per replication one user publishing every
+50 ms for 1000 s (mqttApp2's timer chain, glibc rand() seeded with the global
+replication index + 1), broker and 5 nodes at 1000 MIPS, 1-ms links;
+replications sharded over the ranks (``--R-total``, default 4096, strong
+scaling).  Traces are generated on the host before timing.
+
 ``--workload c4`` runs config C4 (Monte Carlo what-if, BASELINE.json
 configs[3]): 1M replications x T = 10,000 x N = 256 in total, sharded over the
 ranks (strong scaling), traces generated on the device INSIDE the timed
 region in blocks of ``--block`` replications (the whole trace would be
 ~120 GB), only statistics kept.
 
-  python bench.py [--gpus N --steps K --warmup W] [--workload c3|c4|c5]
+  python bench.py [--gpus N --steps K --warmup W] [--workload c1|c3|c4|c5]
   torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -71,7 +79,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--policy", default="REF_V3", choices=("REF_V3", "EXT_LAT"))
-    ap.add_argument("--workload", default="c3", choices=("c3", "c4", "c5"))
+    ap.add_argument("--workload", default="c3", choices=("c1", "c3", "c4", "c5"))
     ap.add_argument("--R-total", type=int, default=None,
                     help="c4/c5: replications over all ranks (default 1,000,000 / 1024)")
     ap.add_argument("--block", type=int, default=4096, help="c4: replications per device block")
@@ -83,6 +91,8 @@ def main():
             args.seed = 0x5EED0004 if args.workload == "c4" else 0x5EED0005
         if args.R_total is None:
             args.R_total = 1_000_000 if args.workload == "c4" else 1024
+    if args.workload == "c1" and args.R_total is None:
+        args.R_total = 4096
     if args.workload == "c5":
         if args.N == 256:
             args.N = 10_000
@@ -111,6 +121,8 @@ def main():
     ctx = fa.Context(gpu)
     if args.workload == "c4":
         return bench_c4(args, ctx, dev, dist, world, rank)
+    if args.workload == "c1":
+        return bench_c1(args, ctx, dev, dist, world, rank)
     T, N = args.T, args.N
     if args.workload == "c5":  # a fixed job split over the ranks
         from fognetsimpp_amd.dist import shard
@@ -337,6 +349,96 @@ def bench_c4(args, ctx, dev, dist, world, rank):
             "stats": {"decisions": summary["decisions"], "queueTime_ms_mean": summary["queueTime_ms"].get("mean"),
                       "response_ms_mean": summary["response_ms"].get("mean"), "energy_j": summary["energy_j"],
                       "max_pending": summary["max_pending"], "hist_counts": [int(hist[0].sum()), int(hist[1].sum())]},
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_c1(args, ctx, dev, dist, world, rank):
+    """Config C1 on the v2 model replay (fognet_run_v2_dev)."""
+    from fognetsimpp_amd import formats
+    from fognetsimpp_amd.dist import shard
+    MS = 10**9
+    stop = 1000 * 10**12  # wirelessNet.ini:50 stopTime = 1000 s
+    n_nodes = 5
+    r0, R = shard(args.R_total, world, rank)
+    t0 = time.time()
+    gens = [formats.gen_trace_mqtt(r0 + r + 1, [0], [50 * MS], [MS], [-1], stop) for r in range(R)]  # :48 sendInterval
+    T = max(g["arrive"].size for g in gens)
+    arrive = np.full((R, T), stop, np.int64)  # padding publishes at the stop tick never run
+    req = np.zeros((R, T), np.int32)
+    for r, g in enumerate(gens):
+        arrive[r, :g["arrive"].size] = g["arrive"]
+        req[r, :g["req"].size] = g["req"]
+    tr = fa.as_device_trace(dict(arrive=arrive, req=req, mips=np.full(n_nodes, 1000, np.int32),
+                                 dl=np.full(n_nodes, MS, np.int64), ul=np.full(n_nodes, MS, np.int64),
+                                 first_adv=np.full(n_nodes, 20 * MS, np.int64)), dev)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] c1: {R} replications x {T} publishes generated in {time.time() - t0:.1f}s")
+
+    def step():
+        return fa.run_v2(ctx, tr, 1000, stop, 0.01)  # wirelessNet.ini:58,64 MIPS = 1000; mqttApp2.cc:372
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record()
+        out = step()
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    st = out.rep_stats()
+    decisions_rank = int(st["n_tasks"].sum())
+    total = torch.tensor([decisions_rank, int(st["events"].sum()), int((st["status"] != 0).sum())],
+                         dtype=torch.int64, device=dev)
+    if dist is not None:
+        dist.all_reduce(total)
+    decisions, events, failed = (int(x) for x in total.cpu().tolist())
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        reps = min(R, 1024)  # ~10-30 s of single-core work in total
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        t1 = time.perf_counter()
+        o = oracle_lib.run_v2(arrive[:reps], req[:reps], 1000, np.full(n_nodes, 1000, np.int32), np.full(n_nodes, MS),
+                              np.full(n_nodes, MS), np.full(n_nodes, 20 * MS), stop, 0.01, threads=threads)
+        dt = time.perf_counter() - t1
+        same = bool(np.array_equal(o["node"], out.node[:reps].cpu().numpy()) and
+                    np.array_equal(o["done"], out.done_tick[:reps].cpu().numpy()))
+        cpu = {"value": float(o["stats"]["n_tasks"].sum()) / dt, "unit": "decisions/s", "cores": threads,
+               "kind": "port", "sample": f"{reps} replications of the same C1 traces (v2 oracle DES), "
+                                         f"outputs identical to the device: {same}", "wall_s": dt}
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": decisions * args.steps / elapsed, "unit": "decisions/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (mqttApp2 task source, glibc rand() per replication)",
+            "config": {"workload": "C1 example General run, v2 modules (BASELINE.json configs[0])",
+                       "R_total": args.R_total, "T_max": T, "N": n_nodes, "model": "BrokerBaseApp2 + ComputeBrokerApp2",
+                       "parallelism": f"replications sharded over {world} GPU(s)"},
+            "roofline": {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None,
+                         "traffic": None, "kernel": "replay_v2_kernel", "kernel_ms_per_step": kern_ms,
+                         "events_per_s": events * args.steps / elapsed,
+                         "note": "event-driven (~53 FES events per publish); no HBM roofline applies"},
+            "cpu_baseline": cpu, "failed_replications": failed,
+            "stats": {"decisions": decisions, "events": events, "local": int(st["n_local"].sum()),
+                      "forwarded": int(st["n_forwarded"].sum())},
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

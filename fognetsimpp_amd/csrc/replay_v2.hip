@@ -37,13 +37,13 @@ constexpr uint8_t kListNone = 0, kListLocal = 1, kListForwarded = 2;
 struct V2Msg {  // a message in flight: arrival tick, insertion sequence, payload
   int64_t tick;
   uint64_t seq;
-  int32_t kind;  // node -> broker: kMsgAdvert / kMsgAck6
+  int32_t kind;  // node -> broker: kMsgAdvert / kMsgAck6; broker -> node: the task's MIPSRequired
   int32_t val;   // task index, or the advertised MIPS
 };
 
 struct V2Res {  // a reservation at a node: Request{requiredTime = now.dbl() + requiredTime}
   int32_t task;
-  int32_t pad;
+  int32_t req;  // its MIPSRequired
   double deadline;
 };
 
@@ -116,6 +116,9 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
   uint64_t seq = (uint64_t)N + (uint64_t)T;  // the publishes hold N .. N+T-1
   int next = 0, list_h = 0;
   int64_t prev_pub = INT64_MIN;
+  // the next publish, loaded one publish ahead
+  int64_t p_tick = T > 0 ? arrive[0] : kNever;
+  int32_t p_req = T > 0 ? reqs[0] : 0;
   fognet_v2_stats st = {};
   uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
   bad = false;
@@ -147,9 +150,7 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
     int kind = wmask ? 1 : 0;  // 1 node-side event of lane w, 2 publish, 3 broker timer
     int64_t e_tick = wmask ? m_tick : kNever;
     uint64_t e_seq = wmask ? m_seq : ~0ull;
-    int64_t p_tick = kNever;
     if (next < T) {
-      p_tick = arrive[next];
       if (earlier(p_tick, (uint64_t)N + (uint64_t)next, e_tick, e_seq)) {
         e_tick = p_tick;
         e_seq = (uint64_t)N + (uint64_t)next;
@@ -173,7 +174,11 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
         break;
       }
       prev_pub = p_tick;
-      const int32_t req = reqs[t];
+      const int32_t req = p_req;
+      if (next < T) {  // the following publish, in flight while this one is handled
+        p_tick = arrive[next];
+        p_req = reqs[next];
+      }
       ++st.n_tasks;
       int32_t k = -1;
       uint32_t status;
@@ -208,7 +213,7 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
           status = FOGNET_V2_ST_FORWARDED;
           ++st.n_forwarded;
           if (lane == k) {
-            const V2Msg m = {now + dl, seq, 0, t};
+            const V2Msg m = {now + dl, seq, req, t};
             if (in_n == Q) {
               bad = true;
             } else {
@@ -295,7 +300,7 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
               // with deadline < now (the oldest: deadlines follow arrival order)
               const V2Res h = res[rs_h & qm];
               if (h.deadline < dbl(now)) {
-                mips += reqs[h.task];  // :226
+                mips += h.req;  // :226
                 ++rs_h;
                 --rs_n;
                 released = true;
@@ -324,17 +329,17 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
           } else {
             // ComputeBrokerApp2::processPacket, FognetMsgTask (:258-318)
             const int32_t t = in_hd.val;
+            const int32_t req = in_hd.kind;
             ++in_h;
             --in_n;
             if (in_n) in_hd = inq[in_h & qm];
             o_task = t;
-            const int32_t req = reqs[t];
             if (req < mips) {  // :269
               mips -= req;     // :272
               o_what = 2u;
               if (rs_n == Q) bad = true;
               else {
-                res[(rs_h + rs_n) & qm] = V2Res{t, 0, add_rn(dbl(now), rt)};  // :274
+                res[(rs_h + rs_n) & qm] = V2Res{t, req, add_rn(dbl(now), rt)};  // :274
                 ++rs_n;
               }
               // cancelEvent + RELEASERESOURCE at now + requiredTime (:292-295)
