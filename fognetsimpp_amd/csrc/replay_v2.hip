@@ -50,6 +50,16 @@ struct V2Res {  // a reservation at a node: Request{requiredTime = now.dbl() + r
 // SimTime::dbl() of OMNeT++ 4.6: ticks times the double scale 1e-12.
 __device__ __forceinline__ double dbl(int64_t t) { return mul_rn((double)t, 1e-12); }
 
+// Wave minimum when only lanes < 16 can hold a candidate (N <= 16): the four
+// in-row DPP butterflies of wave_min_u64, then row 0's value.
+__device__ __forceinline__ uint64_t row0_min_u64(uint64_t v) {
+  v = umin64(v, dpp_u64<0xB1>(v));
+  v = umin64(v, dpp_u64<0x4E>(v));
+  v = umin64(v, dpp_u64<0x141>(v));
+  v = umin64(v, dpp_u64<0x140>(v));
+  return (uint64_t)readlane_i64((int64_t)v, 0);
+}
+
 __device__ __forceinline__ bool earlier(int64_t t, uint64_t s, int64_t t2, uint64_t s2) {
   return t < t2 || (t == t2 && s < s2);
 }
@@ -143,9 +153,16 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       cs = out_hd.seq;
       src = 3;
     }
-    const int64_t m_tick = (int64_t)wave_min_u64((uint64_t)ct);
-    const uint64_t m_seq = wave_min_u64(ct == m_tick ? cs : ~0ull);
-    const uint64_t wmask = ballot(src != 0 && ct == m_tick && cs == m_seq);
+    const int64_t m_tick = (int64_t)(N <= 16 ? row0_min_u64((uint64_t)ct) : wave_min_u64((uint64_t)ct));
+    const uint64_t tied = ballot(src != 0 && ct == m_tick);
+    uint64_t m_seq = ~0ull, wmask = tied;
+    if (__popcll(tied) > 1) {  // same-tick events on several nodes: insertion order decides
+      m_seq = N <= 16 ? row0_min_u64(ct == m_tick ? cs : ~0ull) : wave_min_u64(ct == m_tick ? cs : ~0ull);
+      wmask = ballot(src != 0 && ct == m_tick && cs == m_seq);
+    } else if (tied) {
+      m_seq = ((uint64_t)readlane_u32((uint32_t)(cs >> 32), __builtin_ctzll(tied)) << 32) |
+              readlane_u32((uint32_t)cs, __builtin_ctzll(tied));
+    }
     const int w = wmask ? (int)__builtin_ctzll(wmask) : 0;
     int kind = wmask ? 1 : 0;  // 1 node-side event of lane w, 2 publish, 3 broker timer
     int64_t e_tick = wmask ? m_tick : kNever;
