@@ -22,6 +22,7 @@ FOGNET_ERR_DEVICE = 5
 FOGNET_ERR_OOM = 6
 FOGNET_ERR_CAPACITY = 7
 FOGNET_ERR_UNSUPPORTED = 8
+TASK_QUEUED, TASK_STARTED, TASK_LOST = 4, 5, 9  # fognet_task_status
 
 FOGNET_POLICY_REF_V3 = 1
 FOGNET_POLICY_REF_V2 = 2
@@ -29,7 +30,7 @@ FOGNET_POLICY_EXT_LAT = 16
 TICKS_PER_SECOND = 10**12
 # fognet_v2_action (BrokerBaseApp2 decision outcome)
 V2_LOCAL, V2_FORWARD, V2_DROPPED, V2_NO_NODES = 3, 4, 5, 6
-ABI_VERSION = 4
+ABI_VERSION = 5
 HIST_METRICS = 2  # 0 queueTime, 1 response
 HIST_BINS = 64
 
@@ -107,7 +108,7 @@ class BatchIn(C.Structure):
         ("node_stride", C.c_int32), ("ring_capacity", C.c_int32),
         ("arrive_tick", C.c_void_p), ("req_mips", C.c_void_p), ("mips", C.c_void_p),
         ("dl_tick", C.c_void_p), ("ul_tick", C.c_void_p), ("init_adv_tick", C.c_void_p),
-        ("p_busy_w", C.c_void_p), ("p_idle_w", C.c_void_p),
+        ("p_busy_w", C.c_void_p), ("p_idle_w", C.c_void_p), ("down_tick", C.c_void_p),
     ]
 
 

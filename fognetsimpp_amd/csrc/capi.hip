@@ -65,6 +65,8 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
     return fail(c, FOGNET_ERR_UNSUPPORTED, "unknown policy");
   if ((in->p_busy_w == nullptr) != (in->p_idle_w == nullptr))
     return fail(c, FOGNET_ERR_ARG, "p_busy_w and p_idle_w must both be given or both be null");
+  if (in->down_tick && in->p_busy_w)
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "the power model assumes nodes that stay up (down_tick with p_busy_w)");
   if (in->node_stride != 0 && in->node_stride != in->N)
     return fail(c, FOGNET_ERR_ARG, "node_stride must be 0 or N");
   int q = in->ring_capacity ? in->ring_capacity : 1024;
@@ -96,6 +98,7 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   a->policy = in->policy;
   a->p_busy = in->p_busy_w;
   a->p_idle = in->p_idle_w;
+  a->down = in->down_tick;
   return FOGNET_OK;
 }
 
@@ -273,8 +276,8 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
   a.hist = out->hist;
   if (a.out_energy && !a.p_busy) return fail(c, FOGNET_ERR_ARG, "node_energy_j needs the power model (p_busy_w/p_idle_w)");
   hipError_t e = hipSuccess;
-  if (use_wide(a.N)) {
-    // the wide kernel accumulates the statistics while it replays, so the
+  if (use_wide(a.N) || a.down) {
+    // crashes are only modelled by the wide kernel; it accumulates the statistics while it replays, so the
     // statistics-only stage has nothing left to do
     if (!(which & 1)) return FOGNET_OK;
     const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N);
@@ -324,31 +327,33 @@ int fognet_run_batch(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out*
   const size_t NR = in->node_stride ? R : 1;
   const size_t HB = FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(int64_t);
   const bool pw = in->p_busy_w != nullptr;
-  // inputs 0..7, outputs 8..14
-  const void* hsrc[8] = {in->arrive_tick, in->req_mips, in->mips, in->dl_tick, in->ul_tick, in->init_adv_tick,
-                         in->p_busy_w, in->p_idle_w};
-  const size_t isz[8] = {R * T * 8, R * T * 4, NR * N * 4, NR * N * 8, NR * N * 8, NR * N * 8,
-                         pw ? NR * N * 8 : 0, pw ? NR * N * 8 : 0};
+  const bool dn = in->down_tick != nullptr;
+  // inputs 0..8, outputs 9..15
+  const void* hsrc[9] = {in->arrive_tick, in->req_mips, in->mips, in->dl_tick, in->ul_tick, in->init_adv_tick,
+                         in->p_busy_w, in->p_idle_w, in->down_tick};
+  const size_t isz[9] = {R * T * 8, R * T * 4, NR * N * 4, NR * N * 8, NR * N * 8, NR * N * 8,
+                         pw ? NR * N * 8 : 0, pw ? NR * N * 8 : 0, dn ? NR * N * 8 : 0};
   void* hdst[7] = {out->node, out->status, out->start_tick, out->done_tick, out->stats, out->node_energy_j,
                    out->hist};
   const size_t osz[7] = {R * T * 4, R * T * 1, R * T * 8, R * T * 8, R * sizeof(fognet_rep_stats),
                          out->node_energy_j ? R * N * 8 : 0, out->hist ? HB : 0};
-  void* d[15] = {};
+  void* d[16] = {};
   auto cleanup = [&]() {
-    for (int i = 0; i < 15; ++i)
+    for (int i = 0; i < 16; ++i)
       if (d[i]) (void)hipFree(d[i]);
   };
-  for (int i = 0; i < 15; ++i) {
-    const size_t sz = i < 8 ? isz[i] : osz[i - 8];
+  for (int i = 0; i < 16; ++i) {
+    const size_t sz = i < 9 ? isz[i] : osz[i - 9];
     if (i >= 6 && i < 8 && !pw) continue;
-    if (i >= 13 && !hdst[i - 8]) continue;
+    if (i == 8 && !dn) continue;
+    if (i >= 14 && !hdst[i - 9]) continue;
     hipError_t e = hipMalloc(&d[i], sz ? sz : 8);
     if (e != hipSuccess) {
       cleanup();
       return hip_fail(c, e, "hipMalloc batch");
     }
-    if (i < 8 && sz) e = hipMemcpyAsync(d[i], hsrc[i], sz, hipMemcpyHostToDevice, c->stream);
-    if (i == 14 && e == hipSuccess) e = hipMemcpyAsync(d[i], hdst[6], sz, hipMemcpyHostToDevice, c->stream);
+    if (i < 9 && sz) e = hipMemcpyAsync(d[i], hsrc[i], sz, hipMemcpyHostToDevice, c->stream);
+    if (i == 15 && e == hipSuccess) e = hipMemcpyAsync(d[i], hdst[6], sz, hipMemcpyHostToDevice, c->stream);
     if (e != hipSuccess) {
       cleanup();
       return hip_fail(c, e, "copy-in");
@@ -363,8 +368,9 @@ int fognet_run_batch(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out*
   din.init_adv_tick = (const int64_t*)d[5];
   din.p_busy_w = (const double*)d[6];
   din.p_idle_w = (const double*)d[7];
-  fognet_batch_out dout = {(int32_t*)d[8], (uint8_t*)d[9], (int64_t*)d[10], (int64_t*)d[11],
-                           (fognet_rep_stats*)d[12], (double*)d[13], (int64_t*)d[14]};
+  din.down_tick = (const int64_t*)d[8];
+  fognet_batch_out dout = {(int32_t*)d[9], (uint8_t*)d[10], (int64_t*)d[11], (int64_t*)d[12],
+                           (fognet_rep_stats*)d[13], (double*)d[14], (int64_t*)d[15]};
   rc = fognet_run_batch_dev(c, &din, &dout, c->stream);
   if (rc) {
     cleanup();
@@ -372,7 +378,7 @@ int fognet_run_batch(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out*
   }
   for (int i = 0; i < 7; ++i) {
     if (!hdst[i] || !osz[i]) continue;
-    hipError_t e = hipMemcpyAsync(hdst[i], d[8 + i], osz[i], hipMemcpyDeviceToHost, c->stream);
+    hipError_t e = hipMemcpyAsync(hdst[i], d[9 + i], osz[i], hipMemcpyDeviceToHost, c->stream);
     if (e != hipSuccess) {
       cleanup();
       return hip_fail(c, e, "copy-out");

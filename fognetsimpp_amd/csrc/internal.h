@@ -174,6 +174,7 @@ struct ReplayArgs {
   const double* p_idle;
   double* out_energy;     // [R][N] (nullable)
   int64_t* hist;          // [FOGNET_HIST_METRICS][FOGNET_HIST_BINS], added to (nullable)
+  const int64_t* down;    // [R|1][N] node crash ticks (nullable; wide kernel only)
 };
 
 // FOGNET_HIST_BINS rule (fognet_hip.h): whole milliseconds, log2 bins.

@@ -26,6 +26,14 @@
 // lowest index, the strict '<' of BrokerBaseApp3.cc:273), and the owner lane
 // of the chosen node appends the task and accumulates its statistics (the
 // same record replay.hip's fused epilogue writes).
+//
+// Node-down extension (A.down, fognet_hip.h; handleNodeCrash,
+// ComputeBrokerApp3.cc:423-427): from its crash tick c on a node starts and
+// completes nothing and drops arriving tasks (status 9).  A task's completion
+// is kNever when it would start or finish at or after c, so its advert never
+// becomes due and the broker keeps the node's last advert, as the reference
+// does; lost tasks still join the node's chain so the pending count (and
+// max_pending) follows the reference's `brokers` bookkeeping.
 #include "replay_common.h"
 
 namespace fognet {
@@ -129,7 +137,7 @@ __device__ __forceinline__ bool apply_advert(int j, WideNode* nd, const WideEntr
     h.hd_C = nx.C;
     h.hd_S = nx.S;
     h.hd_next = nx.next;  // valid while npend >= 2
-    L.nxt[j] = nx.done + ul;
+    L.nxt[j] = nx.done == kNever ? kNever : nx.done + ul;  // never: crashed before it completes
   }
   nd[j] = h;
   return busy < 0xFFFFFFFFull;
@@ -163,7 +171,9 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
   for (int j = lane; j < N; j += kWave) {
     const int32_t m = A.mips[nbase + j];
     const int64_t d = A.dl[nbase + j], u = A.ul[nbase + j], ia = A.init[nbase + j];
+    const int64_t dn = A.down ? A.down[nbase + j] : kNever;
     bad |= (m <= 0) | (d < 0) | (u < 0) | (d > kMaxTick) | (u > kMaxTick) | (ia < u) | (ia >= arrive0);
+    bad |= dn != kNever && (dn < ia || dn > kMaxTick);
     if constexpr (kExt) bad |= d >= kExtMaxDl;
     L.nxt[j] = kNever;
     L.busy[j] = 0u;
@@ -180,6 +190,7 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
   lane_min(L, lane, mn, mj, mk);
   Acc acc = acc_identity();
   uint32_t max_pend = 0u;  // over this lane's nodes
+  int n_short = 0;         // tasks of this lane's nodes that never complete (node-down)
   int64_t prev_t = INT64_MIN;
   int n_done = 0;
 
@@ -243,21 +254,29 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
         const int32_t mips_k = A.mips[nbase + k];
         const int64_t dl_k = A.dl[nbase + k], ul_k = A.ul[nbase + k];
         const uint32_t S = rq / (uint32_t)mips_k;  // double tskTime = requiredMIPS / MIPS (:276)
+        const int64_t down_k = A.down ? A.down[nbase + k] : kNever;
         const int64_t a = t + dl_k;
-        // the previous task on node k is its tail (FIFO single server)
+        // the previous task on node k is its tail (FIFO single server); its
+        // done is kNever if the node crashed before completing it
         const int64_t prev_done = h.tl >= 0 ? h.tl_done : INT64_MIN;
         const uint32_t prev_S = h.tl_S;
-        const int64_t start = a > prev_done ? a : prev_done;
-        const int64_t done = start + ticks_of(min(S, kWideMaxS));
-        uint32_t status;
-        if (prev_done < a) {
-          status = 5u;  // idle: "task assigned" (:282-301)
-        } else if (prev_done > a) {
-          status = 4u;  // busy: "task queued" (:304-313)
-        } else {        // the previous task completes at the same tick
-          status = dl_k < (int64_t)prev_S * kTicksPerSecond ? 5u : 4u;
+        int64_t start = kNever, done = kNever;
+        uint32_t status = FOGNET_TASK_LOST;  // reaches a crashed host: dropped, no ack
+        if (a < down_k) {
+          start = a > prev_done ? a : prev_done;
+          if (prev_done < a) {
+            status = 5u;  // idle: "task assigned" (:282-301)
+          } else if (prev_done > a) {
+            status = 4u;  // busy: "task queued" (:304-313)
+          } else {        // the previous task completes at the same tick
+            status = dl_k < (int64_t)prev_S * kTicksPerSecond ? 5u : 4u;
+          }
+          if (start != kNever) {  // start < down_k: prev_done is kNever or < down_k
+            done = start + ticks_of(min(S, kWideMaxS));
+            if (done >= down_k) done = kNever;  // the crash cancels its RELEASERESOURCE
+          }
         }
-        lerr = S > kWideMaxS || a > kMaxTick || done > kMaxTick;
+        lerr = (status != FOGNET_TASK_LOST && S > kWideMaxS) || a > kMaxTick || (done != kNever && done > kMaxTick);
         if (!lerr) {
           const int i = c0 + jp;
           const uint64_t C = h.tl_C + S;
@@ -267,7 +286,7 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
             h.hd_done = done;
             h.hd_C = C;
             h.hd_S = S;
-            const int64_t x = done + ul_k;
+            const int64_t x = done == kNever ? kNever : done + ul_k;
             const int g = ((int)k / kWave) / kWideGroupSlots;
             L.nxt[k] = x;
             if (x < L.g_nxt[g * kWave + lane]) {
@@ -294,12 +313,29 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
           const size_t o = tbase + (size_t)i;
           A.out_node[o] = (int32_t)k;
           A.out_status[o] = (uint8_t)status;
-          A.out_start[o] = start;
-          A.out_done[o] = done;
-          acc_task(acc, t, a, start, done, S, status);
-          if (hist) {
-            atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - t)], 1u);
-            if (status == 4u) atomicAdd(&L.hist[hist_bin(start - a)], 1u);
+          A.out_start[o] = start == kNever ? -1 : start;
+          A.out_done[o] = done == kNever ? -1 : done;
+          if (done != kNever) {
+            acc_task(acc, t, a, start, done, S, status);
+            if (hist) {
+              atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - t)], 1u);
+              if (status == 4u) atomicAdd(&L.hist[hist_bin(start - a)], 1u);
+            }
+          } else {
+            // node-down: acked at arrival (status 4/5) or lost; a queued task that
+            // started before the crash still emitted its queueTime (:238)
+            n_short += 1;
+            if (status == 5u) acc.n5 += 1u;
+            if (status == 4u) {
+              acc.n4 += 1u;
+              if (start != kNever) {
+                const int64_t q = start - a;
+                add_moment(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, (uint64_t)q);
+                acc.qmin = min(acc.qmin, q);
+                acc.qmax = max(acc.qmax, q);
+                if (hist) atomicAdd(&L.hist[hist_bin(q)], 1u);
+              }
+            }
           }
         }
       }
@@ -314,12 +350,16 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
   // ---- per-replication record (the fields replay_kernel + its epilogue write)
   acc = wave_merge(acc);
   const uint32_t mp = ~wave_min_u32(~max_pend);
+  int shorts = n_short;
+  for (int m = kWave / 2; m > 0; m >>= 1) shorts += __shfl_xor(shorts, m, kWave);
   fognet_rep_stats* const S = A.out_stats + r;
   if (lane == 0 && A.out_stats) {
     S->n_tasks = n_done;
     S->max_pending = (int32_t)mp;
     S->status = (int32_t)err;
-    S->events = 2 * (int64_t)N + 4 * (int64_t)n_done;
+    // initial adverts + publish, arrival, release, advert per task (publish,
+    // arrival for a task a crash keeps from completing)
+    S->events = 2 * (int64_t)N + 4 * (int64_t)n_done - 2 * (int64_t)shorts;
     write_rep_stats(S, acc);
   }
   // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12)

@@ -68,9 +68,10 @@ __global__ __launch_bounds__(kUserThreads) void user_stats_kernel(ReplayArgs A, 
     const int64_t at_arrival = t + A.dl[nbase + k] + relay - created;  // node ack sent at the task's arrival
     if (st == 5u)
       mom_add(m[1], at_arrival);  // "task assigned" -> latency
-    else
+    else if (st == 4u)
       mom_add(m[2], at_arrival);  // "task queued" -> latencyH1
-    mom_add(m[3], done + relay - created);        // status 6 -> taskTime
+    // (status 9: the task reached a crashed node, which sends no ack)
+    if (done >= 0) mom_add(m[3], done + relay - created);  // status 6 -> taskTime (-1: never completed)
   }
   fognet_moments* dst[kSignals] = {&out[r].delay, &out[r].latency, &out[r].latencyH1, &out[r].taskTime};
   for (int s = 0; s < kSignals; ++s) {

@@ -29,7 +29,9 @@ _TENSOR_DTYPES = {
     "arrive": torch.int64, "req": torch.int32, "mips": torch.int32,
     "dl": torch.int64, "ul": torch.int64, "init": torch.int64, "first_adv": torch.int64,
     "p_busy": torch.float64, "p_idle": torch.float64,  # optional power model (a11)
+    "down": torch.int64,  # optional node crash ticks (node-down extension)
 }
+NEVER = np.iinfo(np.int64).max  # down tick of a node that never crashes
 POLICIES = {"REF_V3": _abi.FOGNET_POLICY_REF_V3, "EXT_LAT": _abi.FOGNET_POLICY_EXT_LAT}
 
 
@@ -207,7 +209,9 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
 
     ``trace``: device tensors arrive/req [R, T], node params mips/dl/ul/init
     [R, N] (per replication) or [N] (shared), optional power model
-    p_busy/p_idle (W, same shape as mips).  ``stage``: "all", "replay"
+    p_busy/p_idle (W, same shape as mips), optional node crash ticks ``down``
+    (same shape as mips, NEVER = no crash; ComputeBrokerApp3::handleNodeCrash,
+    ComputeBrokerApp3.cc:423-427: lost tasks get status 9).  ``stage``: "all", "replay"
     (fognet_replay_dev) or "stats" (fognet_rep_stats_dev).  ``policy``:
     "REF_V3" (BrokerBaseApp3) or "EXT_LAT" (north-star cost, not in the
     reference).  ``hist``: allocate the job histogram when ``out`` is None.
@@ -220,7 +224,8 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
     pol = POLICIES[policy] if isinstance(policy, str) else int(policy)
     energy = trace.get("p_busy") is not None
     # host-side shape checks: the kernels index every array with these strides
-    for k in ("dl", "ul", "init") + (("p_busy", "p_idle") if energy else ()):
+    down = trace.get("down")
+    for k in ("dl", "ul", "init") + (("p_busy", "p_idle") if energy else ()) + (("down",) if down is not None else ()):
         if tuple(trace[k].shape) != tuple(mips.shape):
             raise FognetError(_abi.FOGNET_ERR_ARG, f"{k} has shape {tuple(trace[k].shape)}, mips {tuple(mips.shape)}")
     if tuple(req.shape) != (R, T) or (mips.dim() == 2 and mips.shape[0] != R):
@@ -231,7 +236,7 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
         out = allocate_outputs(R, T, arrive.device, N=N, energy=energy, hist=hist)
     bi = _abi.BatchIn(R, T, N, pol, stride, ring_capacity,
                       _ptr(arrive), _ptr(req), _ptr(mips), _ptr(trace["dl"]), _ptr(trace["ul"]),
-                      _ptr(trace["init"]), _ptr(trace.get("p_busy")), _ptr(trace.get("p_idle")))
+                      _ptr(trace["init"]), _ptr(trace.get("p_busy")), _ptr(trace.get("p_idle")), _ptr(down))
     bo = _abi.BatchOut(_ptr(out.node), _ptr(out.status), _ptr(out.start_tick), _ptr(out.done_tick),
                        _ptr(out.stats), _ptr(out.node_energy), _ptr(out.hist))
     s = C.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(arrive.device)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define FOGNET_ABI_VERSION 4
+#define FOGNET_ABI_VERSION 5
 #define FOGNET_TICKS_PER_SECOND 1000000000000LL
 
 /* Latency histograms (device-side statistics, summed over replications; the
@@ -143,13 +143,28 @@ typedef struct fognet_batch_in {
                                      ul <= init_adv < arrive[0] (all adverts land before task 0)  */
     const double *p_busy_w;       /* [R|1][N] node power while serving, W (nullable: no energy)   */
     const double *p_idle_w;       /* [R|1][N] node power while idle, W (null iff p_busy_w is)     */
+    /* Node-down extension (not one of the reference's scenarios): [R|1][N] tick at which
+     * node j crashes (INT64_MAX = never; otherwise init_adv_tick <= down < 2^61), nullable.
+     * INET lifecycle, ComputeBrokerApp3::handleNodeCrash (ComputeBrokerApp3.cc:423-427):
+     * the node's RELEASERESOURCE timer is cancelled and the host drops arriving tasks;
+     * the broker keeps its last advert.  The crash precedes every model event of its
+     * tick.  Replays with crashes run on the wide kernel; not combinable with the power
+     * model (ERR_UNSUPPORTED); not stored in trace files (fognet_io.h). */
+    const int64_t *down_tick;
 } fognet_batch_in;
+
+/* Per-task status (fognet_batch_out.status). */
+typedef enum fognet_task_status {
+    FOGNET_TASK_QUEUED = 4,   /* node ack "task queued"   (ComputeBrokerApp3.cc:304-313)       */
+    FOGNET_TASK_STARTED = 5,  /* node ack "task assigned" (ComputeBrokerApp3.cc:282-301)       */
+    FOGNET_TASK_LOST = 9      /* reached a crashed node (down_tick): no ack, never served       */
+} fognet_task_status;
 
 typedef struct fognet_batch_out {
     int32_t *node;            /* [R][T] chosen node                                               */
-    uint8_t *status;          /* [R][T] 5 = started on arrival, 4 = queued                        */
-    int64_t *start_tick;      /* [R][T] service start                                             */
-    int64_t *done_tick;       /* [R][T] completion (RELEASERESOURCE) tick                         */
+    uint8_t *status;          /* [R][T] fognet_task_status: 5 started on arrival, 4 queued, 9 lost */
+    int64_t *start_tick;      /* [R][T] service start (-1: never started, node-down only)         */
+    int64_t *done_tick;       /* [R][T] completion (RELEASERESOURCE) tick (-1: never, node-down)  */
     fognet_rep_stats *stats;  /* [R] (all five arrays are required; a stats-only mode that skips
                                  the per-task arrays is not implemented yet: ERR_UNSUPPORTED)    */
     double *node_energy_j;    /* [R][N] per-node energy (nullable; needs the power model)         */

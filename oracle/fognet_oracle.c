@@ -23,7 +23,7 @@
 
 #define TICKS_PER_SECOND 1000000000000LL /* simtime scale 1e-12 (no simtime-scale in any ini) */
 
-enum { EV_PUBLISH = 0, EV_ADVERT = 1, EV_TASK = 2, EV_SELF = 3, EV_ACK_AT_BROKER = 4, EV_ACK_AT_USER = 5 };
+enum { EV_PUBLISH = 0, EV_ADVERT = 1, EV_TASK = 2, EV_SELF = 3, EV_ACK_AT_BROKER = 4, EV_ACK_AT_USER = 5, EV_CRASH = 6 };
 enum { KIND_ADVERTISEMIPS = 1, KIND_RELEASERESOURCE = 2 }; /* ComputeBrokerApp3.h selfMsg kinds */
 
 typedef struct {
@@ -101,6 +101,7 @@ typedef struct {
     int64_t qh, qn, qcap;
     int64_t pending;       /* assigned by the broker, advert of its completion not yet at broker */
     int64_t served_s;      /* service seconds of completed tasks (energy model, a11) */
+    int down;              /* crashed (node-down extension): the app handles nothing */
 } node_t;
 
 typedef struct {
@@ -267,6 +268,10 @@ static int node_release(sim_t *s, int32_t k) {
 /* ComputeBrokerApp3::processPacket, FognetMsgTask branch, ComputeBrokerApp3.cc:269-320. */
 static int node_task(sim_t *s, int32_t k, int64_t t) {
     node_t *nd = &s->nodes[k];
+    if (nd->down) { /* a crashed host drops the packet: no ack, no service */
+        if (s->out->status) s->out->status[t] = ORC_TASK_LOST;
+        return ORC_OK;
+    }
     int32_t req = s->in->req_mips[t];
     if (nd->MIPS == 0) return ORC_ERR_DIV0;
     double tskTime = (double)(req / nd->MIPS); /* :276 int / int */
@@ -419,6 +424,13 @@ static int dispatch(sim_t *s, const ev_t *e) {
         user_ack(s, e);
         return ORC_OK;
     }
+    if (e->type == EV_CRASH) { /* handleNodeCrash: cancelEvent(selfMsg) (ComputeBrokerApp3.cc:423-427) */
+        s->nodes[e->node].down = 1;
+        node_cancel_self(s, e->node);
+        return ORC_OK;
+    }
+    if (e->type == EV_SELF && (e->gen != s->nodes[e->node].self_gen || !s->nodes[e->node].self_scheduled))
+        return ORC_OK; /* cancelled: cancelEvent removed it from the FES, not an event */
     s->st.events++;
     switch (e->type) {
     case EV_PUBLISH:
@@ -473,8 +485,11 @@ int orc_run_rep(const orc_rep_in *in, orc_rep_out *out) {
         }
     }
     int rc = ORC_OK;
-    if (out->node)
-        for (int64_t t = 0; t < T; t++) out->node[t] = -1;
+    for (int64_t t = 0; t < T; t++) {
+        if (out->node) out->node[t] = -1;
+        if (out->start_tick) out->start_tick[t] = -1;
+        if (out->done_tick) out->done_tick[t] = -1;
+    }
     if (N <= 0) {
         rc = ORC_ERR_NO_NODES;
         goto done;
@@ -494,6 +509,28 @@ int orc_run_rep(const orc_rep_in *in, orc_rep_out *out) {
         rc = node_schedule_self(&s, k, in->init_adv_tick[k] - in->ul_tick[k], KIND_ADVERTISEMIPS);
         if (rc) goto done;
     }
+    /* node-down extension: crashes are scheduled at setup, so each precedes
+     * every event of its tick that is inserted later (all model events).  The
+     * energy model assumes a node that is up for the whole run. */
+    if (in->down_tick && in->p_busy_w) {
+        rc = ORC_ERR_UNSUPPORTED;
+        goto done;
+    }
+    if (in->down_tick)
+        for (int32_t k = 0; k < N; k++) {
+            if (in->down_tick[k] == INT64_MAX) continue;
+            if (in->down_tick[k] < in->init_adv_tick[k]) {
+                rc = ORC_ERR_ARG;
+                goto done;
+            }
+            ev_t c;
+            memset(&c, 0, sizeof c);
+            c.tick = in->down_tick[k];
+            c.type = EV_CRASH;
+            c.node = k;
+            rc = schedule(&s, &c);
+            if (rc) goto done;
+        }
     int sorted = 1;
     for (int64_t t = 1; t < T; t++)
         if (in->arrive_tick[t] < in->arrive_tick[t - 1]) {
@@ -586,6 +623,7 @@ typedef struct {
     const double *p_busy, *p_idle;
     const int64_t *user_ul, *user_dl;
     int32_t user_per_task;
+    const int64_t *down;
     int32_t *node;
     uint8_t *status;
     int64_t *start_tick, *done_tick;
@@ -609,7 +647,8 @@ static void *batch_worker(void *arg) {
         orc_rep_in in = {b->N, b->T, b->arrive_tick + to, b->req_mips + to, b->mips + no,
                          b->dl + no, b->ul + no, b->init_adv + no,
                          b->p_busy ? b->p_busy + no : 0, b->p_idle ? b->p_idle + no : 0, b->policy,
-                         b->user_ul ? b->user_ul + uo : 0, b->user_dl ? b->user_dl + uo : 0, b->user_per_task};
+                         b->user_ul ? b->user_ul + uo : 0, b->user_dl ? b->user_dl + uo : 0, b->user_per_task,
+                         b->down ? b->down + no : 0};
         orc_rep_out out = {b->node ? b->node + to : 0, b->status ? b->status + to : 0,
                            b->start_tick ? b->start_tick + to : 0, b->done_tick ? b->done_tick + to : 0,
                            0, b->stats ? b->stats + r : 0,
@@ -649,9 +688,23 @@ int orc_run_batch3(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t
                    int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
                    orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
                    int threads) {
+    return orc_run_batch4(R, T, N, node_stride, policy, arrive_tick, req_mips, mips, dl, ul, init_adv, p_busy_w,
+                          p_idle_w, user_ul, user_dl, user_per_task, 0, node, status, start_tick, done_tick, stats,
+                          node_energy_j, hist, user_stats, threads);
+}
+
+int orc_run_batch4(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
+                   const int64_t *arrive_tick, const int32_t *req_mips,
+                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                   const double *p_busy_w, const double *p_idle_w,
+                   const int64_t *user_ul, const int64_t *user_dl, int32_t user_per_task,
+                   const int64_t *down_tick,
+                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                   orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
+                   int threads) {
     batch_t b = {R, N, node_stride, policy, T, arrive_tick, req_mips, mips, dl, ul, init_adv, p_busy_w, p_idle_w,
-                 user_ul, user_dl, user_per_task, node, status, start_tick, done_tick, stats, node_energy_j, hist,
-                 user_stats, 0};
+                 user_ul, user_dl, user_per_task, down_tick, node, status, start_tick, done_tick, stats,
+                 node_energy_j, hist, user_stats, 0};
     pthread_mutex_init(&b.mu, 0);
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;

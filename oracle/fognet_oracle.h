@@ -62,7 +62,15 @@ typedef struct {
     const int64_t *user_ul_tick;
     const int64_t *user_dl_tick;
     int32_t user_per_task;
+    /* Node-down extension (not in the reference's scenarios; INET lifecycle,
+     * ComputeBrokerApp3::handleNodeCrash, ComputeBrokerApp3.cc:423-427):
+     * [N] tick at which node j crashes, INT64_MAX = never; nullable.  The
+     * crash precedes every model event of its tick; must be >= init_adv_tick. */
+    const int64_t *down_tick;
 } orc_rep_in;
+
+/* Task status of a task that reached a crashed node (no ack, never served). */
+#define ORC_TASK_LOST 9
 
 /* count / min / max / exact 128-bit sum and sum of squares of values in ticks */
 typedef struct {
@@ -95,9 +103,9 @@ typedef struct {
 
 typedef struct {
     int32_t *node;       /* [T] chosen node index, -1 if never decided (nullable) */
-    uint8_t *status;     /* [T] 5 task assigned (idle) / 4 task queued            */
-    int64_t *start_tick; /* [T] service start tick                                */
-    int64_t *done_tick;  /* [T] RELEASERESOURCE tick                              */
+    uint8_t *status;     /* [T] 5 task assigned (idle) / 4 task queued / 9 lost   */
+    int64_t *start_tick; /* [T] service start tick (-1: never started)            */
+    int64_t *done_tick;  /* [T] RELEASERESOURCE tick (-1: never completed)        */
     double *final_view_busy; /* [N] broker view busyTime after the last event (nullable) */
     orc_rep_stats *stats;
     double *node_energy_j;   /* [N] per-node energy (nullable)                         */
@@ -211,6 +219,17 @@ int orc_run_batch3(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t
                    const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
                    const double *p_busy_w, const double *p_idle_w,
                    const int64_t *user_ul, const int64_t *user_dl, int32_t user_per_task,
+                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                   orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
+                   int threads);
+
+/* orc_run_batch3 plus the node-down extension: down_tick [R|1][N] (nullable). */
+int orc_run_batch4(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
+                   const int64_t *arrive_tick, const int32_t *req_mips,
+                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                   const double *p_busy_w, const double *p_idle_w,
+                   const int64_t *user_ul, const int64_t *user_dl, int32_t user_per_task,
+                   const int64_t *down_tick,
                    int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
                    orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
                    int threads);

@@ -52,3 +52,20 @@ def replay_v2_cases():
         e["done"] = [x * ms if x >= 0 else -1 for x in e.pop("done_ms")]
         out.append((c["name"], tr, e))
     return out
+
+
+def replay_down_cases():
+    d = json.load(open(os.path.join(GOLDEN, "kat_replay_down.json")))
+    ms = d["ms"]
+    never = np.iinfo(np.int64).max
+    out = []
+    for c in d["cases"]:
+        tr = dict(arrive=np.array(c["arrive_ms"], np.int64) * ms, req=np.array(c["req"], np.int32),
+                  mips=np.array(c["mips"], np.int32), dl=np.array(c["dl_ms"], np.int64) * ms,
+                  ul=np.array(c["ul_ms"], np.int64) * ms, init=np.array(c["init_ms"], np.int64) * ms,
+                  down=np.array([never if x is None else x * ms for x in c["down_ms"]], np.int64))
+        e = dict(c["expect"])
+        e["start"] = [x * ms if x >= 0 else -1 for x in e.pop("start_ms")]
+        e["done"] = [x * ms if x >= 0 else -1 for x in e.pop("done_ms")]
+        out.append((c["name"], tr, e))
+    return out

@@ -39,6 +39,7 @@ MOMENTS_DTYPE = np.dtype([("count", np.int64), ("min_ticks", np.int64), ("max_ti
 USER_SIGNALS = ("delay", "latency", "latencyH1", "taskTime")
 USER_STATS_DTYPE = np.dtype([(n, MOMENTS_DTYPE) for n in USER_SIGNALS])
 POLICY_REF_V3, POLICY_EXT_LAT = 1, 16
+POLICIES = {"REF_V3": POLICY_REF_V3, "EXT_LAT": POLICY_EXT_LAT}
 
 _lib = None
 
@@ -62,6 +63,9 @@ def lib():
         _lib.orc_run_batch3.argtypes = ([C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [p] * 10 +
                                         [C.c_int32] + [p] * 8 + [C.c_int])
         _lib.orc_run_batch3.restype = C.c_int
+        _lib.orc_run_batch4.argtypes = ([C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [p] * 10 +
+                                        [C.c_int32] + [p] * 9 + [C.c_int])
+        _lib.orc_run_batch4.restype = C.c_int
         _lib.orc_decide_ext_lat.argtypes = [C.c_int32, p, p, p, C.c_int32, C.POINTER(C.c_int32)]
         _lib.orc_decide_ext_lat.restype = C.c_int
         _lib.orc_hist_bin.argtypes = [C.c_int64]
@@ -109,12 +113,13 @@ def decide_ext_lat(adv_busy, mips, dl, req):
 
 
 def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool = True, policy: int = 1,
-              p_busy=None, p_idle=None, hist: bool = False, user_ul=None, user_dl=None):
+              p_busy=None, p_idle=None, hist: bool = False, user_ul=None, user_dl=None, down=None):
     """Replay R replications.  arrive/req: [R,T]; node params [R,N] or [N] (shared).
     ``p_busy``/``p_idle`` (same shape as mips) enable the energy model; ``hist``
     returns per-replication histograms [R, 2, 64]; ``user_ul``/``user_dl``
     ([R] one user per replication, or [R, T] per task) model the publishing
-    users' links and return the user-side signals as ``user`` [R] (USER_STATS_DTYPE)."""
+    users' links and return the user-side signals as ``user`` [R] (USER_STATS_DTYPE).
+    ``down`` (same shape as mips, INT64_MAX = never): node crash ticks."""
     arrive = np.ascontiguousarray(np.atleast_2d(arrive), dtype=np.int64)
     req = np.ascontiguousarray(np.atleast_2d(req), dtype=np.int32)
     R, T = arrive.shape
@@ -140,8 +145,10 @@ def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool =
         per_task = 1 if uu.ndim == 2 else 0
         user = np.zeros(R, USER_STATS_DTYPE)
     stats = (OrcRepStats * R)()
-    lib().orc_run_batch3(R, T, N, stride, policy, _ptr(arrive), _ptr(req), _ptr(mips), _ptr(dl), _ptr(ul),
-                         _ptr(init), _ptr(pb), _ptr(pi), _ptr(uu), _ptr(ud), per_task, _ptr(node), _ptr(status),
+    dn = np.ascontiguousarray(down, dtype=np.int64) if down is not None else None
+    lib().orc_run_batch4(R, T, N, stride, policy, _ptr(arrive), _ptr(req), _ptr(mips), _ptr(dl), _ptr(ul),
+                         _ptr(init), _ptr(pb), _ptr(pi), _ptr(uu), _ptr(ud), per_task, _ptr(dn), _ptr(node),
+                         _ptr(status),
                          _ptr(start), _ptr(done), C.cast(stats, C.c_void_p), _ptr(energy), _ptr(h), _ptr(user),
                          threads)
     st = np.frombuffer(stats, dtype=ORC_STATS_DTYPE, count=R).copy()

@@ -41,13 +41,13 @@ def test_struct_sizes_match_header():
     # sizes fixed by the header's field lists (all naturally aligned)
     assert ctypes.sizeof(abi.RepStats) == 8 * 17 + 4 * 2 + 8 * 2
     assert ctypes.sizeof(abi.JobStats) == 8 * 10 + 8 * 12 + 8 * 2 + 8 * 2
-    assert ctypes.sizeof(abi.BatchIn) == 4 * 6 + 8 * 8
+    assert ctypes.sizeof(abi.BatchIn) == 4 * 6 + 8 * 9
     assert ctypes.sizeof(abi.BatchOut) == 8 * 7
 
 
 def test_status_strings_and_version():
     lib = abi.load()
-    assert lib.fognet_abi_version() == abi.ABI_VERSION == 4
+    assert lib.fognet_abi_version() == abi.ABI_VERSION == 5
     assert lib.fognet_status_string(abi.FOGNET_ERR_CAPACITY) == b"pending-task ring capacity exceeded"
     assert lib.fognet_status_string(99) == b"unknown status"
 

@@ -264,3 +264,50 @@ def test_v2_c1_example_run_has_rounding_forwards():
     assert int(st["n_accepted"]) == int(st["n_relayed"]) == 19990
     fw = o["node"][0][o["status"][0] != 3]
     assert (fw == 0).all()
+
+
+@pytest.mark.parametrize("case", golden_io.replay_down_cases(), ids=lambda c: c[0])
+def test_replay_down_known_answers(case):
+    """Node-down extension (handleNodeCrash, ComputeBrokerApp3.cc:423-427): hand-traced cases."""
+    name, tr, exp = case
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], down=tr["down"])
+    st = o["stats"][0]
+    assert st["status"] == 0
+    np.testing.assert_array_equal(o["node"][0], exp["node"])
+    np.testing.assert_array_equal(o["status"][0], exp["status"])
+    np.testing.assert_array_equal(o["start"][0], exp["start"])
+    np.testing.assert_array_equal(o["done"][0], exp["done"])
+    for k in ("n_queued", "n_started", "busy_s", "events", "max_pending"):
+        assert st[k] == exp[k], k
+    assert st["n_tasks"] == len(exp["node"])
+    assert st["queue_sum_lo"] == exp["queue_sum_ms"] * 10**9 and st["queue_sum_hi"] == 0
+    assert st["resp_sum_lo"] == exp["resp_sum_ms"] * 10**9 and st["resp_sum_hi"] == 0
+
+
+def test_replay_down_never_is_identity():
+    """down = INT64_MAX everywhere reproduces the run without the extension."""
+    rng = np.random.default_rng(5)
+    T, N = 400, 6
+    arrive = np.cumsum(rng.integers(0, 3 * 10**11, T)).astype(np.int64)
+    req = rng.integers(0, 9000, T).astype(np.int32)
+    mips = rng.integers(500, 4000, N).astype(np.int32)
+    dl = rng.integers(0, 10**10, N).astype(np.int64)
+    ul = rng.integers(0, 10**10, N).astype(np.int64)
+    init = ul.copy()
+    a = ol.run_batch(arrive + 10**10, req, mips, dl, ul, init)
+    b = ol.run_batch(arrive + 10**10, req, mips, dl, ul, init, down=np.full(N, np.iinfo(np.int64).max))
+    for k in ("node", "status", "start", "done"):
+        np.testing.assert_array_equal(a[k], b[k])
+    assert a["stats"].tobytes() == b["stats"].tobytes()
+
+
+def test_replay_down_rejects_early_crash_and_energy():
+    tr = golden_io.replay_down_cases()[0][1]
+    bad = tr["down"].copy()
+    bad[0] = tr["init"][0] - 1  # before the node's first advert reaches the broker
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], down=bad)
+    assert o["stats"]["status"][0] == 1  # ORC_ERR_ARG
+    pw = np.full(2, 30.0)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], down=tr["down"],
+                     p_busy=pw, p_idle=pw)
+    assert o["stats"]["status"][0] == 8  # ORC_ERR_UNSUPPORTED

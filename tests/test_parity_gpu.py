@@ -648,3 +648,103 @@ def test_v2_errors(ctx):
     tr2, broker, stop, rt = v2_random(9, 2, 3, 500)
     g = run_v2_gpu(ctx, tr2, broker, np.full(2, 2**53 + 1), rt)
     assert (g["stats"]["status"] == _abi.FOGNET_ERR_ARG).all()
+
+
+# ------------------------------------------------------------------ node-down extension
+
+def with_crashes(tr, seed, frac=0.3, grid=None):
+    """Crash ticks for a fraction of the nodes, between each node's first advert
+    and the last publish (snapped to ``grid`` so crashes collide with events)."""
+    rng = np.random.default_rng(seed)
+    init = np.asarray(tr["init"])
+    last = int(np.asarray(tr["arrive"]).max())
+    down = np.full(init.shape, fa.NEVER, np.int64)
+    pick = rng.random(init.shape) < frac
+    pick[..., 0] = True  # the stale view favours low indices: make the crashes matter
+    t = rng.integers(init, np.maximum(init + 1, last), dtype=np.int64)
+    if grid:
+        t = np.maximum(init, (t // grid) * grid)
+    down[pick] = t[pick]
+    return dict(tr, down=down)
+
+
+def oracle_down(tr, **kw):
+    return ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], down=tr["down"],
+                        hist=True, **kw)
+
+
+@pytest.mark.parametrize("case", golden_io.replay_down_cases(), ids=lambda c: c[0])
+def test_down_known_answers_gpu(ctx, case):
+    name, tr, exp = case
+    tr = dict(tr, arrive=tr["arrive"][None], req=tr["req"][None])
+    g = run_gpu_full(ctx, tr)
+    np.testing.assert_array_equal(g["node"][0], exp["node"])
+    np.testing.assert_array_equal(g["status"][0], exp["status"])
+    np.testing.assert_array_equal(g["start"][0], exp["start"])
+    np.testing.assert_array_equal(g["done"][0], exp["done"])
+    o = oracle_down(tr)
+    assert g["stats"].tobytes() == o["stats"].tobytes()
+    np.testing.assert_array_equal(g["hist"], o["hist"].sum(axis=0))
+
+
+@pytest.mark.parametrize("N,T,R,policy", [(5, 2000, 6, "REF_V3"), (64, 2000, 4, "REF_V3"), (300, 2000, 3, "REF_V3"),
+                                          (1000, 1500, 2, "REF_V3"), (40, 1500, 4, "EXT_LAT"),
+                                          (300, 1500, 3, "EXT_LAT")])
+def test_down_matches_oracle(ctx, N, T, R, policy):
+    tr = with_crashes(tg.make_batch(0xD0 + N, R, N, T, rho=0.9, lat_scale=10), seed=N)
+    g = run_gpu_full(ctx, tr, policy=policy)
+    o = oracle_down(tr, threads=R, policy=ol.POLICIES[policy])
+    assert (o["stats"]["status"] == 0).all()
+    assert ((o["status"] == 9) | (o["done"] == -1)).any()  # the crashes bite
+    assert_parity(tr, g, o)
+    assert g["stats"].tobytes() == o["stats"].tobytes()
+    np.testing.assert_array_equal(g["hist"], o["hist"].sum(axis=0))
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_down_tie_heavy(ctx, seed):
+    """Crash ticks on the same coarse grid as arrivals, completions and adverts."""
+    tr = with_crashes(tie_heavy(300 + seed, 6, 1 + 23 * seed, 1500), seed=seed, frac=0.5, grid=10**11)
+    g = run_gpu_full(ctx, tr)
+    o = oracle_down(tr, threads=6)
+    assert_parity(tr, g, o)
+    assert g["stats"].tobytes() == o["stats"].tobytes()
+
+
+def test_down_never_equals_plain_run(ctx):
+    tr = tg.make_batch(0xD1, 3, 50, 1500, rho=0.9)
+    plain = run_gpu_full(ctx, tr)
+    g = run_gpu_full(ctx, dict(tr, down=np.full(np.shape(tr["mips"]), fa.NEVER, np.int64)))
+    for k in ("node", "status", "start", "done", "hist"):
+        np.testing.assert_array_equal(g[k], plain[k])
+    assert g["stats"].tobytes() == plain["stats"].tobytes()
+
+
+def test_down_user_stats(ctx):
+    """Lost tasks send no node ack, never-completed tasks no status-6 ack."""
+    tr = with_crashes(tg.make_batch(0xD2, 4, 30, 2000, rho=0.9), seed=2, frac=0.4)
+    R = 4
+    rng = np.random.default_rng(3)
+    uu = rng.integers(0, 5 * 10**9, R).astype(np.int64)
+    ud = rng.integers(0, 5 * 10**9, R).astype(np.int64)
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(tr, dev)
+    out = fa.run_batch(ctx, d)
+    g = fa.user_stats(ctx, d, out, uu, ud)
+    o = oracle_down(tr, threads=4, user_ul=uu, user_dl=ud)
+    assert (o["stats"]["status"] == 0).all()
+    assert_user_parity(g, o["user"])
+
+
+def test_down_errors(ctx):
+    tr = golden_io.replay_down_cases()[0][1]
+    tr = dict(tr, arrive=tr["arrive"][None], req=tr["req"][None])
+    bad = tr["down"].copy()
+    bad[0] = tr["init"][0] - 1
+    g = run_gpu(ctx, dict(tr, down=bad))
+    assert g["stats"]["status"][0] == _abi.FOGNET_ERR_ARG
+    pb, pi = fa.power_model(tr["mips"])
+    dev = torch.device("cuda", ctx.device)
+    with pytest.raises(fa.FognetError) as ei:
+        fa.run_batch(ctx, fa.as_device_trace(dict(tr, p_busy=pb, p_idle=pi), dev))
+    assert ei.value.code == _abi.FOGNET_ERR_UNSUPPORTED
