@@ -41,7 +41,7 @@ struct Slot {
   int64_t nxt;       // tick at which the head's completion advert reaches the broker
   // (head completion tick = nxt - ul: the advert leaves the node at completion)
   uint32_t hd_C;     // cumulative service up to and including the head
-  uint32_t hd_S;     // head service seconds (bits 0-23) | nh prefetch stamp (bits 24-31)
+  uint32_t hd_S;     // head service seconds (< 2^24)
   // (entry head+1 {a lo, a hi, C, S} lives in reserved VGPRs, see nh_prefetch)
   int64_t tl_a;      // tail (newest) task: arrival tick at the node
   // (tail completion tick, cumulative service and service time live in LDS:
@@ -74,7 +74,7 @@ constexpr uint32_t kNoKey = ~0u;
 __device__ __forceinline__ uint32_t n_push(const Slot& st) { return st.cnt & 0xFFFFu; }
 __device__ __forceinline__ uint32_t n_head(const Slot& st) { return st.cnt >> 16; }
 __device__ __forceinline__ uint32_t pending(const Slot& st) { return (n_push(st) - n_head(st)) & 0xFFFFu; }
-__device__ __forceinline__ uint32_t head_S(const Slot& st) { return st.hd_S & 0xFFFFFFu; }
+__device__ __forceinline__ uint32_t head_S(const Slot& st) { return st.hd_S; }
 __device__ __forceinline__ int64_t nh_a(u32x4 v) { return (int64_t)(((uint64_t)v.y << 32) | v.x); }
 
 // ---- head+1 prefetch, outside the compiler's register allocation
@@ -191,16 +191,19 @@ __device__ __forceinline__ void nh_prefetch(const RingEntry* p) {
   else nh_prefetch_3(p);
 }
 
-__device__ __forceinline__ void stamp_prefetch(Slot& st, uint32_t ops) {
-  st.hd_S = (st.hd_S & 0xFFFFFFu) | (ops << 24);
+// Prefetch stamps are kept per slot, not per node: byte s of the wave-uniform
+// `pf` is the tally of the youngest head+1 load issued into slot s's
+// registers (by any lane).  A read of slot s waits for that one, which covers
+// every older load into the slot: conservative, but needs no per-lane ages
+// and no wave reduction.
+__device__ __forceinline__ uint32_t set_stamp(uint32_t pf, int s, uint32_t ops) {
+  return (pf & ~(0xFFu << (8 * s))) | ((ops & 0xFFu) << (8 * s));
 }
 
-// Wave-level read of slot S's head+1 entry for the lanes in `need`: waits
-// until the youngest of their prefetches has landed.
+// Wave-level read of slot S's head+1 entry (`need`: some lane uses it).
 template <int S>
-__device__ __forceinline__ u32x4 read_nh(const Slot& st, bool need, uint32_t ops) {
-  const uint32_t age = need ? ((ops - (st.hd_S >> 24)) & 0xFFu) : 0xFFu;
-  const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane(wave_min_u32(age));
+__device__ __forceinline__ u32x4 read_nh(bool need, uint32_t pf, uint32_t ops) {
+  const uint32_t m = ballot(need) ? ((ops - (pf >> (8 * S))) & 0xFFu) : 0xFFu;
   if constexpr (S == 0) return nh_read_0(m);
   else if constexpr (S == 1) return nh_read_1(m);
   else if constexpr (S == 2) return nh_read_2(m);
@@ -349,11 +352,10 @@ __device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, i
   const int64_t start = na > hd_done ? na : hd_done;
   const int64_t done = start + (int64_t)nhw.w * kTicksPerSecond;
   st.hd_C = nhw.z;
-  st.hd_S = (st.hd_S & 0xFF000000u) | nhw.w;
+  st.hd_S = nhw.w;
   st.nxt = done + ul;
   if (pend >= 2u) {  // the ring holds every pending entry, the tail included
-    nh_prefetch<SL>(ring + ((n_head(st) + 1u) & qmask));
-    stamp_prefetch(st, ops);
+    nh_prefetch<SL>(ring + ((n_head(st) + 1u) & qmask));  // the caller stamps slot SL
   }
 }
 
@@ -455,11 +457,15 @@ __device__ __forceinline__ uint32_t scan_add_level(uint32_t v) {
   return v + dpp_or_u32<kCtrl, kRowMask>(0u, v);
 }
 
-// One level of the run's inclusive i64 prefix maximum (invalid sources read INT64_MIN).
+// One level of the run's inclusive i64 prefix maximum.  `tmp` carries the
+// DPP destination from level to level: a lane whose source is invalid (or
+// whose row is masked off) keeps the value it read at an earlier level, an
+// element of an earlier lane that its running maximum already covers (or the
+// initial INT64_MIN), so no identity has to be rewritten per level.
 template <int kCtrl, int kRowMask>
-__device__ __forceinline__ int64_t scan_max_level(int64_t v) {
-  const int64_t l = dpp_or_i64<kCtrl, kRowMask>(INT64_MIN, v);
-  return l > v ? l : v;
+__device__ __forceinline__ int64_t scan_max_level(int64_t v, int64_t& tmp) {
+  tmp = dpp_or_i64<kCtrl, kRowMask>(tmp, v);
+  return tmp > v ? tmp : v;
 }
 
 // ---------------------------------------------------------------- statistics
@@ -469,10 +475,12 @@ __device__ __forceinline__ int64_t scan_max_level(int64_t v) {
 // (plus the per-node service seconds s_busy and the histogram s_hist in LDS
 // when those statistics are on).  The loads of UNROLL tasks are issued
 // before any is used.  dl_of(k): node k's downlink latency.
-template <int UNROLL, class DlOf>
+// kPerTask = false: busy seconds, per-node service and `last` are not
+// accumulated per task (the fused epilogue takes them from the node tails).
+template <int UNROLL, bool kPerTask = true, class DlOf>
 __device__ __forceinline__ void stats_accumulate(const ReplayArgs& A, size_t tbase, int n, int i0, int stride, Acc& a,
                                                  unsigned long long* s_busy, uint32_t* s_hist, DlOf dl_of) {
-  const bool energy = A.p_busy != nullptr;
+  const bool energy = kPerTask && A.p_busy != nullptr;
   const bool hist = A.hist != nullptr;
   for (int ib = i0; ib < n; ib += stride * UNROLL) {
     int64_t t[UNROLL], st0[UNROLL], dn[UNROLL];
@@ -493,13 +501,15 @@ __device__ __forceinline__ void stats_accumulate(const ReplayArgs& A, size_t tba
       if (ib + u * stride < n) {
         const int32_t k = kk[u];
         const int64_t resp = dn[u] - t[u];
-        const uint64_t svc = (uint64_t)(dn[u] - st0[u]) / (uint64_t)kTicksPerSecond;  // whole seconds
-        a.busy += svc;
-        if (energy) atomicAdd(&s_busy[k], (unsigned long long)svc);
+        if constexpr (kPerTask) {
+          const uint64_t svc = (uint64_t)(dn[u] - st0[u]) / (uint64_t)kTicksPerSecond;  // whole seconds
+          a.busy += svc;
+          if (energy) atomicAdd(&s_busy[k], (unsigned long long)svc);
+          a.last = max(a.last, dn[u]);
+        }
         add_moment(a.rs_lo, a.rs_hi, a.rq_lo, a.rq_hi, (uint64_t)resp);
         a.rmin = min(a.rmin, resp);
         a.rmax = max(a.rmax, resp);
-        a.last = max(a.last, dn[u]);
         if (hist) atomicAdd(&s_hist[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
         if (stt[u] == 4u) {
           const int64_t q = st0[u] - (t[u] + dl_of(k));
@@ -626,6 +636,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
   int64_t prev_t = INT64_MIN;
   uint32_t max_pend = 0u;
   uint32_t ops = T > 0 ? kChunkOps : 0u;  // tally of issued vector-memory instructions (see kPrefetchOps)
+  uint32_t pf = 0u;                       // per-slot stamps of the youngest head+1 loads (set_stamp)
   ch_stamp = ops;
   int64_t n_done = 0;
   uint32_t scan = 0u;  // profile builds: ring entries read by c_arrived (per lane)
@@ -637,7 +648,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
 #if FOGNET_REPLAY_PROFILE == 1
   uint64_t p_iter = 0, p_advit = 0, p_adv = 0, p_end_k = 0, p_end_j = 0, p_end_c = 0, p_hz = 0, p_refill = 0, p_w0 = 0, p_rd = 0,
            p_chunks = 0, p_pk0 = 0, p_resume = 0;
-  auto young = [&](const Slot& x, bool need) { return ballot(need && ((ops - (x.hd_S >> 24)) & 0xFFu) < 2u) != 0; };
+  auto young = [&](int s, bool need) { return ballot(need) && ((ops - (pf >> (8 * s))) & 0xFFu) < 2u; };
 #endif
   // A run that consumed the rest of its chunk continues into the next one
   // while the publishes stay within its horizon E_carry (argmin unchanged).
@@ -689,13 +700,16 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
             if (!ballot(due)) return;
             any = true;
             dirty = true;
-            PROF(p_advit++; p_adv += __popcll(ballot(due)); p_rd++; p_w0 += young(st[s], due && pending(st[s]) >= 2u);)
+            PROF(p_advit++; p_adv += __popcll(ballot(due)); p_rd++; p_w0 += young(s, due && pending(st[s]) >= 2u);)
             TMARK(1)
-            const u32x4 nhw = read_nh<s>(st[s], due && pending(st[s]) >= 2u, ops);
+            const u32x4 nhw = read_nh<s>(due && pending(st[s]) >= 2u, pf, ops);
             TMARK(8)
             // apply_advert prefetches head+2 where >= 3 are pending: tally it
             // first, so the stamp already counts the load itself
-            if (ballot(due && pending(st[s]) >= 3u)) ops += 1u;
+            if (ballot(due && pending(st[s]) >= 3u)) {
+              ops += 1u;
+              pf = set_stamp(pf, s, ops);
+            }
             if (due) {
               const int k = s * kWave + lane;
               apply_advert<s>(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops, scan);
@@ -736,9 +750,9 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
             }
           }
           if (ballot(deep)) {
-            PROF(p_hz++; p_rd++; p_w0 += young(st[s], deep && pending(st[s]) >= 2u);)
+            PROF(p_hz++; p_rd++; p_w0 += young(s, deep && pending(st[s]) >= 2u);)
             TMARK(3)
-            const u32x4 nhw = read_nh<s>(st[s], deep && pending(st[s]) >= 2u, ops);
+            const u32x4 nhw = read_nh<s>(deep && pending(st[s]) >= 2u, pf, ops);
             TMARK(9)
             if (deep) {
               const int64_t h = horizon(st[s], nhw, j, best, s_tlC[j], s_dl[j], s_ul[j], ring_s(s), qmask, scan);
@@ -814,12 +828,13 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
       Cs = scan_add_level<0x142, 0xA>(Cs);  // row_bcast:15
       Cs = scan_add_level<0x143, 0xC>(Cs);  // row_bcast:31
       int64_t X = in_run ? (int64_t)((uint64_t)a - (uint64_t)ticks_of(Cs - S)) : INT64_MIN;
-      X = scan_max_level<0x111, 0xF>(X);
-      X = scan_max_level<0x112, 0xF>(X);
-      X = scan_max_level<0x114, 0xF>(X);
-      X = scan_max_level<0x118, 0xF>(X);
-      X = scan_max_level<0x142, 0xA>(X);
-      X = scan_max_level<0x143, 0xC>(X);
+      int64_t xt = INT64_MIN;
+      X = scan_max_level<0x111, 0xF>(X, xt);
+      X = scan_max_level<0x112, 0xF>(X, xt);
+      X = scan_max_level<0x114, 0xF>(X, xt);
+      X = scan_max_level<0x118, 0xF>(X, xt);
+      X = scan_max_level<0x142, 0xA>(X, xt);
+      X = scan_max_level<0x143, 0xC>(X, xt);
       const int64_t base_done = tld_k;  // INT64_MIN when k never ran a task
       const int64_t dmax = base_done > X ? base_done : X;
       const int64_t done = (int64_t)((uint64_t)dmax + (uint64_t)ticks_of(Cs));
@@ -879,7 +894,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
           if (lane == kl) {
             if (pend_k == 0u) {
               st[s].hd_C = C_f;
-              st[s].hd_S = (st[s].hd_S & 0xFF000000u) | S_f;
+              st[s].hd_S = S_f;
               st[s].nxt = done_f + ul_k;
             }
             st[s].tl_a = a_z;
@@ -893,7 +908,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
             refill_nh(s, st[s], ring_s(s), qmask, kl);
             PROF(p_refill++;)
             ops += 1u;
-            if (lane == kl) stamp_prefetch(st[s], ops);  // stamp counts the refill itself
+            pf = set_stamp(pf, s, ops);  // the stamp counts the refill itself
           }
         }
       }
@@ -965,13 +980,31 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     double* e_e = reinterpret_cast<double*>(s_ul);                              // [NPL*64] f64
     uint32_t* e_hist = s_ch;                                                    // 192 >= 2*64 u32
     static_assert(3 * kWave >= FOGNET_HIST_METRICS * FOGNET_HIST_BINS, "histogram fits the chunk stage");
-    if (A.p_busy)
+    // A completed replay leaves every node's total service (its tail's
+    // cumulative service, exact while n_done * max_s < 2^32) and its last
+    // completion (the tail's, FIFO) in the tail state: busy seconds, per-node
+    // service for the energy model and `last` then need no per-task work.
+    const bool from_tails = err == FOGNET_OK && (uint64_t)n_done * (uint64_t)A.max_s < (1ull << 32);
+    Acc acc = acc_identity();
+    if (from_tails) {
+      for (int j = lane; j < NPL * kWave; j += kWave) {
+        const uint32_t B = s_tlC[j];  // 0 for unused nodes and lanes past N
+        const int64_t ld = s_tld[j];  // INT64_MIN for unused nodes
+        acc.busy += B;
+        acc.last = max(acc.last, ld);
+        if (A.p_busy) e_busy[j] = B;  // aliases s_tld[j]: read above by this lane
+      }
+    } else if (A.p_busy) {
       for (int j = lane; j < NPL * kWave; j += kWave) e_busy[j] = 0ull;
+    }
     if (A.hist)
       for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) e_hist[h] = 0u;
     __syncthreads();
-    Acc acc = acc_identity();
-    stats_accumulate<4>(A, tbase, (int)n_done, lane, kWave, acc, e_busy, e_hist, [&](int k) { return s_dl[k]; });
+    if (from_tails)
+      stats_accumulate<4, false>(A, tbase, (int)n_done, lane, kWave, acc, e_busy, e_hist,
+                                 [&](int k) { return s_dl[k]; });
+    else
+      stats_accumulate<4>(A, tbase, (int)n_done, lane, kWave, acc, e_busy, e_hist, [&](int k) { return s_dl[k]; });
     acc = wave_merge(acc);
     __syncthreads();
     fognet_rep_stats* S = A.out_stats + r;

@@ -1,0 +1,21 @@
+"""Replay-only vs replay+fused-statistics kernel time at C3 (GPU; diagnostics only)."""
+import sys, os, time
+import numpy as np, torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import fognetsimpp_amd as fa
+
+R = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+T, N = 100_000, 256
+dev = torch.device("cuda", 0)
+ctx = fa.Context(0)
+mg, sc = fa.sweep_params(np.arange(R), N)
+tr = fa.generate_trace(ctx, 0x5EED0003, R, T, N, mg, sc)
+out = fa.allocate_outputs(R, T, dev, N=N, energy=False, hist=True)
+torch.cuda.synchronize()
+for stage in ("all", "replay", "stats", "all", "replay"):
+    ts = []
+    for i in range(4):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(); fa.run_batch(ctx, tr, out, ring_capacity=2048, stage=stage); b.record()
+        torch.cuda.synchronize(); ts.append(a.elapsed_time(b))
+    print(stage, ["%.2f" % t for t in ts], flush=True)
