@@ -200,10 +200,16 @@ __device__ __forceinline__ uint32_t set_stamp(uint32_t pf, int s, uint32_t ops) 
   return (pf & ~(0xFFu << (8 * s))) | ((ops & 0xFFu) << (8 * s));
 }
 
-// Wave-level read of slot S's head+1 entry (`need`: some lane uses it).
+// Lanes (of the active ones) with x >= c, as a mask straight from the compare
+// (a ballot of a compound bool makes hipcc round-trip it through a VGPR).
+__device__ __forceinline__ uint64_t lanes_ge(uint32_t x, uint32_t c) {
+  return __builtin_amdgcn_uicmp(x, c, 35 /* ICMP_UGE */);
+}
+
+// Wave-level read of slot S's head+1 entry (`need`: wave-uniform, some lane uses it).
 template <int S>
 __device__ __forceinline__ u32x4 read_nh(bool need, uint32_t pf, uint32_t ops) {
-  const uint32_t m = ballot(need) ? ((ops - (pf >> (8 * S))) & 0xFFu) : 0xFFu;
+  const uint32_t m = need ? ((ops - (pf >> (8 * S))) & 0xFFu) : 0xFFu;
   if constexpr (S == 0) return nh_read_0(m);
   else if constexpr (S == 1) return nh_read_1(m);
   else if constexpr (S == 2) return nh_read_2(m);
@@ -697,16 +703,18 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
           static_for<0, NPL>([&](auto sc) {
             constexpr int s = decltype(sc)::value;
             const bool due = st[s].nxt < t_p;
-            if (!ballot(due)) return;
+            const uint64_t dm = ballot(due);
+            if (!dm) return;
+            const uint32_t pd = pending(st[s]);
             any = true;
             dirty = true;
             PROF(p_advit++; p_adv += __popcll(ballot(due)); p_rd++; p_w0 += young(s, due && pending(st[s]) >= 2u);)
             TMARK(1)
-            const u32x4 nhw = read_nh<s>(due && pending(st[s]) >= 2u, pf, ops);
+            const u32x4 nhw = read_nh<s>((dm & lanes_ge(pd, 2u)) != 0, pf, ops);
             TMARK(8)
             // apply_advert prefetches head+2 where >= 3 are pending: tally it
             // first, so the stamp already counts the load itself
-            if (ballot(due && pending(st[s]) >= 3u)) {
+            if (dm & lanes_ge(pd, 3u)) {
               ops += 1u;
               pf = set_stamp(pf, s, ops);
             }
@@ -736,7 +744,8 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
         static_for<0, NPL>([&](auto sc) {
           constexpr int s = decltype(sc)::value;
           const int j = s * kWave + lane;
-          const bool rel = j < N && j != k && (uint32_t)j < best && pending(st[s]) >= 1u;
+          const uint32_t pd = pending(st[s]);
+          const bool rel = j < N && j != k && (uint32_t)j < best && pd >= 1u;
           bool deep = false;
           if (rel) {
             const uint32_t tlC_j = s_tlC[j];
@@ -749,10 +758,11 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
               e_lane = st[s].nxt < e_lane ? st[s].nxt : e_lane;  // beyond this chunk: its first advert
             }
           }
-          if (ballot(deep)) {
+          const uint64_t dm = ballot(deep);
+          if (dm) {
             PROF(p_hz++; p_rd++; p_w0 += young(s, deep && pending(st[s]) >= 2u);)
             TMARK(3)
-            const u32x4 nhw = read_nh<s>(deep && pending(st[s]) >= 2u, pf, ops);
+            const u32x4 nhw = read_nh<s>((dm & lanes_ge(pd, 2u)) != 0, pf, ops);
             TMARK(9)
             if (deep) {
               const int64_t h = horizon(st[s], nhw, j, best, s_tlC[j], s_dl[j], s_ul[j], ring_s(s), qmask, scan);

@@ -2,6 +2,9 @@
 import sys, os, time
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fognetsimpp_amd import _abi
+if os.environ.get("FOGNET_LIB"):  # time a variant build (tools/build_variant.sh)
+    _abi.LIB_PATH = os.environ["FOGNET_LIB"]
 import fognetsimpp_amd as fa
 
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
@@ -12,10 +15,10 @@ mg, sc = fa.sweep_params(np.arange(R), N)
 tr = fa.generate_trace(ctx, 0x5EED0003, R, T, N, mg, sc)
 out = fa.allocate_outputs(R, T, dev, N=N, energy=False, hist=True)
 torch.cuda.synchronize()
-for stage in ("all", "replay", "stats", "all", "replay"):
+for stage in os.environ.get("FOGNET_STAGES", "all,replay,stats,all,replay").split(","):
     ts = []
     for i in range(4):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(); fa.run_batch(ctx, tr, out, ring_capacity=2048, stage=stage); b.record()
         torch.cuda.synchronize(); ts.append(a.elapsed_time(b))
-    print(stage, ["%.2f" % t for t in ts], flush=True)
+    print(os.path.basename(os.path.dirname(_abi.LIB_PATH)), stage, ["%.2f" % t for t in ts], "min %.2f" % min(ts), flush=True)
