@@ -10,7 +10,14 @@ OBJS := $(patsubst $(SRC_DIR)/%.hip,$(OBJDIR)/%.o,$(SRCS)) $(OBJDIR)/io.o
 HOSTCXX ?= g++
 LIB := fognetsimpp_amd/libfognet_hip.so
 
-all: $(LIB) oracle
+DRIVER := fognetsimpp_amd/fognet_replay
+
+all: $(LIB) $(DRIVER) oracle
+
+# command-line trace-replay driver (host C++ over the C ABI; reads omnetpp.ini keys)
+$(DRIVER): $(SRC_DIR)/fognet_replay.cpp include/fognet_hip.h include/fognet_io.h $(LIB)
+	$(HOSTCXX) -O2 -std=c++17 -Wall -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ $< -o $@ \
+	  -Lfognetsimpp_amd -lfognet_hip -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib
 
 $(OBJDIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -31,7 +38,7 @@ asm: $(SRC_DIR)/replay.hip $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o build/asm/replay.o -save-temps=obj -Rpass-analysis=kernel-resource-usage
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(DRIVER)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean asm
