@@ -573,6 +573,8 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
   __shared__ int64_t s_dl[NPL * kWave];
   __shared__ int64_t s_ul[NPL * kWave];
   __shared__ int32_t s_mips[NPL * kWave];
+  __shared__ uint32_t s_dvm[NPL * kWave];  // division by the node's MIPS (udiv_magic): multiplier
+  __shared__ uint8_t s_dvs[NPL * kWave];   //   and shifts sh1 | sh2 << 1 (sh1 <= 1, sh2 <= 31)
   __shared__ int64_t s_tld[NPL * kWave];   // tail completion tick (INT64_MIN: node never used)
   __shared__ uint32_t s_tlC[NPL * kWave];  // tail cumulative service (mod 2^32)
   __shared__ uint32_t s_tlS[NPL * kWave];  // tail service seconds
@@ -606,6 +608,9 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     s_dl[k] = d;
     s_ul[k] = u;
     s_mips[k] = m;
+    const UDiv dv = udiv_magic((uint32_t)(m > 0 ? m : 1));
+    s_dvm[k] = dv.m;
+    s_dvs[k] = (uint8_t)((dv.sh & 1u) | ((dv.sh >> 8) << 1));
     // every node's first advert {MIPS, busyTime = 0.0} has reached the broker
     st[s].vkey = k < N ? (uint32_t)k : kNoKey;
     st[s].nxt = kNever;
@@ -782,7 +787,8 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
 
       // node k: parameters and tail state (uniform)
       const int64_t dl_k = s_dl[k], ul_k = s_ul[k];
-      const int32_t mips_k = s_mips[k];
+      const uint32_t dvs_k = s_dvs[k];
+      const UDiv div_k{s_dvm[k], (dvs_k & 1u) | ((dvs_k >> 1) << 8)};
       const uint32_t tlC_k = s_tlC[k], tlS_k = s_tlS[k];
       const int64_t tld_k = s_tld[k];
       uint32_t cnt_k = 0u;
@@ -801,7 +807,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
         E = nxt_k < E ? nxt_k : E;  // k's own next advert changes its key
       } else {
         // the run's first task becomes k's head: its advert ends the run
-        const uint32_t s_p = (uint32_t)readlane_u32((uint32_t)cr, jp) / (uint32_t)mips_k;
+        const uint32_t s_p = udiv(readlane_u32((uint32_t)cr, jp), div_k);
         const int64_t a_p = t_p + dl_k;
         const int64_t done_p = (a_p > tld_k ? a_p : tld_k) + (int64_t)(s_p & 0xFFFFu) * kTicksPerSecond;
         const int64_t x_p = done_p + ul_k;
@@ -821,7 +827,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
       int64_t a = 0, dd = 0;
       bool lerr = false;
       if (in_run) {
-        S = (uint32_t)cr / (uint32_t)mips_k;  // double tskTime = requiredMIPS / MIPS (:276)
+        S = udiv((uint32_t)cr, div_k);  // double tskTime = requiredMIPS / MIPS (:276)
         a = ca + dl_k;
         dd = (int64_t)S * kTicksPerSecond;
         lerr = S > A.max_s || a > kMaxTick;

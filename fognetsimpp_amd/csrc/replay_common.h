@@ -55,6 +55,25 @@ struct Acc {
   int64_t qmin, qmax, rmin, rmax, last;
 };
 
+// Unsigned 32-bit division by a per-node constant (the node's MIPS) as a
+// multiply-high and two shifts (Granlund & Montgomery 1994, Fig. 4.1):
+// n / d = (t + ((n - t) >> sh1)) >> sh2 with t = umulhi(m, n), exact for
+// every n < 2^32 and d >= 1.  sh = sh1 | sh2 << 8.
+struct UDiv {
+  uint32_t m, sh;
+};
+
+__device__ __forceinline__ UDiv udiv_magic(uint32_t d) {
+  const uint32_t l = d <= 1u ? 0u : 32u - (uint32_t)__clz((int)(d - 1u));  // ceil(log2 d)
+  const uint32_t m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1u);
+  return UDiv{m, (l < 1u ? l : 1u) | ((l > 1u ? l - 1u : 0u) << 8)};
+}
+
+__device__ __forceinline__ uint32_t udiv(uint32_t n, UDiv q) {
+  const uint32_t t = __umulhi(q.m, n);
+  return (t + ((n - t) >> (q.sh & 0xFFu))) >> (q.sh >> 8);
+}
+
 __device__ __forceinline__ Acc acc_identity() {
   Acc a = {};
   a.qmin = a.rmin = INT64_MAX;

@@ -311,3 +311,23 @@ def test_replay_down_rejects_early_crash_and_energy():
     o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], down=tr["down"],
                      p_busy=pw, p_idle=pw)
     assert o["stats"]["status"][0] == 8  # ORC_ERR_UNSUPPORTED
+
+
+def test_udiv_magic_exact():
+    """replay_common.h udiv_magic/udiv (Granlund-Montgomery): the replay
+    kernel's S = MIPSRequired / MIPS (ComputeBrokerApp3.cc:276) as a
+    multiply-high and shifts, restated in numpy and checked against integer
+    division for every divisor up to 2^16, large divisors and extreme numerators."""
+    d = np.concatenate([np.arange(1, 1 << 16, dtype=np.uint64),
+                        np.array([(1 << 31) - 1, 1 << 31, (1 << 32) - 1, 3 << 30, 123456789], np.uint64)])
+    l = np.array([0 if x <= 1 else int(x - 1).bit_length() for x in d], np.uint64)
+    m = ((np.uint64(1) << np.uint64(32)) * ((np.uint64(1) << l) - d)) // d + np.uint64(1)
+    m &= np.uint64(0xFFFFFFFF)
+    sh1 = np.minimum(l, 1)
+    sh2 = np.where(l > 1, l - 1, 0).astype(np.uint64)
+    rng = np.random.default_rng(5)
+    for n in [np.uint64(0), np.uint64(1), np.uint64(0xFFFFFFFF), np.uint64(0x7FFFFFFF), np.uint64(64000), None]:
+        nn = rng.integers(0, 1 << 32, d.size, dtype=np.uint64) if n is None else np.full(d.size, n, np.uint64)
+        t = (m * nn) >> np.uint64(32)
+        q = (t + ((nn - t) >> sh1)) >> sh2
+        np.testing.assert_array_equal(q, nn // d)
