@@ -82,7 +82,9 @@ def main():
     ap.add_argument("--workload", default="c3", choices=("c1", "c3", "c4", "c5"))
     ap.add_argument("--R-total", type=int, default=None,
                     help="c4/c5: replications over all ranks (default 1,000,000 / 1024)")
-    ap.add_argument("--block", type=int, default=4096, help="c4: replications per device block")
+    ap.add_argument("--block", type=int, default=16384,
+                    help="c4: replications per device block (replay launches queue 4x the resident waves, so "
+                         "waves that finish early are refilled)")
     args = ap.parse_args()
     if args.workload in ("c4", "c5"):
         if args.T == 100_000:
@@ -264,28 +266,47 @@ def bench_c4(args, ctx, dev, dist, world, rank):
     mg_all, sc_all = fa.sweep_params(np.arange(r0, r0 + n), N)
     mg_d = torch.from_numpy(np.ascontiguousarray(mg_all)).to(dev)
     sc_d = torch.from_numpy(np.ascontiguousarray(sc_all)).to(dev)
-    bufs = fa.allocate_trace(B, T, N, dev)
+    # two trace buffers: block i + 1 is generated on a side stream while block
+    # i replays (generation is HBM-bound, the replay issue/latency-bound)
+    bufs = [fa.allocate_trace(B, T, N, dev) for _ in range(2)]
     pb, pi = fa.power_model(1000 * (1 + np.arange(N) % 4))  # the generator's MIPS pattern
-    bufs["p_busy"] = torch.from_numpy(np.tile(pb, (B, 1))).to(dev)  # same [R][N] layout as mips
-    bufs["p_idle"] = torch.from_numpy(np.tile(pi, (B, 1))).to(dev)
+    for bf in bufs:
+        bf["p_busy"] = torch.from_numpy(np.tile(pb, (B, 1))).to(dev)  # same [R][N] layout as mips
+        bf["p_idle"] = torch.from_numpy(np.tile(pi, (B, 1))).to(dev)
     out = fa.allocate_outputs(B, T, dev, N=N, energy=False, hist=True)
     jrec = torch.zeros((max(1, len(blocks)), _abi.JOB_STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
     stream = fa.engine._stream_ptr(dev)
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    generated = [torch.cuda.Event() for _ in range(2)]
+    consumed = [torch.cuda.Event() for _ in range(2)]
     log(f"[rank {rank}] c4: {n} replications in {len(blocks)} blocks of <= {B}, T={T} N={N}")
+
+    def generate(i):
+        b0, nb = blocks[i]
+        bf = bufs[i % 2]
+        with torch.cuda.stream(side):
+            side.wait_event(consumed[i % 2])  # block i - 2's replay has read this buffer
+            fa.generate_trace(ctx, args.seed, nb, T, N, mg_d[b0 - r0: b0 - r0 + nb], sc_d[b0 - r0: b0 - r0 + nb],
+                              r0=b0, out=bf)
+            generated[i % 2].record(side)
 
     def step(evs=None):
         out.hist.zero_()
+        generate(0)
         for i, (b0, nb) in enumerate(blocks):
-            tr = {k: v[:nb] for k, v in bufs.items()}
+            if i + 1 < len(blocks):
+                generate(i + 1)
+            tr = {k: v[:nb] for k, v in bufs[i % 2].items() if not k.startswith("_")}
             o = fa.BatchResult(out.node[:nb], out.status[:nb], out.start_tick[:nb], out.done_tick[:nb],
                                out.stats[: nb * _abi.REP_STATS_DTYPE.itemsize], None, out.hist)
-            fa.generate_trace(ctx, args.seed, nb, T, N, mg_d[b0 - r0: b0 - r0 + nb], sc_d[b0 - r0: b0 - r0 + nb],
-                              r0=b0, out=tr)
+            main.wait_event(generated[i % 2])
             if evs is not None:
                 evs[i][0].record()
             fa.run_batch(ctx, tr, o, ring_capacity=args.ring, stage="all", policy=args.policy)
             if evs is not None:
                 evs[i][1].record()
+            consumed[i % 2].record(main)
             ctx.check(ctx._lib.fognet_reduce_stats_dev(ctx.handle, fa.engine._ptr(o.stats), nb,
                                                        fa.engine._ptr(jrec[i]), stream), "reduce")
         job = fa.merge_job_stats(list(jrec.cpu().numpy().view(_abi.JOB_STATS_DTYPE).reshape(-1)[:len(blocks)]))
@@ -325,7 +346,7 @@ def bench_c4(args, ctx, dev, dist, world, rank):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         nb = blocks[0][1]
-        tr = {k: v[:nb] for k, v in bufs.items() if k not in ("p_busy", "p_idle")}
+        tr = {k: v[:nb] for k, v in bufs[0].items() if k not in ("p_busy", "p_idle", "_keep")}
         fa.generate_trace(ctx, args.seed, nb, T, N, mg_d[:nb], sc_d[:nb], r0=r0, out=tr)
         torch.cuda.synchronize()
         cpu = cpu_baseline(tr, args, nb, T, N)
