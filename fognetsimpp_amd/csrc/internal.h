@@ -215,12 +215,11 @@ struct WideNode {
 };
 static_assert(sizeof(WideNode) == 64, "wide node record is one 64-B line");
 
-// LDS of the wide kernel per node: next advert tick (8 B) + advertised busy
-// (4 B); per lane and group of 16 of its nodes: earliest advert, its node and
-// the smallest view key (20 B); + the histogram.  N = 12,288 fills 160 KiB
-// (a single workgroup may use all of it on gfx950).
+// LDS of the wide kernel: per lane and group of 16 of its nodes the earliest
+// advert, its node and the smallest view key (20 B) + the histogram; the
+// per-node view (next advert tick, advertised busy) is in HBM.
 constexpr int kWideGroupSlots = 16;
-constexpr int kWideMaxNodes = 12288;
+constexpr int kWideMaxNodes = 65536;  // LDS: 82 KiB of group minima
 size_t replay_wide_lds_bytes(int32_t N);
 // workspace: R*T WideEntry followed by R*N WideNode
 size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N);

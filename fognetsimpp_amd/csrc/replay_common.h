@@ -1,5 +1,5 @@
 // replay_common.h — device pieces shared by the two replay kernels:
-// replay.hip (N <= 256, node state in VGPRs) and replay_wide.hip (N <= 12,288,
+// replay.hip (N <= 256, node state in VGPRs) and replay_wide.hip (N <= 65,536,
 // node state in LDS + HBM).  Tick arithmetic, the FES same-tick rule and the
 // exact per-replication statistics accumulator.
 #pragma once

@@ -1,5 +1,5 @@
 // replay_wide.hip — batched trace replay for large fog-node sets on gfx950
-// (BASELINE.json configs[4], C5: 10,000 fog nodes; here N <= 12,288).  Same
+// (BASELINE.json configs[4], C5: 10,000 fog nodes; here N <= 65,536).  Same
 // reference semantics and the same closed form as replay.hip,
 // restated for node sets that do not fit in registers:
 //   decision   BrokerBaseApp3::sendPubAck(status=false)   BrokerBaseApp3.cc:265-304
@@ -8,21 +8,25 @@
 //   advert     advertiseMIPS + broker view update          ComputeBrokerApp3.cc:205-222,
 //                                                          BrokerBaseApp3.cc:123-130
 //
-// One wavefront replays one replication.  Node j belongs to lane j % 64 and
-// only that lane reads or writes node j's state, so the loop needs no
-// barriers:
-//   LDS    nxt[N]     i64  tick at which the advert of node j's head completion
-//                          reaches the broker (kNever: nothing pending)
-//          busy[N]    u32  the broker's advertised busyTime of node j (seconds)
-//          per lane and group of 16 of its nodes: earliest advert, its node,
-//          smallest view key (busy << 32 | j); the lane's minima in VGPRs
-//   HBM    WideEntry [R][T]: per task its arrival, completion, cumulative
+// One wavefront replays one replication.  Node j belongs to lane j % 64 (slot
+// j / 64 of that lane) and only that lane reads or writes node j's state, so
+// the loop needs no barriers:
+//   HBM    view: per lane, its slots' next-advert tick (i64: the head
+//          completion's advert reaches the broker; kNever: nothing pending)
+//          and advertised busyTime (u32 seconds), slot-contiguous, so a group
+//          of 16 slots is two cache lines of ticks and one of busy values;
+//          WideEntry [R][T]: per task its arrival, completion, cumulative
 //          service and the links of its node's pending chain;
 //          WideNode [R][N]: chain ends + copies of head and tail fields (64 B).
+//   LDS    per lane and group of 16 of its slots: earliest advert, its node,
+//          smallest view key (busy << 32 | j); the lane's minima in VGPRs.
+//          13 KiB at N = 10,000, so four replications share a CU (the loop is
+//          latency-bound: every applied advert and push waits on HBM).
 // Publishes are decided one at a time in trace order: adverts that reached
 // the broker strictly before the publish are applied first (lane-parallel:
 // adverts of different nodes commute, those of one node come in completion
-// order), the decision is a wave-wide u64 minimum of the lane minima (ties ->
+// order; an applied advert reloads its group's view with the node record and
+// rescans it), the decision is a wave-wide u64 minimum of the lane minima (ties ->
 // lowest index, the strict '<' of BrokerBaseApp3.cc:273), and the owner lane
 // of the chosen node appends the task and accumulates its statistics (the
 // same record replay.hip's fused epilogue writes).
@@ -43,13 +47,10 @@ namespace {
 constexpr uint32_t kWideMaxS = 0xFFFFu;  // service seconds < 2^16 (kMaxTick arithmetic)
 
 // Per-lane minima are kept in two levels: for each group of kWideGroupSlots
-// of the lane's nodes (node j is slot j / 64 of lane j % 64) the earliest
-// pending advert, its node and the smallest view key live in LDS
-// ([group][lane], conflict-free); the lane's overall minima in VGPRs.  An
-// applied advert rescans one group and the group minima.
+// of the lane's slots the earliest pending advert, its node and the smallest
+// view key live in LDS ([group][lane], conflict-free); the lane's overall
+// minima in VGPRs.  An applied advert rescans one group and the group minima.
 struct WideLds {
-  int64_t* nxt;     // [N]
-  uint32_t* busy;   // [N]
   int64_t* g_nxt;   // [G][64]
   int32_t* g_j;     // [G][64]
   uint64_t* g_key;  // [G][64]
@@ -57,25 +58,41 @@ struct WideLds {
   int G;
 };
 
+// This lane's view in HBM: slot s (node s * 64 + lane) at [s].
+struct WideView {
+  int64_t* nxt;    // [G * kWideGroupSlots]
+  uint32_t* busy;  // [G * kWideGroupSlots]
+};
+
 __host__ __device__ __forceinline__ int wide_groups(int N) {
   return ((N + kWave - 1) / kWave + kWideGroupSlots - 1) / kWideGroupSlots;
 }
 
-// Recompute group g of this lane from the per-node arrays.
-__device__ __forceinline__ void group_scan(const WideLds& L, int N, int lane, int g) {
+// Rescan group g of this lane from its view (slot `sl` replaced by the
+// values just computed: its load may have been issued before their store).
+__device__ __forceinline__ void group_scan(const WideLds& L, const WideView& V, int N, int lane, int g, int sl,
+                                           int64_t sl_nxt, uint32_t sl_busy) {
+  int64_t x[kWideGroupSlots];
+  uint32_t b[kWideGroupSlots];
+#pragma unroll
+  for (int i = 0; i < kWideGroupSlots; ++i) {
+    x[i] = V.nxt[g * kWideGroupSlots + i];
+    b[i] = V.busy[g * kWideGroupSlots + i];
+  }
   int64_t mn = kNever;
   int mj = lane;
   uint64_t mk = ~0ull;
 #pragma unroll
   for (int i = 0; i < kWideGroupSlots; ++i) {
-    const int j = (g * kWideGroupSlots + i) * kWave + lane;
+    const int s = g * kWideGroupSlots + i;
+    const int j = s * kWave + lane;
     if (j < N) {
-      const int64_t x = L.nxt[j];
-      if (x < mn) {
-        mn = x;
+      const int64_t xi = s == sl ? sl_nxt : x[i];
+      if (xi < mn) {
+        mn = xi;
         mj = j;
       }
-      const uint64_t key = ((uint64_t)L.busy[j] << 32) | (uint32_t)j;
+      const uint64_t key = ((uint64_t)(s == sl ? sl_busy : b[i]) << 32) | (uint32_t)j;
       mk = key < mk ? key : mk;
     }
   }
@@ -108,7 +125,7 @@ __device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn
 // are not done yet, a difference of cumulative sums; the head advances.
 // Returns false when the advertised busy time does not fit 32 bits.
 __device__ __forceinline__ bool apply_advert(int j, WideNode* nd, const WideEntry* e, int64_t dl, int64_t ul,
-                                             const WideLds& L) {
+                                             int64_t& nxt_j, uint32_t& busy_j) {
   WideNode h = nd[j];
   uint64_t c_arrived = h.hd_C;  // only the completing task itself ...
   if (arrives_before(h.tl_a, h.hd_done, dl, h.hd_S)) {
@@ -124,10 +141,10 @@ __device__ __forceinline__ bool apply_advert(int j, WideNode* nd, const WideEntr
     }
   }
   const uint64_t busy = c_arrived - h.hd_C;
-  L.busy[j] = (uint32_t)busy;
+  busy_j = (uint32_t)busy;
   h.npend -= 1;
   if (h.npend == 0) {
-    L.nxt[j] = kNever;
+    nxt_j = kNever;
   } else {
     // FIFO: the next task started at max(arrival, this completion); its
     // done tick was fixed when it was pushed
@@ -137,14 +154,33 @@ __device__ __forceinline__ bool apply_advert(int j, WideNode* nd, const WideEntr
     h.hd_C = nx.C;
     h.hd_S = nx.S;
     h.hd_next = nx.next;  // valid while npend >= 2
-    L.nxt[j] = nx.done == kNever ? kNever : nx.done + ul;  // never: crashed before it completes
+    nxt_j = nx.done == kNever ? kNever : nx.done + ul;  // never: crashed before it completes
   }
   nd[j] = h;
   return busy < 0xFFFFFFFFull;
 }
 
+// Workspace layout (launch_replay_wide, replay_wide_workspace_bytes).
+struct WideWs {
+  size_t e_off, nd_off, nxt_off, busy_off, bytes;
+};
+
+__host__ __device__ __forceinline__ size_t align64(size_t x) { return (x + 63) & ~(size_t)63; }
+
+__host__ __device__ __forceinline__ WideWs wide_ws(int32_t R, int32_t T, int32_t N) {
+  const size_t SP = (size_t)wide_groups(N) * kWideGroupSlots;  // view slots per lane
+  WideWs w;
+  w.e_off = 0;
+  w.nd_off = align64(w.e_off + (size_t)R * (size_t)T * sizeof(WideEntry));
+  w.nxt_off = align64(w.nd_off + (size_t)R * (size_t)N * sizeof(WideNode));
+  w.busy_off = align64(w.nxt_off + (size_t)R * kWave * SP * sizeof(int64_t));
+  w.bytes = align64(w.busy_off + (size_t)R * kWave * SP * sizeof(uint32_t));
+  return w;
+}
+
 template <int POL>
-__global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry* E, WideNode* ND) {
+__global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry* E, WideNode* ND, int64_t* VN,
+                                                         uint32_t* VB) {
   constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
   extern __shared__ __align__(16) unsigned char w_lds[];
   const int r = blockIdx.x;
@@ -152,12 +188,12 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
   const int T = A.T, N = A.N;
   WideLds L;
   L.G = wide_groups(N);
-  L.nxt = reinterpret_cast<int64_t*>(w_lds);
-  L.g_nxt = L.nxt + N;
+  L.g_nxt = reinterpret_cast<int64_t*>(w_lds);
   L.g_key = reinterpret_cast<uint64_t*>(L.g_nxt + L.G * kWave);
-  L.busy = reinterpret_cast<uint32_t*>(L.g_key + L.G * kWave);
-  L.g_j = reinterpret_cast<int32_t*>(L.busy + N);
+  L.g_j = reinterpret_cast<int32_t*>(L.g_key + L.G * kWave);
   L.hist = reinterpret_cast<uint32_t*>(L.g_j + L.G * kWave);
+  const int SP = L.G * kWideGroupSlots;
+  const WideView V{VN + ((size_t)r * kWave + lane) * SP, VB + ((size_t)r * kWave + lane) * SP};
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)T;
   WideEntry* const e = E + tbase;
@@ -175,12 +211,19 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
     bad |= (m <= 0) | (d < 0) | (u < 0) | (d > kMaxTick) | (u > kMaxTick) | (ia < u) | (ia >= arrive0);
     bad |= dn != kNever && (dn < ia || dn > kMaxTick);
     if constexpr (kExt) bad |= d >= kExtMaxDl;
-    L.nxt[j] = kNever;
-    L.busy[j] = 0u;
     nd[j] = WideNode{-1, -1, 0, -1, 0, 0u, 0, 0, 0u, 0u, 0u};
   }
+  for (int s = 0; s < SP; ++s) {  // slots past N too (group rescans read them)
+    V.nxt[s] = kNever;
+    V.busy[s] = 0u;
+  }
   for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) L.hist[h] = 0u;
-  for (int g = 0; g < L.G; ++g) group_scan(L, N, lane, g);  // lane-local: no barrier needed
+  for (int g = 0; g < L.G; ++g) {  // the initial view: nothing pending, every busy 0
+    const int j0 = g * kWideGroupSlots * kWave + lane;
+    L.g_nxt[g * kWave + lane] = kNever;
+    L.g_j[g * kWave + lane] = lane;
+    L.g_key[g * kWave + lane] = j0 < N ? (uint64_t)(uint32_t)j0 : ~0ull;
+  }
   __syncthreads();
   uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
 
@@ -216,8 +259,13 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
       while (ballot(mn < t)) {
         if (mn < t) {
           const int j = mj;
-          lerr |= !apply_advert(j, nd, e, A.dl[nbase + j], A.ul[nbase + j], L);
-          group_scan(L, N, lane, (j / kWave) / kWideGroupSlots);
+          const int sl = j / kWave;
+          int64_t nxt_j;
+          uint32_t busy_j;
+          lerr |= !apply_advert(j, nd, e, A.dl[nbase + j], A.ul[nbase + j], nxt_j, busy_j);
+          V.nxt[sl] = nxt_j;
+          V.busy[sl] = busy_j;
+          group_scan(L, V, N, lane, sl / kWideGroupSlots, sl, nxt_j, busy_j);
           lane_min(L, lane, mn, mj, mk);
         }
       }
@@ -234,7 +282,7 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
         uint32_t mjj = ~0u;
         for (int j = lane; j < N; j += kWave) {
           const uint32_t S = min(rq / (uint32_t)A.mips[nbase + j], kExtSatS);
-          const uint64_t c = (uint64_t)A.dl[nbase + j] + ((uint64_t)L.busy[j] + S) * (uint64_t)kTicksPerSecond;
+          const uint64_t c = (uint64_t)A.dl[nbase + j] + ((uint64_t)V.busy[j / kWave] + S) * (uint64_t)kTicksPerSecond;
           if (c < mc) {
             mc = c;
             mjj = (uint32_t)j;
@@ -288,7 +336,7 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
             h.hd_S = S;
             const int64_t x = done == kNever ? kNever : done + ul_k;
             const int g = ((int)k / kWave) / kWideGroupSlots;
-            L.nxt[k] = x;
+            V.nxt[k / kWave] = x;
             if (x < L.g_nxt[g * kWave + lane]) {
               L.g_nxt[g * kWave + lane] = x;
               L.g_j[g * kWave + lane] = (int)k;
@@ -365,22 +413,23 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
   // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12)
   // with B_j = node j's service seconds (its tail's cumulative sum), summed in node order
   if (A.p_busy && A.out_stats) {
+    // per node j (lane j % 64), then summed in node order 64 at a time
     const int64_t H = n_done > 0 ? acc.last : 0;
-    double* const s_e = reinterpret_cast<double*>(L.nxt);  // dead now; lane j%64 wrote nxt[j]
-    for (int j = lane; j < N; j += kWave) {
-      const int64_t B = (int64_t)nd[j].tl_C;
-      const double eb = mul_rn(A.p_busy[nbase + j], (double)B);
-      const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
-      const double en = add_rn(eb, mul_rn(A.p_idle[nbase + j], idle));
-      s_e[j] = en;
-      if (A.out_energy) A.out_energy[(size_t)r * (size_t)N + j] = en;
+    double sum = 0.0;
+    for (int j0 = 0; j0 < N; j0 += kWave) {
+      const int j = j0 + lane;
+      double en = 0.0;
+      if (j < N) {
+        const int64_t B = (int64_t)nd[j].tl_C;
+        const double eb = mul_rn(A.p_busy[nbase + j], (double)B);
+        const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
+        en = add_rn(eb, mul_rn(A.p_idle[nbase + j], idle));
+        if (A.out_energy) A.out_energy[(size_t)r * (size_t)N + j] = en;
+      }
+      const int m = min(kWave, N - j0);
+      for (int l = 0; l < m; ++l) sum = add_rn(sum, __longlong_as_double(readlane_i64(__double_as_longlong(en), l)));
     }
-    __syncthreads();
-    if (lane == 0) {
-      double sum = 0.0;
-      for (int j = 0; j < N; ++j) sum = add_rn(sum, s_e[j]);
-      S->energy_j = sum;
-    }
+    if (lane == 0) S->energy_j = sum;
   }
   if (hist) {
     __syncthreads();
@@ -390,35 +439,33 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
 }
 
 template <int POL>
-void launch_wide_pol(const ReplayArgs& a, WideEntry* e, WideNode* nd, size_t lds, hipStream_t s) {
-  // dynamic LDS above 64 KiB (a single workgroup may take all 160 KiB on gfx950)
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&replay_wide_kernel<POL>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  (void)hipGetLastError();
-  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(a.R), dim3(kWave), lds, s, a, e, nd);
+void launch_wide_pol(const ReplayArgs& a, WideEntry* e, WideNode* nd, int64_t* vn, uint32_t* vb, size_t lds,
+                     hipStream_t s) {
+  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(a.R), dim3(kWave), lds, s, a, e, nd, vn, vb);
 }
 
 }  // namespace
 
 size_t replay_wide_lds_bytes(int32_t N) {
   const size_t G = (size_t)wide_groups(N);
-  return (size_t)N * (sizeof(int64_t) + sizeof(uint32_t)) +
-         G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int32_t)) +
+  return G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int32_t)) +
          FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t);
 }
 
-size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N) {
-  return (size_t)R * (size_t)T * sizeof(WideEntry) + (size_t)R * (size_t)N * sizeof(WideNode);
-}
+size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N) { return wide_ws(R, T, N).bytes; }
 
 hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, hipStream_t s) {
-  WideEntry* const e = reinterpret_cast<WideEntry*>(workspace);
-  WideNode* const nd = reinterpret_cast<WideNode*>(e + (size_t)a.R * (size_t)a.T);
+  const WideWs w = wide_ws(a.R, a.T, a.N);
+  unsigned char* const base = static_cast<unsigned char*>(workspace);
+  WideEntry* const e = reinterpret_cast<WideEntry*>(base + w.e_off);
+  WideNode* const nd = reinterpret_cast<WideNode*>(base + w.nd_off);
+  int64_t* const vn = reinterpret_cast<int64_t*>(base + w.nxt_off);
+  uint32_t* const vb = reinterpret_cast<uint32_t*>(base + w.busy_off);
   const size_t lds = replay_wide_lds_bytes(a.N);
   if (a.policy == FOGNET_POLICY_EXT_LAT)
-    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, e, nd, lds, s);
+    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, e, nd, vn, vb, lds, s);
   else
-    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, e, nd, lds, s);
+    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, e, nd, vn, vb, lds, s);
   return hipGetLastError();
 }
 

@@ -209,7 +209,7 @@ def test_precondition_errors(ctx, bad, N):
 
 
 def test_unsupported_sizes(ctx):
-    tr = tg.make_batch(5, 1, 12289, 10)  # the wide kernel's LDS holds the view of 12,288 nodes
+    tr = tg.make_batch(5, 1, 65537, 10)  # kWideMaxNodes: the wide kernel's LDS group minima
     with pytest.raises(fa.FognetError) as e:
         run_gpu(ctx, tr)
     assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED
@@ -411,7 +411,7 @@ def test_ext_lat_latency_bound(ctx):
 # completion advert lands, so the C3 loads (rho 0.5..0.95) keep 10^3-10^4 nodes
 # on node 0 for the whole trace; light loads spread decisions over many nodes.
 @pytest.mark.parametrize("N,T,R,rho", [(257, 2000, 3, 0.8), (700, 3000, 3, 0.01), (4096, 4000, 2, 0.01),
-                                       (12288, 3000, 1, 0.002)])
+                                       (12288, 3000, 1, 0.002), (20000, 1500, 1, 0.001)])
 def test_wide_matches_oracle(ctx, N, T, R, rho):
     tr = tg.make_batch(0x5EED0005 + N, R, N, T, rho=rho, lat_scale=10)
     pb, pi = fa.power_model(tr["mips"])
