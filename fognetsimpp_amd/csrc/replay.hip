@@ -658,7 +658,9 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
 #endif
 #if FOGNET_REPLAY_PROFILE == 1
   uint64_t p_iter = 0, p_advit = 0, p_adv = 0, p_end_k = 0, p_end_j = 0, p_end_c = 0, p_hz = 0, p_refill = 0, p_w0 = 0, p_rd = 0,
-           p_chunks = 0, p_pk0 = 0, p_resume = 0;
+           p_chunks = 0, p_pk0 = 0, p_resume = 0, p_same = 0, p_endh_same = 0;
+  int prev_k = -1;
+  bool prev_end_h = false;
   auto young = [&](int s, bool need) { return ballot(need) && ((ops - (pf >> (8 * s))) & 0xFFu) < 2u; };
 #endif
   // A run that consumed the rest of its chunk continues into the next one
@@ -742,6 +744,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
         }
         TMARK(2)
         const int k = (int)(best & 0xFFu);
+        PROF(p_same += k == prev_k; p_endh_same += prev_end_h && k == prev_k;)
 
         // 3) run horizon: earliest advert that could change the decision.
         //    Only nodes whose key can drop below best (busy >= 0) matter.
@@ -936,7 +939,8 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
         E_carry = E;
       }
       TMARK(6)
-      PROF(p_pk0 += pend_k == 0u; if (jq >= cnt) p_end_c++; else if (E == E_other) p_end_j++; else p_end_k++;)
+      PROF(p_pk0 += pend_k == 0u; if (jq >= cnt) p_end_c++; else if (E == E_other) p_end_j++; else p_end_k++;
+           prev_k = k; prev_end_h = jq < cnt && E == E_other;)
       jp = jq;
     }
   }
@@ -984,6 +988,8 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     S->resp_sum_hi = p_end_c;
     S->resp_sq_lo = p_resume;
     S->resp_sum_lo = p_pk0;
+    S->busy_s = (int64_t)p_same;
+    S->resp_sq_hi = p_endh_same;
 #endif
   }
 #if !defined(FOGNET_REPLAY_PROFILE) || FOGNET_REPLAY_PROFILE == 0
