@@ -124,9 +124,9 @@ __device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn
 // :254) = the service of the tasks that reached j before that completion and
 // are not done yet, a difference of cumulative sums; the head advances.
 // Returns false when the advertised busy time does not fit 32 bits.
-__device__ __forceinline__ bool apply_advert(int j, WideNode* nd, const WideEntry* e, int64_t dl, int64_t ul,
+// h: node j's record (loaded from HBM or the lane's cached copy), updated in place.
+__device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, int64_t dl, int64_t ul,
                                              int64_t& nxt_j, uint32_t& busy_j) {
-  WideNode h = nd[j];
   uint64_t c_arrived = h.hd_C;  // only the completing task itself ...
   if (arrives_before(h.tl_a, h.hd_done, dl, h.hd_S)) {
     c_arrived = h.tl_C;  // ... or everything up to the newest task (the common case)
@@ -156,7 +156,6 @@ __device__ __forceinline__ bool apply_advert(int j, WideNode* nd, const WideEntr
     h.hd_next = nx.next;  // valid while npend >= 2
     nxt_j = nx.done == kNever ? kNever : nx.done + ul;  // never: crashed before it completes
   }
-  nd[j] = h;
   return busy < 0xFFFFFFFFull;
 }
 
@@ -236,6 +235,14 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
   int n_short = 0;         // tasks of this lane's nodes that never complete (node-down)
   int64_t prev_t = INT64_MIN;
   int n_done = 0;
+  // the node this lane pushed to last: under the stale view the broker keeps
+  // choosing it, so its record and parameters stay in registers between
+  // pushes; nd[cj] in HBM is stale until the record is written back (when
+  // the lane pushes to another node, and after the loop)
+  int cj = -1;
+  WideNode ch{};
+  int32_t c_mips = 1;
+  int64_t c_dl = 0, c_ul = 0, c_down = kNever;
 
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
@@ -262,7 +269,11 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
           const int sl = j / kWave;
           int64_t nxt_j;
           uint32_t busy_j;
-          lerr |= !apply_advert(j, nd, e, A.dl[nbase + j], A.ul[nbase + j], nxt_j, busy_j);
+          const bool hit = j == cj;
+          WideNode h = hit ? ch : nd[j];
+          lerr |= !apply_advert(h, e, hit ? c_dl : A.dl[nbase + j], hit ? c_ul : A.ul[nbase + j], nxt_j, busy_j);
+          if (hit) ch = h;
+          else nd[j] = h;
           V.nxt[sl] = nxt_j;
           V.busy[sl] = busy_j;
           group_scan(L, V, N, lane, sl / kWideGroupSlots, sl, nxt_j, busy_j);
@@ -298,11 +309,20 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
 
       // 3) node k: task arrival (ComputeBrokerApp3.cc:269-320), owner lane
       if (lane == (int)(k % kWave)) {
-        WideNode h = nd[k];
-        const int32_t mips_k = A.mips[nbase + k];
-        const int64_t dl_k = A.dl[nbase + k], ul_k = A.ul[nbase + k];
+        if ((int)k != cj) {
+          if (cj >= 0) nd[cj] = ch;  // write back the previous node's record
+          cj = (int)k;
+          ch = nd[k];
+          c_mips = A.mips[nbase + k];
+          c_dl = A.dl[nbase + k];
+          c_ul = A.ul[nbase + k];
+          c_down = A.down ? A.down[nbase + k] : kNever;
+        }
+        WideNode h = ch;
+        const int32_t mips_k = c_mips;
+        const int64_t dl_k = c_dl, ul_k = c_ul;
         const uint32_t S = rq / (uint32_t)mips_k;  // double tskTime = requiredMIPS / MIPS (:276)
-        const int64_t down_k = A.down ? A.down[nbase + k] : kNever;
+        const int64_t down_k = c_down;
         const int64_t a = t + dl_k;
         // the previous task on node k is its tail (FIFO single server); its
         // done is kNever if the node crashed before completing it
@@ -356,7 +376,7 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
           h.tl_C = C;
           h.tl_S = S;
           h.npend += 1;
-          nd[k] = h;
+          ch = h;
           max_pend = max(max_pend, (uint32_t)h.npend);
           const size_t o = tbase + (size_t)i;
           A.out_node[o] = (int32_t)k;
@@ -394,6 +414,8 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
       ++n_done;
     }
   }
+
+  if (cj >= 0) nd[cj] = ch;
 
   // ---- per-replication record (the fields replay_kernel + its epilogue write)
   acc = wave_merge(acc);
