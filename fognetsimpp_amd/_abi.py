@@ -30,9 +30,10 @@ FOGNET_POLICY_EXT_LAT = 16
 TICKS_PER_SECOND = 10**12
 # fognet_v2_action (BrokerBaseApp2 decision outcome)
 V2_LOCAL, V2_FORWARD, V2_DROPPED, V2_NO_NODES = 3, 4, 5, 6
-ABI_VERSION = 5
+ABI_VERSION = 6
 HIST_METRICS = 2  # 0 queueTime, 1 response
 HIST_BINS = 64
+COMM_ID_BYTES = 128  # FOGNET_COMM_ID_BYTES
 
 
 class RepStats(C.Structure):
@@ -187,6 +188,10 @@ SIGNATURES = {
     "fognet_gen_trace_dev": (C.c_int, [P, C.POINTER(GenParams), C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                        P, P, P, P, P, P, P]),
     "fognet_sync": (C.c_int, [P]),
+    "fognet_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "fognet_comm_create": (C.c_int, [P, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.POINTER(P)]),
+    "fognet_comm_destroy": (None, [P]),
+    "fognet_allreduce_stats": (C.c_int, [P, P, C.POINTER(JobStats), P, P]),
     # include/fognet_io.h (host only, no context)
     "fognet_io_last_error": (C.c_char_p, []),
     "fognet_trace_write": (C.c_int, [C.c_char_p, C.POINTER(BatchIn), P, C.c_char_p]),

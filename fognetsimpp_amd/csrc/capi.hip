@@ -2,6 +2,7 @@
 // Pure host C++ around the gfx950 kernels; there is no CPU compute path: every
 // decision is evaluated on the device, and the library refuses to create a
 // context without a gfx950 GPU.
+#include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -536,6 +537,145 @@ int fognet_gen_trace_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t r0, 
   hipError_t e = fognet::launch_gen_trace(*p, r0, R, T, N, arrive_tick, req_mips, mips, dl_tick, ul_tick,
                                           init_adv_tick, (hipStream_t)stream);
   return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "tracegen launch");
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- RCCL stats exchange
+// RCCL's C API, resolved with dlsym on first use (no link-time dependency).
+namespace {
+
+typedef struct {
+  char internal[FOGNET_COMM_ID_BYTES];
+} RcclId;
+typedef void* RcclComm;
+enum { kRcclInt8 = 0, kRcclUint8 = 1, kRcclInt64 = 4, kRcclSum = 0 };
+
+struct Rccl {
+  int (*get_unique_id)(RcclId*) = nullptr;
+  int (*comm_init_rank)(RcclComm*, int, RcclId, int) = nullptr;
+  int (*comm_destroy)(RcclComm) = nullptr;
+  int (*all_gather)(const void*, void*, size_t, int, RcclComm, hipStream_t) = nullptr;
+  int (*all_reduce)(const void*, void*, size_t, int, int, RcclComm, hipStream_t) = nullptr;
+  const char* (*error_string)(int) = nullptr;
+  bool ok = false;
+  std::string why;
+};
+
+Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      x.why = std::string("cannot load librccl: ") + dlerror();
+      return x;
+    }
+    x.get_unique_id = reinterpret_cast<decltype(x.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+    x.comm_init_rank = reinterpret_cast<decltype(x.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+    x.comm_destroy = reinterpret_cast<decltype(x.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    x.all_gather = reinterpret_cast<decltype(x.all_gather)>(dlsym(h, "ncclAllGather"));
+    x.all_reduce = reinterpret_cast<decltype(x.all_reduce)>(dlsym(h, "ncclAllReduce"));
+    x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(h, "ncclGetErrorString"));
+    x.ok = x.get_unique_id && x.comm_init_rank && x.comm_destroy && x.all_gather && x.all_reduce && x.error_string;
+    if (!x.ok) x.why = "librccl lacks the NCCL collective API";
+    return x;
+  }();
+  return r;
+}
+
+int rccl_fail(fognet_ctx* c, int e, const char* what) {
+  return fail(c, FOGNET_ERR_DEVICE, std::string(what) + ": " + rccl().error_string(e));
+}
+
+}  // namespace
+
+struct fognet_comm {
+  RcclComm comm = nullptr;
+  int32_t world = 0, rank = 0;
+  int device = -1;
+  void* buf = nullptr;  // [world] job records
+};
+
+extern "C" {
+
+int fognet_comm_unique_id(uint8_t id[FOGNET_COMM_ID_BYTES]) {
+  if (!id) return FOGNET_ERR_ARG;
+  Rccl& r = rccl();
+  if (!r.ok) return FOGNET_ERR_UNSUPPORTED;
+  RcclId x;
+  if (r.get_unique_id(&x) != 0) return FOGNET_ERR_DEVICE;
+  memcpy(id, x.internal, FOGNET_COMM_ID_BYTES);
+  return FOGNET_OK;
+}
+
+int fognet_comm_create(fognet_ctx* c, int32_t world, int32_t rank, const uint8_t id[FOGNET_COMM_ID_BYTES],
+                       fognet_comm** out) {
+  if (!c || !out || !id || world <= 0 || rank < 0 || rank >= world) return fail(c, FOGNET_ERR_ARG, "comm: bad world/rank");
+  *out = nullptr;
+  Rccl& r = rccl();
+  if (!r.ok) return fail(c, FOGNET_ERR_UNSUPPORTED, r.why);
+  int rc = set_device(c);
+  if (rc) return rc;
+  fognet_comm* m = new fognet_comm;
+  m->world = world;
+  m->rank = rank;
+  m->device = c->device;
+  RcclId x;
+  memcpy(x.internal, id, FOGNET_COMM_ID_BYTES);
+  const int e = r.comm_init_rank(&m->comm, world, x, rank);
+  if (e != 0) {
+    delete m;
+    return rccl_fail(c, e, "ncclCommInitRank");
+  }
+  const hipError_t he = hipMalloc(&m->buf, (size_t)world * sizeof(fognet_job_stats));
+  if (he != hipSuccess) {
+    r.comm_destroy(m->comm);
+    delete m;
+    return hip_fail(c, he, "hipMalloc comm buffer");
+  }
+  *out = m;
+  return FOGNET_OK;
+}
+
+void fognet_comm_destroy(fognet_comm* m) {
+  if (!m) return;
+  (void)hipSetDevice(m->device);
+  if (m->comm) rccl().comm_destroy(m->comm);
+  if (m->buf) (void)hipFree(m->buf);
+  delete m;
+}
+
+int fognet_allreduce_stats(fognet_ctx* c, fognet_comm* m, fognet_job_stats* inout, int64_t* hist, void* stream) {
+  if (!c || !m || !inout) return fail(c, FOGNET_ERR_ARG, "allreduce_stats: null argument");
+  if (m->device != c->device) return fail(c, FOGNET_ERR_ARG, "allreduce_stats: comm and context on different devices");
+  int rc = set_device(c);
+  if (rc) return rc;
+  Rccl& r = rccl();
+  hipStream_t s = (hipStream_t)stream;
+  const size_t sz = sizeof(fognet_job_stats);
+  unsigned char* const buf = static_cast<unsigned char*>(m->buf);
+  hipError_t he = hipMemcpyAsync(buf + (size_t)m->rank * sz, inout, sz, hipMemcpyHostToDevice, s);
+  if (he != hipSuccess) return hip_fail(c, he, "allreduce_stats copy-in");
+  int e = r.all_gather(buf + (size_t)m->rank * sz, buf, sz, kRcclUint8, m->comm, s);  // in place
+  if (e != 0) return rccl_fail(c, e, "ncclAllGather");
+  if (hist) {
+    e = r.all_reduce(hist, hist, (size_t)FOGNET_HIST_METRICS * FOGNET_HIST_BINS, kRcclInt64, kRcclSum, m->comm, s);
+    if (e != 0) return rccl_fail(c, e, "ncclAllReduce");
+  }
+  std::string recs((size_t)m->world * sz, '\0');
+  he = hipMemcpyAsync(&recs[0], buf, recs.size(), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess) return hip_fail(c, he, "allreduce_stats copy-out");
+  fognet_job_stats acc;
+  fognet_job_stats_init(&acc);
+  for (int32_t k = 0; k < m->world; ++k) {  // rank order: exact and identical on every rank
+    fognet_job_stats rec;
+    memcpy(&rec, recs.data() + (size_t)k * sz, sz);
+    fognet_job_stats_merge(&acc, &rec);
+  }
+  *inout = acc;
+  return FOGNET_OK;
 }
 
 }  // extern "C"

@@ -58,3 +58,50 @@ def allreduce_hist_energy(hist: torch.Tensor, energy: torch.Tensor, group=None) 
 
     dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
     dist.all_reduce(energy, op=dist.ReduceOp.SUM, group=group)
+
+
+class StatsComm:
+    """The library's own stats exchange (``fognet_allreduce_stats``, the C-ABI
+    path a C++/OMNeT++ host uses without PyTorch): one RCCL communicator per
+    rank; the 128-byte id from :meth:`unique_id` on rank 0 reaches the other
+    ranks over any channel (here typically ``torch.distributed.broadcast_object_list``)."""
+
+    def __init__(self, ctx, world: int, rank: int, uid: bytes):
+        import ctypes as C
+
+        if len(uid) != _abi.COMM_ID_BYTES:
+            raise ValueError("comm id must be 128 bytes")
+        self._ctx = ctx
+        self._lib = ctx._lib
+        buf = (C.c_uint8 * _abi.COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        ctx.check(self._lib.fognet_comm_create(ctx.handle, world, rank, buf, C.byref(h)), "comm_create")
+        self._h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+
+        buf = (C.c_uint8 * _abi.COMM_ID_BYTES)()
+        rc = _abi.load().fognet_comm_unique_id(buf)
+        if rc != _abi.FOGNET_OK:
+            raise _abi.FognetError(rc, "fognet_comm_unique_id")
+        return bytes(buf)
+
+    def allreduce(self, job, hist: torch.Tensor | None = None) -> np.ndarray:
+        """Exact job record over all ranks (all-gather + rank-order merge);
+        ``hist`` (device int64 [2, 64]) is summed in place."""
+        import ctypes as C
+
+        from .engine import _ptr, _stream_ptr
+
+        js = _abi.JobStats.from_buffer_copy(np.ascontiguousarray(job).tobytes())
+        dev = torch.device("cuda", self._ctx.device)
+        self._ctx.check(self._lib.fognet_allreduce_stats(self._ctx.handle, self._h, C.byref(js),
+                                                         _ptr(hist), _stream_ptr(dev)), "allreduce_stats")
+        return np.frombuffer(bytes(js), dtype=_abi.JOB_STATS_DTYPE)[0]
+
+    def close(self):
+        if self._h:
+            self._lib.fognet_comm_destroy(self._h)
+            self._h = None

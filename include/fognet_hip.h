@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define FOGNET_ABI_VERSION 5
+#define FOGNET_ABI_VERSION 6
 #define FOGNET_TICKS_PER_SECOND 1000000000000LL
 
 /* Latency histograms (device-side statistics, summed over replications; the
@@ -348,6 +348,28 @@ int fognet_gen_trace_dev(fognet_ctx *ctx, const fognet_gen_params *p, int64_t r0
 
 /* Synchronise the context's device. */
 int fognet_sync(fognet_ctx *ctx);
+
+/* ---- Multi-GPU statistics exchange over RCCL (xGMI), SURVEY.md §8(b)
+ * `fognet_allreduce_stats` and §8(e): replications are sharded over ranks (one
+ * process per GPU) and this end-of-run exchange is the only collective.  RCCL
+ * is loaded on first use (librccl.so.1; a copy already in the process, e.g.
+ * PyTorch's, is reused).  Rank 0 creates the id; the caller moves its bytes to
+ * the other ranks (MPI, a shared file, a TCP store ...).  Collective calls:
+ * every rank calls fognet_comm_create / fognet_allreduce_stats in the same order. */
+#define FOGNET_COMM_ID_BYTES 128
+typedef struct fognet_comm fognet_comm;
+int fognet_comm_unique_id(uint8_t id[FOGNET_COMM_ID_BYTES]);
+int fognet_comm_create(fognet_ctx *ctx, int32_t world, int32_t rank, const uint8_t id[FOGNET_COMM_ID_BYTES],
+                       fognet_comm **out);
+void fognet_comm_destroy(fognet_comm *comm);
+/* *inout (host): this rank's job record in, the job record of all ranks out:
+ * the records are all-gathered and merged in rank order with
+ * fognet_job_stats_merge, so the result is exact and identical on every rank
+ * (energy: fp64 sum in rank order).  hist (device pointer to
+ * [FOGNET_HIST_METRICS][FOGNET_HIST_BINS] int64, nullable): summed in place.
+ * Enqueued on hip_stream; returns after the exchange completed. */
+int fognet_allreduce_stats(fognet_ctx *ctx, fognet_comm *comm, fognet_job_stats *inout, int64_t *hist,
+                           void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -111,3 +111,47 @@ def test_gloo_world2_job_stats_match_single_process():
     # and the merge is associative: per-replication records merged one by one
     one_by_one = merge_job_stats([job_from_rep_stats(st[i:i + 1]) for i in range(reps)])
     assert one_by_one.tobytes() == got
+
+
+# ------------------------------------------------------------------ C-ABI stats exchange (fognet_allreduce_stats)
+
+def test_comm_unique_id_and_argument_checks():
+    """RCCL is loaded on first use; ids are 128 opaque bytes; a communicator
+    needs a context and a valid (world, rank)."""
+    import ctypes as C
+
+    from fognetsimpp_amd import _abi, dist
+
+    a, b = dist.StatsComm.unique_id(), dist.StatsComm.unique_id()
+    assert len(a) == _abi.COMM_ID_BYTES and a != b
+    lib = _abi.load()
+    h = C.c_void_p()
+    uid = (C.c_uint8 * _abi.COMM_ID_BYTES).from_buffer_copy(a)
+    assert lib.fognet_comm_create(None, 1, 0, uid, C.byref(h)) == _abi.FOGNET_ERR_ARG
+    assert lib.fognet_allreduce_stats(None, None, None, None, None) == _abi.FOGNET_ERR_ARG
+    lib.fognet_comm_destroy(None)  # no-op
+
+
+@pytest.mark.gpu
+def test_comm_allreduce_world1_is_identity(ctx):
+    """World 1 over the library's own RCCL communicator: the merged record is
+    this rank's record and the histogram is unchanged."""
+    import torch
+
+    import fognetsimpp_amd as fa
+    import tracegen as tg
+    from fognetsimpp_amd import dist
+
+    dev = torch.device("cuda", 0)
+    tr = tg.make_batch(0x5EED0001, 4, 64, 3000)
+    out = fa.run_batch(ctx, fa.as_device_trace(tr, dev), hist=True)
+    torch.cuda.synchronize()
+    job = fa.job_from_reps(out.rep_stats())
+    hist0 = out.hist.clone()
+    comm = dist.StatsComm(ctx, 1, 0, dist.StatsComm.unique_id())
+    try:
+        merged = comm.allreduce(job, out.hist)
+    finally:
+        comm.close()
+    assert merged.tobytes() == job.tobytes()
+    assert torch.equal(out.hist, hist0)
