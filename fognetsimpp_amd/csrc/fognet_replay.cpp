@@ -35,6 +35,8 @@
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <chrono>
+#include <thread>
 #include <vector>
 
 #include "fognet_hip.h"
@@ -326,7 +328,8 @@ int64_t parse_int(const std::string& raw, const std::string& what) {
 
 struct Options {
   std::string ini, config = "General", trace_in, trace_out, sca, vec, users = "user";
-  std::string node_prefix = "ComputeBroker";
+  std::string node_prefix = "ComputeBroker", comm_id;
+  int world = 1, rank = 0;
   int nodes = 0, reps = 1, device = 0, ring = 0;
   uint32_t seed = 1;
   int64_t dl = kMs, ul = kMs, user_ul = kMs, user_dl = kMs, stop = kNoTick;
@@ -418,7 +421,8 @@ void hip_check(hipError_t e, const char* what) {
 
 // The publish traces of R replications (glibc seeds seed .. seed + R - 1).
 // Returns T (equal for every replication: the seed only changes MIPSRequired).
-int32_t gen_traces(const Scenario& sc, const Options& o, int64_t user_dl, std::vector<int64_t>& arrive,
+// Replications r0 .. r0 + n - 1 of the job (glibc seed o.seed + r).
+int32_t gen_traces(const Scenario& sc, const Options& o, int64_t user_dl, int r0, int n, std::vector<int64_t>& arrive,
                    std::vector<int32_t>& req) {
   const int32_t U = (int32_t)sc.users.size();
   std::vector<int64_t> up(U, o.user_ul), dn(U, user_dl);
@@ -433,20 +437,21 @@ int32_t gen_traces(const Scenario& sc, const Options& o, int64_t user_dl, std::v
   int32_t T = -1;
   std::vector<int64_t> a(cap);
   std::vector<int32_t> q(cap);
-  for (int r = 0; r < o.reps; ++r) {
+  for (int i = 0; i < n; ++i) {
+    const int r = r0 + i;
     int32_t t = 0;
     check(fognet_gen_trace_mqtt(o.seed + (uint32_t)r, U, sc.u_start.data(), sc.u_interval.data(), up.data(), dn.data(),
                                 sc.stop, 200, 701, cap, a.data(), q.data(), nullptr, &t),
           "fognet_gen_trace_mqtt");
     if (T < 0) {
       T = t;
-      arrive.assign((size_t)o.reps * T, 0);
-      req.assign((size_t)o.reps * T, 0);
+      arrive.assign((size_t)n * T, 0);
+      req.assign((size_t)n * T, 0);
     } else if (t != T) {
       die("replications produced different publish counts");
     }
-    std::copy(a.begin(), a.begin() + T, arrive.begin() + (size_t)r * T);
-    std::copy(q.begin(), q.begin() + T, req.begin() + (size_t)r * T);
+    std::copy(a.begin(), a.begin() + T, arrive.begin() + (size_t)i * T);
+    std::copy(q.begin(), q.begin() + T, req.begin() + (size_t)i * T);
   }
   return T;
 }
@@ -467,6 +472,10 @@ void usage() {
       "  --ring N             per-node pending capacity (power of two)\n"
       "  --trace-out FILE     write the FOGNTRC1 trace  --sca FILE / --vec FILE (replication 0)\n"
       "  --device D           HIP device (default 0)\n"
+      "  --world W --rank K --comm-id FILE   one process per GPU: rank K replays its block of the\n"
+      "                       --reps replications; the job statistics are exchanged over RCCL\n"
+      "                       (fognet_allreduce_stats) and rank 0 writes the results; FILE carries\n"
+      "                       the communicator id from rank 0 (a fresh path per run)\n"
       "  --dry-run            read the scenario and build the trace only (no GPU)\n"
       "  --show               print the resolved node and user parameters\n"
       "  --quiet              no summary on stdout");
@@ -515,6 +524,9 @@ Options parse_args(int argc, char** argv) {
     } else if (a == "--dry-run") o.dry_run = true;
     else if (a == "--quiet") o.quiet = true;
     else if (a == "--show") o.show = true;
+    else if (a == "--world") o.world = (int)parse_int(need(i), "--world");
+    else if (a == "--rank") o.rank = (int)parse_int(need(i), "--rank");
+    else if (a == "--comm-id") o.comm_id = need(i);
     else if (a == "-h" || a == "--help") {
       usage();
       std::exit(0);
@@ -522,12 +534,51 @@ Options parse_args(int argc, char** argv) {
   }
   if (o.ini.empty() == o.trace_in.empty()) die("give exactly one of -f INI and --trace FILE (--help)");
   if (o.reps <= 0) die("--reps must be > 0");
+  if (o.world < 1 || o.rank < 0 || o.rank >= o.world) die("--world / --rank: need 0 <= rank < world");
+  if (o.world > 1 && o.comm_id.empty()) die("--world > 1 needs --comm-id FILE (the communicator id's rendezvous)");
+  if (o.reps < o.world) die("--reps must be >= --world (every rank replays a block of replications)");
   return o;
 }
 
 // ---------------------------------------------------------------- runs
 
 // BrokerBaseApp3 + ComputeBrokerApp3 (the batch engine, host-buffer entry point).
+// The job record of all ranks (fognet_allreduce_stats over the library's RCCL
+// communicator); the 128-byte id goes from rank 0 to the others through the
+// file o.comm_id (written atomically, removed once every rank has joined).
+void exchange_stats(const Options& o, fognet_ctx* ctx, fognet_job_stats* job, std::vector<int64_t>& hist) {
+  uint8_t id[FOGNET_COMM_ID_BYTES];
+  if (o.rank == 0) {
+    check(fognet_comm_unique_id(id), "fognet_comm_unique_id");
+    const std::string tmp = o.comm_id + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f || std::fwrite(id, 1, sizeof id, f) != sizeof id || std::fclose(f) != 0) die("cannot write " + tmp);
+    if (std::rename(tmp.c_str(), o.comm_id.c_str()) != 0) die("cannot create " + o.comm_id);
+  } else {
+    for (int waited = 0;; waited += 50) {
+      FILE* f = std::fopen(o.comm_id.c_str(), "rb");
+      if (f) {
+        const size_t got = std::fread(id, 1, sizeof id, f);
+        std::fclose(f);
+        if (got == sizeof id) break;
+      }
+      if (waited > 300000) die("no communicator id in " + o.comm_id + " after 300 s (is rank 0 running?)");
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+  }
+  fognet_comm* comm = nullptr;
+  check_ctx(ctx, fognet_comm_create(ctx, o.world, o.rank, id, &comm), "fognet_comm_create");
+  if (o.rank == 0) std::remove(o.comm_id.c_str());  // every rank has joined
+  int64_t* d_hist = nullptr;
+  const size_t hb = hist.size() * sizeof(int64_t);
+  hip_check(hipMalloc((void**)&d_hist, hb), "hipMalloc");
+  hip_check(hipMemcpy(d_hist, hist.data(), hb, hipMemcpyHostToDevice), "hipMemcpy");
+  check_ctx(ctx, fognet_allreduce_stats(ctx, comm, job, d_hist, nullptr), "fognet_allreduce_stats");
+  hip_check(hipMemcpy(hist.data(), d_hist, hb, hipMemcpyDeviceToHost), "hipMemcpy");
+  (void)hipFree(d_hist);
+  fognet_comm_destroy(comm);
+}
+
 int run_v3(const Options& o, fognet_batch_in in, const std::string& network, const std::string& run_id) {
   const size_t RT = (size_t)in.R * (size_t)in.T;
   std::vector<int32_t> node(RT);
@@ -542,6 +593,12 @@ int run_v3(const Options& o, fognet_batch_in in, const std::string& network, con
   fognet_job_stats job;
   fognet_job_stats_init(&job);
   for (const fognet_rep_stats& s : stats) fognet_job_stats_add_rep(&job, &s);
+  const int64_t local_failed = job.n_failed;
+  if (!o.comm_id.empty()) exchange_stats(o, ctx, &job, hist);  // job + histogram of every rank
+  if (o.rank != 0) {  // rank 0 writes the results
+    fognet_destroy(ctx);
+    return local_failed ? 1 : 0;
+  }
   if (!o.sca.empty()) check(fognet_write_sca(o.sca.c_str(), run_id.c_str(), network.c_str(), &job, hist.data()), "sca");
   if (!o.vec.empty())
     check(fognet_write_vec(o.vec.c_str(), run_id.c_str(), network.c_str(), in.T, in.N, in.arrive_tick, in.dl_tick,
@@ -554,7 +611,7 @@ int run_v3(const Options& o, fognet_batch_in in, const std::string& network, con
                 job.n_started, job.n_failed, job.last_tick, job.max_pending);
     std::vector<int64_t> per(in.N, 0);
     for (int32_t k : node) ++per[k];
-    std::printf("tasks_per_node=");
+    std::printf(o.world > 1 ? "tasks_per_node(rank 0)=" : "tasks_per_node=");
     for (int k = 0; k < in.N; ++k) std::printf("%s%" PRId64, k ? "," : "", per[k]);
     std::printf("\n");
     for (int r = 0; r < in.R; ++r)
@@ -669,6 +726,7 @@ int main(int argc, char** argv) {
   const std::string run_id = o.trace_in.empty() ? o.config + "-0" : "trace-0";
 
   if (!o.trace_in.empty()) {  // replay a trace file (REF_V3 / EXT_LAT engine)
+    if (o.world > 1) die("--trace replays run on one GPU (--world 1)");
     fognet_trace_info ti;
     check(fognet_trace_info_read(o.trace_in.c_str(), &ti), "trace header");
     const size_t NR = ti.node_stride ? (size_t)ti.R : 1, RT = (size_t)ti.R * (size_t)ti.T;
@@ -710,7 +768,10 @@ int main(int argc, char** argv) {
   const int64_t user_dl = o.user_dl_set ? o.user_dl : (v2 ? -1 : o.user_dl);
   std::vector<int64_t> arrive;
   std::vector<int32_t> req;
-  const int32_t T = gen_traces(sc, o, user_dl, arrive, req);
+  // rank's contiguous block of the job's replications (the first reps % world ranks take one more)
+  const int q = o.reps / o.world, rem = o.reps % o.world;
+  const int r0 = o.rank * q + std::min(o.rank, rem), nr = q + (o.rank < rem ? 1 : 0);
+  const int32_t T = gen_traces(sc, o, user_dl, r0, nr, arrive, req);
 
   // node k: CONNECT at startTime reaches the broker after ul, the CONNACK
   // comes back after dl, the first ADVERTISEMIPS fires 0.01 s later
@@ -748,7 +809,7 @@ int main(int argc, char** argv) {
 
   std::vector<double> pb, pi;
   fognet_batch_in in{};
-  in.R = o.reps;
+  in.R = nr;
   in.T = T;
   in.N = N;
   in.policy = o.policy;
@@ -772,6 +833,9 @@ int main(int argc, char** argv) {
           "trace write");
   }
   if (o.dry_run) return 0;
-  if (v2) return run_v2(o, sc, T, arrive, req, dl, ul, first_adv, run_id);
+  if (v2) {
+    if (o.world > 1) die("BrokerBaseApp2 replays run on one GPU (--world 1)");
+    return run_v2(o, sc, T, arrive, req, dl, ul, first_adv, run_id);
+  }
   return run_v3(o, in, sc.network, run_id);
 }

@@ -152,3 +152,30 @@ def test_driver_v2_example_all_to_node0():
     out = drive("-f", INI, "-c", "Example", "--nodes", "5").stdout
     assert "local=9 forwarded=19990" in out and "failed_reps=0" in out
     assert "forwarded_per_node(rep0)=19990,0,0,0,0" in out
+
+
+def test_rank_block_of_replications(tmp_path):
+    """--world/--rank: rank k replays a contiguous block of the --reps
+    replications (the first reps % world ranks take one more), each with its
+    global glibc seed, so the job does not depend on the number of GPUs."""
+    p = str(tmp_path / "r1.fogntrc")
+    drive("-f", INI, "--users", "user[2]", "--reps", "5", "--seed", "3", "--world", "2", "--rank", "1",
+          "--comm-id", str(tmp_path / "id"), "--dry-run", "--trace-out", p)
+    tr = formats.load_trace(p)
+    assert tr["arrive"].shape[0] == 2  # replications 3 and 4
+    for i, r in enumerate((3, 4)):
+        g = formats.gen_trace_mqtt(3 + r, [200 * MS] * 2, [1500 * MS] * 2, [MS] * 2, [MS] * 2, 300 * SEC)
+        np.testing.assert_array_equal(tr["req"][i], g["req"])
+    p = drive("-f", INI, "--users", "user[2]", "--world", "2", "--dry-run", check=False)
+    assert p.returncode == 2 and "--comm-id" in p.stderr
+
+
+@pytest.mark.gpu
+def test_driver_stats_exchange_world1(ctx, tmp_path):
+    """The RCCL exchange path (fognet_allreduce_stats) at world 1 writes the
+    same .sca as the plain run, and removes the rendezvous file."""
+    a, b, cid = str(tmp_path / "a.sca"), str(tmp_path / "b.sca"), str(tmp_path / "comm.id")
+    drive("-f", INI, "--users", "user[10]", "--reps", "4", "--sca", a)
+    drive("-f", INI, "--users", "user[10]", "--reps", "4", "--sca", b, "--comm-id", cid)
+    assert open(a).read() == open(b).read()
+    assert not os.path.exists(cid)
