@@ -21,7 +21,10 @@
 //   LDS    per lane and group of 16 of its slots: earliest advert, its node,
 //          smallest view key (busy << 32 | j); the lane's minima in VGPRs.
 //          13 KiB at N = 10,000, so four replications share a CU (the loop is
-//          latency-bound: every applied advert and push waits on HBM).
+//          latency-bound: every applied advert waits on HBM).
+//   VGPRs  the record and parameters of the node the lane pushed to last
+//          (the stale view keeps choosing it), written back when the lane
+//          pushes to another node: a push issues no load.
 // Publishes are decided one at a time in trace order: adverts that reached
 // the broker strictly before the publish are applied first (lane-parallel:
 // adverts of different nodes commute, those of one node come in completion
