@@ -71,17 +71,23 @@ __host__ __device__ __forceinline__ int wide_groups(int N) {
   return ((N + kWave - 1) / kWave + kWideGroupSlots - 1) / kWideGroupSlots;
 }
 
-// Rescan group g of this lane from its view (slot `sl` replaced by the
-// values just computed: its load may have been issued before their store).
-__device__ __forceinline__ void group_scan(const WideLds& L, const WideView& V, int N, int lane, int g, int sl,
-                                           int64_t sl_nxt, uint32_t sl_busy) {
-  int64_t x[kWideGroupSlots];
-  uint32_t b[kWideGroupSlots];
+// Load group g of this lane's view (issued before the advert that changes
+// one of its slots, so these loads overlap the node-record load instead of
+// queueing behind the advert's stores: gfx9's vmcnt counts both).
+__device__ __forceinline__ void group_load(const WideView& V, int g, int64_t (&x)[kWideGroupSlots],
+                                           uint32_t (&b)[kWideGroupSlots]) {
 #pragma unroll
   for (int i = 0; i < kWideGroupSlots; ++i) {
     x[i] = V.nxt[g * kWideGroupSlots + i];
     b[i] = V.busy[g * kWideGroupSlots + i];
   }
+}
+
+// Rescan group g of this lane from its loaded view (slot `sl` replaced by the
+// values just computed: its load was issued before their store).
+__device__ __forceinline__ void group_scan(const WideLds& L, int N, int lane, int g, int sl, int64_t sl_nxt,
+                                           uint32_t sl_busy, const int64_t (&x)[kWideGroupSlots],
+                                           const uint32_t (&b)[kWideGroupSlots]) {
   int64_t mn = kNever;
   int mj = lane;
   uint64_t mk = ~0ull;
@@ -130,6 +136,10 @@ __device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn
 // h: node j's record (loaded from HBM or the lane's cached copy), updated in place.
 __device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, int64_t dl, int64_t ul,
                                              int64_t& nxt_j, uint32_t& busy_j) {
+  // the entry after the head, loaded first: for the lane's cached node h is in
+  // registers, so this load issues together with the group's view loads
+  WideEntry nx{};
+  if (h.npend >= 2) nx = e[h.hd_next];
   uint64_t c_arrived = h.hd_C;  // only the completing task itself ...
   if (arrives_before(h.tl_a, h.hd_done, dl, h.hd_S)) {
     c_arrived = h.tl_C;  // ... or everything up to the newest task (the common case)
@@ -151,7 +161,6 @@ __device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, in
   } else {
     // FIFO: the next task started at max(arrival, this completion); its
     // done tick was fixed when it was pushed
-    const WideEntry nx = e[h.hd_next];
     h.hd = h.hd_next;
     h.hd_done = nx.done;
     h.hd_C = nx.C;
@@ -273,13 +282,17 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
           int64_t nxt_j;
           uint32_t busy_j;
           const bool hit = j == cj;
+          const int g = sl / kWideGroupSlots;
+          int64_t gx[kWideGroupSlots];
+          uint32_t gb[kWideGroupSlots];
+          group_load(V, g, gx, gb);
           WideNode h = hit ? ch : nd[j];
           lerr |= !apply_advert(h, e, hit ? c_dl : A.dl[nbase + j], hit ? c_ul : A.ul[nbase + j], nxt_j, busy_j);
           if (hit) ch = h;
           else nd[j] = h;
           V.nxt[sl] = nxt_j;
           V.busy[sl] = busy_j;
-          group_scan(L, V, N, lane, sl / kWideGroupSlots, sl, nxt_j, busy_j);
+          group_scan(L, N, lane, g, sl, nxt_j, busy_j, gx, gb);
           lane_min(L, lane, mn, mj, mk);
         }
       }
