@@ -10,6 +10,6 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
 echo "smoke rc=$rc $(date +%T)"; tail -3 gpurun_out/smoke.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-3} --warmup 1 --cpu-reps ${CPU_REPS:-32} > gpurun_out/bench.log 2>&1; rc=$?
+timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-3} --warmup 1 --cpu-reps ${CPU_REPS:-1024} > gpurun_out/bench.log 2>&1; rc=$?
 echo "bench rc=$rc $(date +%T)"; tail -3 gpurun_out/bench.log
 exit $rc
