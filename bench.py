@@ -202,7 +202,8 @@ def main():
     achieved_gbs = R * T * bpd / replay_avg_s / 1e9
 
     traffic = None
-    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json" if args.workload == "c3" else
+                        f"pmc_traffic_{args.workload}.json")
     if os.path.exists(prof):
         try:
             pj = json.load(open(prof))

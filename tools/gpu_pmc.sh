@@ -1,9 +1,14 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run, no tracing domains mixed in)
-# over the default C3 bench workload, one timed step.
+# over one timed step of the bench workload: C3 (default) or WORKLOAD=c5.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/pmc
+if [ "${WORKLOAD:-c3}" = c5 ]; then
+  BARGS="--workload c5"; KERNEL=replay_wide_kernel; DEC=10240000; OUT=pmc_traffic_c5.json; CFG=1024,10000,10000
+else
+  BARGS=""; KERNEL=replay_kernel; DEC=409600000; OUT=pmc_traffic.json; CFG=4096,100000,256
+fi
 export TMPDIR=/tmp
 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
 i=0
@@ -12,8 +17,8 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_W
            "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc/p$i -o p$i -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu > gpurun_out/pmc/p$i.log 2>&1; rc=$?
+    python3 bench.py $BARGS --steps 1 --warmup 0 --no-cpu > gpurun_out/pmc/p$i.log 2>&1; rc=$?
   echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/p$i.log; exit $rc; fi
 done
-python3 tools/pmc_summary.py replay_kernel 409600000 gpurun_out/pmc/pmc_traffic.json 2048 > /dev/null
+python3 tools/pmc_summary.py $KERNEL $DEC gpurun_out/pmc/$OUT 2048 $CFG > /dev/null

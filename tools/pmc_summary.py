@@ -40,9 +40,10 @@ def main():
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
             if k in per:
                 out[k + "_frac_of_wave_cycles"] = per[k] / per["SQ_WAVE_CYCLES"]
-    # the record bench.py reads (profiles/pmc_traffic.json): C3 default config
+    # the record bench.py reads (profiles/pmc_traffic[_c5].json): argv[5] = "R,T,N" (default C3)
     if "hbm_bytes_per_launch" in out:
-        out["config"] = {"R": 4096, "T": 100000, "N": 256, "ring": int(sys.argv[4]) if len(sys.argv) > 4 else 2048}
+        R, T, N = (int(x) for x in sys.argv[5].split(",")) if len(sys.argv) > 5 else (4096, 100000, 256)
+        out["config"] = {"R": R, "T": T, "N": N, "ring": int(sys.argv[4]) if len(sys.argv) > 4 else 2048}
         out["replay_hbm_bytes_per_launch"] = out["hbm_bytes_per_launch"]
     txt = json.dumps(out, indent=1)
     print(txt)
