@@ -25,7 +25,7 @@ $(OBJDIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 
 $(OBJDIR)/io.o: $(SRC_DIR)/io.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HOSTCXX) -O2 -std=c++17 -fPIC -Wall -Iinclude -c $< -o $@
+	$(HOSTCXX) -O2 -std=c++17 -fPIC -Wall -ffp-contract=off -Iinclude -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)

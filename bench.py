@@ -76,7 +76,8 @@ def main():
     ap.add_argument("--ring", type=int, default=2048)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0003)
     ap.add_argument("--cpu-reps", type=int, default=1024, help="replications in the CPU-baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this job may use")
+    ap.add_argument("--cpu-reps-1t", type=int, default=16, help="replications of the single-thread CPU sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--policy", default="REF_V3", choices=("REF_V3", "EXT_LAT"))
     ap.add_argument("--workload", default="c3", choices=("c1", "c3", "c4", "c5"))
@@ -214,7 +215,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(trace, args, R, T, N)
+        cpu = cpu_baseline(trace, args, R, T, N, out=out)
 
     if rank == 0:
         line = {
@@ -435,7 +436,7 @@ def bench_c1(args, ctx, dev, dist, world, rank):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
         reps = min(R, 1024)  # ~10-30 s of single-core work in total
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        threads = host_cpu_info()[3] if args.cpu_threads <= 0 else args.cpu_threads
         t1 = time.perf_counter()
         o = oracle_lib.run_v2(arrive[:reps], req[:reps], 1000, np.full(n_nodes, 1000, np.int32), np.full(n_nodes, MS),
                               np.full(n_nodes, MS), np.full(n_nodes, 20 * MS), stop, 0.01, threads=threads)
@@ -467,40 +468,65 @@ def bench_c1(args, ctx, dev, dist, world, rank):
         dist.destroy_process_group()
 
 
-def cpu_baseline(trace, args, R, T, N):
+def host_cpu_info():
+    """CPU model, host logical CPUs, and the CPUs this process may run on (the
+    GPU box allots each GPU's job a share of the host: its affinity mask, or
+    OMP_NUM_THREADS when the mask shows the whole host)."""
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    cores = min(avail, share) if share > 0 else avail
+    return model, nproc, avail, cores
+
+
+def cpu_baseline(trace, args, R, T, N, out=None):
     """Oracle (tests/oracle_lib: the CPU restatement, kind "port") timed on this
-    host on a bounded sample of the same workload."""
+    host on a bounded sample of the same workload: on every core this job may
+    use (one replication per thread) and on 1 thread over >= 16 replications.
+    With ``out`` (the device outputs of the timed steps) the oracle's outputs on
+    the sample are compared with the device's: ``parity``."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
 
     reps = min(args.cpu_reps, R)
     h = {k: trace[k][:reps].cpu().numpy() for k in ("arrive", "req", "mips", "dl", "ul", "init")}
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    log(f"cpu baseline: {reps} replications on {threads} threads ...")
+    model, nproc, avail, cores = host_cpu_info()
+    threads = max(1, min(args.cpu_threads, cores)) if args.cpu_threads > 0 else cores
+    log(f"cpu baseline: {reps} replications on {threads} threads (host {nproc} CPUs, {avail} in this job's mask) ...")
     t0 = time.perf_counter()
     o = oracle_lib.run_batch(h["arrive"], h["req"], h["mips"], h["dl"], h["ul"], h["init"], threads=threads,
                              outputs=True)
     dt = time.perf_counter() - t0
     ok = int((o["stats"]["status"] == 0).sum())
-    # single-thread rate on 4 replications of the sample
+    parity = None
+    if out is not None:
+        parity = bool(np.array_equal(o["node"], out.node[:reps].cpu().numpy())
+                      and np.array_equal(o["status"], out.status[:reps].cpu().numpy())
+                      and np.array_equal(o["start"], out.start_tick[:reps].cpu().numpy())
+                      and np.array_equal(o["done"], out.done_tick[:reps].cpu().numpy())
+                      and o["stats"].tobytes() == out.stats[: reps * _abi.REP_STATS_DTYPE.itemsize].cpu().numpy().tobytes())
+    del o
+    s1 = min(max(16, args.cpu_reps_1t), reps)
     t1 = time.perf_counter()
-    s4 = min(4, reps)
-    oracle_lib.run_batch(h["arrive"][:s4], h["req"][:s4], h["mips"][:s4], h["dl"][:s4], h["ul"][:s4], h["init"][:s4],
-                         threads=1)
+    oracle_lib.run_batch(h["arrive"][:s1], h["req"][:s1], h["mips"][:s1], h["dl"][:s1], h["ul"][:s1], h["init"][:s1],
+                         threads=1, outputs=False)
     dt1 = time.perf_counter() - t1
-    cpu_model = ""
-    try:
-        for ln in open("/proc/cpuinfo"):
-            if ln.startswith("model name"):
-                cpu_model = ln.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
     return {"value": reps * T / dt, "unit": "decisions/s", "cores": threads, "kind": "port",
             "sample": f"{reps} replications x {T} tasks x {N} nodes (rank 0's first replications of the same "
                       f"trace), one replication per thread, {ok}/{reps} completed",
-            "wall_s": dt, "single_thread_value": s4 * T / dt1, "host_cpu": cpu_model,
-            "host_nproc": os.cpu_count()}
+            "wall_s": dt, "single_thread_value": s1 * T / dt1, "single_thread_sample": f"{s1} replications",
+            "single_thread_wall_s": dt1, "host_cpu": model, "host_nproc": nproc, "job_cpus": avail,
+            "parity": parity,
+            "parity_sample": f"oracle vs device outputs (node, status, start, done, stats record) on the {reps} "
+                             f"replications"}
 
 
 if __name__ == "__main__":

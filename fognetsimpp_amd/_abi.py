@@ -30,7 +30,7 @@ FOGNET_POLICY_EXT_LAT = 16
 TICKS_PER_SECOND = 10**12
 # fognet_v2_action (BrokerBaseApp2 decision outcome)
 V2_LOCAL, V2_FORWARD, V2_DROPPED, V2_NO_NODES = 3, 4, 5, 6
-ABI_VERSION = 6
+ABI_VERSION = 7
 HIST_METRICS = 2  # 0 queueTime, 1 response
 HIST_BINS = 64
 COMM_ID_BYTES = 128  # FOGNET_COMM_ID_BYTES
@@ -40,7 +40,7 @@ class RepStats(C.Structure):
     _fields_ = [
         ("n_tasks", C.c_int64), ("n_queued", C.c_int64), ("n_started", C.c_int64),
         ("last_tick", C.c_int64),
-        ("queue_min_ticks", C.c_int64), ("queue_max_ticks", C.c_int64),
+        ("queue_min_raw", C.c_int64), ("queue_max_raw", C.c_int64),
         ("resp_min_ticks", C.c_int64), ("resp_max_ticks", C.c_int64),
         ("queue_sum_lo", C.c_uint64), ("queue_sum_hi", C.c_uint64),
         ("queue_sq_lo", C.c_uint64), ("queue_sq_hi", C.c_uint64),
@@ -48,6 +48,7 @@ class RepStats(C.Structure):
         ("resp_sq_lo", C.c_uint64), ("resp_sq_hi", C.c_uint64),
         ("events", C.c_int64), ("max_pending", C.c_int32), ("status", C.c_int32),
         ("busy_s", C.c_int64), ("energy_j", C.c_double),
+        ("queue_sq_top", C.c_uint64), ("n_qtime", C.c_int64), ("n_qtime_overflow", C.c_int64),
     ]
 
 
@@ -73,12 +74,13 @@ class JobStats(C.Structure):
         ("n_reps", C.c_int64), ("n_failed", C.c_int64),
         ("n_tasks", C.c_int64), ("n_queued", C.c_int64), ("n_started", C.c_int64),
         ("last_tick", C.c_int64),
-        ("queue_min_ticks", C.c_int64), ("queue_max_ticks", C.c_int64),
+        ("queue_min_raw", C.c_int64), ("queue_max_raw", C.c_int64),
         ("resp_min_ticks", C.c_int64), ("resp_max_ticks", C.c_int64),
         ("queue_sum", C.c_uint64 * 3), ("queue_sq", C.c_uint64 * 3),
         ("resp_sum", C.c_uint64 * 3), ("resp_sq", C.c_uint64 * 3),
         ("events", C.c_int64), ("max_pending", C.c_int64),
         ("busy_s", C.c_int64), ("energy_j", C.c_double),
+        ("n_qtime", C.c_int64), ("n_qtime_overflow", C.c_int64),
     ]
 
 
@@ -86,9 +88,9 @@ JOB_STATS_DTYPE = _np_dtype(JobStats)
 
 
 class Moments(C.Structure):
-    _fields_ = [("count", C.c_int64), ("min_ticks", C.c_int64), ("max_ticks", C.c_int64),
+    _fields_ = [("count", C.c_int64), ("min_raw", C.c_int64), ("max_raw", C.c_int64),
                 ("sum_lo", C.c_uint64), ("sum_hi", C.c_uint64), ("sq_lo", C.c_uint64), ("sq_hi", C.c_uint64),
-                ("pad", C.c_int64)]
+                ("sq_top", C.c_uint64), ("overflow", C.c_int64)]
 
 
 USER_SIGNALS = ("delay", "latency", "latencyH1", "taskTime")

@@ -457,8 +457,8 @@ int fognet_reduce_stats_dev(fognet_ctx* c, const fognet_rep_stats* stats, int32_
 void fognet_job_stats_init(fognet_job_stats* s) {
   if (!s) return;
   memset(s, 0, sizeof *s);
-  s->queue_min_ticks = s->resp_min_ticks = INT64_MAX;
-  s->queue_max_ticks = s->resp_max_ticks = s->last_tick = INT64_MIN;
+  s->queue_min_raw = s->resp_min_ticks = INT64_MAX;
+  s->queue_max_raw = s->resp_max_ticks = s->last_tick = INT64_MIN;
 }
 
 static void add192_host(uint64_t* a, const uint64_t* b) {
@@ -478,8 +478,10 @@ void fognet_job_stats_merge(fognet_job_stats* a, const fognet_job_stats* b) {
   a->n_started += b->n_started;
   a->events += b->events;
   if (b->last_tick > a->last_tick) a->last_tick = b->last_tick;
-  if (b->queue_min_ticks < a->queue_min_ticks) a->queue_min_ticks = b->queue_min_ticks;
-  if (b->queue_max_ticks > a->queue_max_ticks) a->queue_max_ticks = b->queue_max_ticks;
+  if (b->queue_min_raw < a->queue_min_raw) a->queue_min_raw = b->queue_min_raw;
+  if (b->queue_max_raw > a->queue_max_raw) a->queue_max_raw = b->queue_max_raw;
+  a->n_qtime += b->n_qtime;
+  a->n_qtime_overflow += b->n_qtime_overflow;
   if (b->resp_min_ticks < a->resp_min_ticks) a->resp_min_ticks = b->resp_min_ticks;
   if (b->resp_max_ticks > a->resp_max_ticks) a->resp_max_ticks = b->resp_max_ticks;
   if (b->max_pending > a->max_pending) a->max_pending = b->max_pending;
@@ -505,8 +507,10 @@ void fognet_job_stats_add_rep(fognet_job_stats* a, const fognet_rep_stats* s) {
   b.n_started = s->n_started;
   b.events = s->events;
   b.last_tick = s->last_tick;
-  b.queue_min_ticks = s->queue_min_ticks;
-  b.queue_max_ticks = s->queue_max_ticks;
+  b.queue_min_raw = s->queue_min_raw;
+  b.queue_max_raw = s->queue_max_raw;
+  b.n_qtime = s->n_qtime;
+  b.n_qtime_overflow = s->n_qtime_overflow;
   b.resp_min_ticks = s->resp_min_ticks;
   b.resp_max_ticks = s->resp_max_ticks;
   b.max_pending = s->max_pending;
@@ -514,8 +518,10 @@ void fognet_job_stats_add_rep(fognet_job_stats* a, const fognet_rep_stats* s) {
   b.energy_j = s->energy_j;
   b.queue_sum[0] = s->queue_sum_lo;
   b.queue_sum[1] = s->queue_sum_hi;
+  b.queue_sum[2] = (int64_t)s->queue_sum_hi < 0 ? ~(uint64_t)0 : 0;  // two's complement sign extension
   b.queue_sq[0] = s->queue_sq_lo;
   b.queue_sq[1] = s->queue_sq_hi;
+  b.queue_sq[2] = s->queue_sq_top;
   b.resp_sum[0] = s->resp_sum_lo;
   b.resp_sum[1] = s->resp_sum_hi;
   b.resp_sq[0] = s->resp_sq_lo;

@@ -147,32 +147,60 @@ struct Moments {
   double mean, stddev, sum, sqrsum, min, max;  // ms
 };
 
-// count/mean/stddev/sum/sqrsum/min/max in ms of values in ticks given by
-// their exact sum S and sum of squares Q (cStdDev's fields, unbiased stddev).
-Moments moments(int64_t n, const uint64_t* S, const uint64_t* Q, int64_t mn, int64_t mx) {
+// count/mean/stddev/sum/sqrsum/min/max in ms of integer values given by their
+// exact sum S (192-bit, two's complement if `sgn`) and sum of squares Q
+// (cStdDev's fields, unbiased stddev).  ms_per_unit: 1e-9 for tick values,
+// 1e-12 for raw emitted ms signals (the recorded value is raw * 1e-12, dbl()).
+Moments moments(int64_t n, const uint64_t* S, const uint64_t* Q, int64_t mn, int64_t mx, bool sgn,
+                bool raw_units) {
   Moments m;
   m.count = n;
-  const long double s = big_ld(big_of(S, 3)), q = big_ld(big_of(Q, 3));
-  m.sum = (double)(s / 1e9L);
-  m.sqrsum = (double)(q / 1e18L);
+  Big sa = big_of(S, 3);
+  bool neg = false;
+  if (sgn && (int64_t)S[2] < 0) {  // |S| by two's complement negation
+    neg = true;
+    const Big zero;
+    Big ext = sa;
+    for (int i = 3; i < 7; ++i) ext.l[i] = ~(uint64_t)0;
+    sa = big_sub(zero, ext);
+  }
+  const long double unit = raw_units ? 1e-12L : 1e-9L;
+  const long double s = (neg ? -1.0L : 1.0L) * big_ld(sa), q = big_ld(big_of(Q, 3));
+  m.sum = (double)(s * unit);
+  m.sqrsum = (double)(q * unit * unit);
   if (n == 0) {
     m.mean = m.stddev = m.min = m.max = NAN;
     return m;
   }
-  m.mean = (double)(s / (long double)n / 1e9L);
-  m.min = (double)mn / 1e9;
-  m.max = (double)mx / 1e9;
+  m.mean = (double)(s / (long double)n * unit);
+  m.min = raw_units ? (double)mn * 1e-12 : (double)mn / 1e9;  // raw: exactly the recorded dbl()
+  m.max = raw_units ? (double)mx * 1e-12 : (double)mx / 1e9;
   if (n < 2) {
     m.stddev = NAN;  // cStdDev: variance undefined for a single value
     return m;
   }
   const uint64_t nn[1] = {(uint64_t)n};
   const Big nq = big_mul(big_of(nn, 1), big_of(Q, 3));
-  const Big s2 = big_mul(big_of(S, 3), big_of(S, 3));
+  const Big s2 = big_mul(sa, sa);
   const long double num = big_ge(nq, s2) ? big_ld(big_sub(nq, s2)) : 0.0L;
   const long double var = num / ((long double)n * (long double)(n - 1));
-  m.stddev = (double)(sqrtl(var) / 1e9L);
+  m.stddev = (double)(sqrtl(var) * unit);
   return m;
+}
+
+// OMNeT++ 4.6 SimTime::toInt64 and the queueTime emission (replay_common.h
+// qtime_raw, the host twin; x86-64 SSE2 doubles, no contraction).
+bool simtime_to_int64(double x, int64_t* out) {
+  const double f = floor(x + 0.5);
+  if (!(fabs(f) < 9223372036854775808.0)) return false;
+  *out = (int64_t)f;
+  return true;
+}
+
+bool qtime_raw(int64_t now, int64_t a, int64_t* raw) {
+  int64_t qs = 0;
+  simtime_to_int64(1e12 * ((double)a * 1e-12), &qs);
+  return simtime_to_int64((double)(now - qs) * 1000.0, raw);
 }
 
 // OMNeT++ number formatting (%.14g; NaN printed as "-nan" like cStdDev's 0/0).
@@ -416,8 +444,10 @@ int fognet_write_sca(const char* path, const char* run_id, const char* network, 
   fprintf(f, "scalar %s \t\"energy J\" \t%s\n", nodes.c_str(), num(job->energy_j).c_str());
   fprintf(f, "scalar %s \t\"makespan s\" \t%s\n", nodes.c_str(),
           job->n_tasks > 0 ? simtime_str(job->last_tick).c_str() : "-nan");
-  const Moments q = moments(job->n_queued, job->queue_sum, job->queue_sq, job->queue_min_ticks, job->queue_max_ticks);
-  const Moments r = moments(job->n_tasks, job->resp_sum, job->resp_sq, job->resp_min_ticks, job->resp_max_ticks);
+  fprintf(f, "scalar %s \t\"queueTime simtime overflows\" \t%lld\n", nodes.c_str(), (long long)job->n_qtime_overflow);
+  const Moments q = moments(job->n_qtime, job->queue_sum, job->queue_sq, job->queue_min_raw, job->queue_max_raw, true, true);
+  const Moments r = moments(job->n_tasks, job->resp_sum, job->resp_sq, job->resp_min_ticks, job->resp_max_ticks, false,
+                            false);
   statistic(f, nodes, "queueTime", "stats", q);
   stat_attrs(f, "queueTime", "stats");
   statistic(f, broker, "response", "stats", r);
@@ -467,8 +497,9 @@ int fognet_write_vec(const char* path, const char* run_id, const char* network, 
     if (status[i] == 4) per[node[i]].push_back(i);
   for (int32_t j = 0; j < N; ++j)
     for (int32_t i : per[j]) {
-      const int64_t q = start_tick[i] - (arrive_tick[i] + dl_tick[j]);
-      fprintf(f, "%d\t%s\t%s\n", 1 + j, simtime_str(start_tick[i]).c_str(), num((double)q / 1e9).c_str());
+      int64_t raw;  // the value ComputeBrokerApp3.cc:238 emits (fognet_hip.h "Reference signal values")
+      if (!qtime_raw(start_tick[i], arrive_tick[i] + dl_tick[j], &raw)) continue;  // the reference throws
+      fprintf(f, "%d\t%s\t%s\n", 1 + j, simtime_str(start_tick[i]).c_str(), num((double)raw * 1e-12).c_str());
     }
   const bool ok = ferror(f) == 0;
   return (fclose(f) == 0 && ok) ? FOGNET_OK : fail(FOGNET_ERR_ARG, std::string("write_vec: write failed: ") + path);

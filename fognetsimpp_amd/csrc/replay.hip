@@ -517,13 +517,10 @@ __device__ __forceinline__ void stats_accumulate(const ReplayArgs& A, size_t tba
         a.rmin = min(a.rmin, resp);
         a.rmax = max(a.rmax, resp);
         if (hist) atomicAdd(&s_hist[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
-        if (stt[u] == 4u) {
-          const int64_t q = st0[u] - (t[u] + dl_of(k));
+        if (stt[u] == 4u) {  // queueTime emission (ComputeBrokerApp3.cc:238), enqueued at its arrival
           a.n4 += 1u;
-          add_moment(a.qs_lo, a.qs_hi, a.qq_lo, a.qq_hi, (uint64_t)q);
-          a.qmin = min(a.qmin, q);
-          a.qmax = max(a.qmax, q);
-          if (hist) atomicAdd(&s_hist[hist_bin(q)], 1u);
+          acc_qtime(a.qs_lo, a.qs_hi, a.qq_lo, a.qq_hi, a.qq_top, a.qmin, a.qmax, a.nqt, a.nqo, st0[u],
+                    t[u] + dl_of(k), hist ? s_hist : nullptr);
         } else {
           a.n5 += 1u;
         }
@@ -964,8 +961,8 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     S->n_queued = p_t[0];
     S->n_started = p_t[1];
     S->last_tick = p_t[2];
-    S->queue_min_ticks = p_t[3];
-    S->queue_max_ticks = p_t[4];
+    S->queue_min_raw = p_t[3];
+    S->queue_max_raw = p_t[4];
     S->resp_min_ticks = p_t[5];
     S->resp_max_ticks = p_t[6];
     S->queue_sum_lo = p_t[7];
@@ -977,8 +974,8 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     S->n_queued = p_iter;
     S->n_started = p_advit;
     S->last_tick = p_adv;
-    S->queue_min_ticks = p_scan;
-    S->queue_max_ticks = p_end_k;
+    S->queue_min_raw = p_scan;
+    S->queue_max_raw = p_end_k;
     S->resp_min_ticks = p_hz;
     S->resp_max_ticks = p_refill;
     S->queue_sum_lo = p_w0;

@@ -43,16 +43,57 @@ __device__ __forceinline__ double add_rn(double a, double b) {
   return a + b;
 }
 
+// ---------------------------------------------------------------- OMNeT++ SimTime
+// The reference's signal arithmetic on simtime_t (OMNeT++ 4.6, scale 1e-12;
+// fognet_hip.h "Reference signal values"): dbl() = t * 1e-12, SimTime(double)
+// and SimTime * double round with toInt64(x) = floor(x + 0.5) and throw
+// outside the int64 range.  Every double operation is separately rounded.
+
+__device__ __forceinline__ double simtime_dbl(int64_t t) { return mul_rn((double)t, 1e-12); }
+
+// SimTime::toInt64; false where the reference throws cRuntimeError
+__device__ __forceinline__ bool simtime_to_int64(double x, int64_t& out) {
+  const double f = floor(add_rn(x, 0.5));
+  const bool ok = fabs(f) < 0x1p63;
+  out = ok ? (int64_t)f : 0;
+  return ok;
+}
+
+// queueTime (ComputeBrokerApp3.cc:238, 306): the raw simtime_t of
+// (simTime() - SimTime(queueStartTime)) * 1000 for a task enqueued at tick a
+// (queueStartTime = simTime().dbl()) that starts at tick now.
+__device__ __forceinline__ bool qtime_raw(int64_t now, int64_t a, int64_t& raw) {
+  int64_t qs;
+  simtime_to_int64(mul_rn(1e12, simtime_dbl(a)), qs);  // a < 2^61: in range
+  return simtime_to_int64(mul_rn((double)(now - qs), 1000.0), raw);
+}
+
+// (simTime() - t0) * 1000 with t0 a simtime_t (mqttApp2.cc:260,272,282)
+__device__ __forceinline__ bool ms_raw(int64_t d, int64_t& raw) {
+  return simtime_to_int64(mul_rn((double)d, 1000.0), raw);
+}
+
+// histogram bin of a raw ms signal: whole part of the recorded double (ms)
+__device__ __forceinline__ int hist_bin_raw(int64_t raw) {
+  const double v = simtime_dbl(raw);
+  if (!(v >= 1.0)) return 0;
+  const uint64_t q = (uint64_t)v;
+  const int b = 64 - __clzll((long long)q);
+  return b > FOGNET_HIST_BINS - 1 ? FOGNET_HIST_BINS - 1 : b;
+}
+
 // ---------------------------------------------------------------- statistics
 // Exact per-replication statistics: queueTime (ComputeBrokerApp3.cc:238) over
-// queued tasks, response (done - publish arrival) over all tasks.  128-bit
-// integer sums are bit-identical for any summation order, so every kernel that
-// accumulates them writes the same record.
+// queued tasks as the raw values the reference emits, response (done -
+// publish arrival, ticks) over all tasks.  Integer sums are bit-identical for
+// any summation order, so every kernel that accumulates them writes the same
+// record.
 
 struct Acc {
   uint64_t n4, n5, busy;
-  uint64_t qs_lo, qs_hi, qq_lo, qq_hi, rs_lo, rs_hi, rq_lo, rq_hi;
+  uint64_t qs_lo, qs_hi, qq_lo, qq_hi, qq_top, rs_lo, rs_hi, rq_lo, rq_hi;
   int64_t qmin, qmax, rmin, rmax, last;
+  uint64_t nqt, nqo;  // queueTime emissions in the moments / lost to simtime overflow
 };
 
 // Unsigned 32-bit division by a per-node constant (the node's MIPS) as a
@@ -93,12 +134,53 @@ __device__ __forceinline__ void add_moment(uint64_t& slo, uint64_t& shi, uint64_
   add128(qlo, qhi, v * v, __umul64hi(v, v));
 }
 
+// 192-bit a += (b_lo, b_hi, b_top)
+__device__ __forceinline__ void add192(uint64_t& lo, uint64_t& hi, uint64_t& top, uint64_t blo, uint64_t bhi,
+                                       uint64_t btop) {
+  const uint64_t o = lo;
+  lo += blo;
+  const uint64_t c0 = lo < o ? 1u : 0u;
+  const uint64_t h0 = hi;
+  hi += bhi;
+  uint64_t c1 = hi < h0 ? 1u : 0u;
+  const uint64_t h1 = hi;
+  hi += c0;
+  c1 += hi < h1 ? 1u : 0u;
+  top += btop + c1;
+}
+
+// signed value: two's complement 128-bit sum, 192-bit sum of squares
+__device__ __forceinline__ void add_moment_signed(uint64_t& slo, uint64_t& shi, uint64_t& qlo, uint64_t& qhi,
+                                                  uint64_t& qtop, int64_t v) {
+  const uint64_t m = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+  add128(slo, shi, (uint64_t)v, v < 0 ? ~(uint64_t)0 : 0u);
+  add192(qlo, qhi, qtop, m * m, __umul64hi(m, m), 0u);
+}
+
+// one queueTime emission of a task enqueued at tick a, started at tick start
+__device__ __forceinline__ void acc_qtime(uint64_t& qs_lo, uint64_t& qs_hi, uint64_t& qq_lo, uint64_t& qq_hi,
+                                          uint64_t& qq_top, int64_t& qmin, int64_t& qmax, uint64_t& nqt,
+                                          uint64_t& nqo, int64_t start, int64_t a, uint32_t* hist) {
+  int64_t raw;
+  if (qtime_raw(start, a, raw)) {
+    add_moment_signed(qs_lo, qs_hi, qq_lo, qq_hi, qq_top, raw);
+    qmin = min(qmin, raw);
+    qmax = max(qmax, raw);
+    nqt += 1u;
+    if (hist) atomicAdd(&hist[hist_bin_raw(raw)], 1u);
+  } else {
+    nqo += 1u;
+  }
+}
+
 __device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
   a.n4 += b.n4;
   a.n5 += b.n5;
   a.busy += b.busy;
+  a.nqt += b.nqt;
+  a.nqo += b.nqo;
   add128(a.qs_lo, a.qs_hi, b.qs_lo, b.qs_hi);
-  add128(a.qq_lo, a.qq_hi, b.qq_lo, b.qq_hi);
+  add192(a.qq_lo, a.qq_hi, a.qq_top, b.qq_lo, b.qq_hi, b.qq_top);
   add128(a.rs_lo, a.rs_hi, b.rs_lo, b.rs_hi);
   add128(a.rq_lo, a.rq_hi, b.rq_lo, b.rq_hi);
   a.qmin = min(a.qmin, b.qmin);
@@ -109,9 +191,10 @@ __device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
 }
 
 // One task's contribution: response = done - publish tick t; queued tasks
-// (status 4) also their queueTime = start - arrival at the node a.
+// (status 4) also their queueTime emission (enqueued at arrival a, started at
+// start).  hist: the queueTime histogram row (nullable).
 __device__ __forceinline__ void acc_task(Acc& acc, int64_t t, int64_t a, int64_t start, int64_t done, uint32_t S,
-                                         uint32_t status) {
+                                         uint32_t status, uint32_t* hist) {
   acc.busy += S;
   const int64_t resp = done - t;
   add_moment(acc.rs_lo, acc.rs_hi, acc.rq_lo, acc.rq_hi, (uint64_t)resp);
@@ -119,11 +202,9 @@ __device__ __forceinline__ void acc_task(Acc& acc, int64_t t, int64_t a, int64_t
   acc.rmax = max(acc.rmax, resp);
   acc.last = max(acc.last, done);
   if (status == 4u) {
-    const int64_t q = start - a;
     acc.n4 += 1u;
-    add_moment(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, (uint64_t)q);
-    acc.qmin = min(acc.qmin, q);
-    acc.qmax = max(acc.qmax, q);
+    acc_qtime(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, acc.qq_top, acc.qmin, acc.qmax, acc.nqt, acc.nqo, start, a,
+              hist);
   } else {
     acc.n5 += 1u;
   }
@@ -147,6 +228,9 @@ __device__ __forceinline__ Acc wave_merge(Acc a) {
     b.qs_hi = shfl_xor_u64(a.qs_hi, m);
     b.qq_lo = shfl_xor_u64(a.qq_lo, m);
     b.qq_hi = shfl_xor_u64(a.qq_hi, m);
+    b.qq_top = shfl_xor_u64(a.qq_top, m);
+    b.nqt = shfl_xor_u64(a.nqt, m);
+    b.nqo = shfl_xor_u64(a.nqo, m);
     b.rs_lo = shfl_xor_u64(a.rs_lo, m);
     b.rs_hi = shfl_xor_u64(a.rs_hi, m);
     b.rq_lo = shfl_xor_u64(a.rq_lo, m);
@@ -165,8 +249,8 @@ __device__ __forceinline__ void write_rep_stats(fognet_rep_stats* S, const Acc& 
   S->n_queued = (int64_t)b.n4;
   S->n_started = (int64_t)b.n5;
   S->last_tick = b.last;
-  S->queue_min_ticks = b.qmin;
-  S->queue_max_ticks = b.qmax;
+  S->queue_min_raw = b.qmin;
+  S->queue_max_raw = b.qmax;
   S->resp_min_ticks = b.rmin;
   S->resp_max_ticks = b.rmax;
   S->queue_sum_lo = b.qs_lo;
@@ -179,6 +263,9 @@ __device__ __forceinline__ void write_rep_stats(fognet_rep_stats* S, const Acc& 
   S->resp_sq_hi = b.rq_hi;
   S->busy_s = (int64_t)b.busy;
   S->energy_j = 0.0;
+  S->queue_sq_top = b.qq_top;
+  S->n_qtime = (int64_t)b.nqt;
+  S->n_qtime_overflow = (int64_t)b.nqo;
 }
 
 }  // namespace fognet

@@ -400,11 +400,8 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
           A.out_start[o] = start == kNever ? -1 : start;
           A.out_done[o] = done == kNever ? -1 : done;
           if (done != kNever) {
-            acc_task(acc, t, a, start, done, S, status);
-            if (hist) {
-              atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - t)], 1u);
-              if (status == 4u) atomicAdd(&L.hist[hist_bin(start - a)], 1u);
-            }
+            acc_task(acc, t, a, start, done, S, status, hist ? L.hist : nullptr);
+            if (hist) atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - t)], 1u);
           } else {
             // node-down: acked at arrival (status 4/5) or lost; a queued task that
             // started before the crash still emitted its queueTime (:238)
@@ -412,13 +409,9 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
             if (status == 5u) acc.n5 += 1u;
             if (status == 4u) {
               acc.n4 += 1u;
-              if (start != kNever) {
-                const int64_t q = start - a;
-                add_moment(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, (uint64_t)q);
-                acc.qmin = min(acc.qmin, q);
-                acc.qmax = max(acc.qmax, q);
-                if (hist) atomicAdd(&L.hist[hist_bin(q)], 1u);
-              }
+              if (start != kNever)
+                acc_qtime(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, acc.qq_top, acc.qmin, acc.qmax, acc.nqt,
+                          acc.nqo, start, a, hist ? L.hist : nullptr);
             }
           }
         }

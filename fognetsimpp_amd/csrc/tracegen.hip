@@ -112,8 +112,8 @@ __device__ __forceinline__ void add192(uint64_t* a, uint64_t lo, uint64_t mid, u
 
 __device__ __forceinline__ void job_init(fognet_job_stats& j) {
   j = fognet_job_stats{};
-  j.queue_min_ticks = j.resp_min_ticks = INT64_MAX;
-  j.queue_max_ticks = j.resp_max_ticks = j.last_tick = INT64_MIN;
+  j.queue_min_raw = j.resp_min_ticks = INT64_MAX;
+  j.queue_max_raw = j.resp_max_ticks = j.last_tick = INT64_MIN;
 }
 
 __device__ __forceinline__ void job_merge(fognet_job_stats& a, const fognet_job_stats& b) {
@@ -124,8 +124,10 @@ __device__ __forceinline__ void job_merge(fognet_job_stats& a, const fognet_job_
   a.n_started += b.n_started;
   a.events += b.events;
   a.last_tick = max(a.last_tick, b.last_tick);
-  a.queue_min_ticks = min(a.queue_min_ticks, b.queue_min_ticks);
-  a.queue_max_ticks = max(a.queue_max_ticks, b.queue_max_ticks);
+  a.queue_min_raw = min(a.queue_min_raw, b.queue_min_raw);
+  a.queue_max_raw = max(a.queue_max_raw, b.queue_max_raw);
+  a.n_qtime += b.n_qtime;
+  a.n_qtime_overflow += b.n_qtime_overflow;
   a.resp_min_ticks = min(a.resp_min_ticks, b.resp_min_ticks);
   a.resp_max_ticks = max(a.resp_max_ticks, b.resp_max_ticks);
   a.max_pending = max(a.max_pending, b.max_pending);
@@ -154,15 +156,17 @@ __global__ __launch_bounds__(kRedThreads) void reduce_kernel(const fognet_rep_st
     a.n_started += s.n_started;
     a.events += s.events;
     a.last_tick = max(a.last_tick, s.last_tick);
-    a.queue_min_ticks = min(a.queue_min_ticks, s.queue_min_ticks);
-    a.queue_max_ticks = max(a.queue_max_ticks, s.queue_max_ticks);
+    a.queue_min_raw = min(a.queue_min_raw, s.queue_min_raw);
+    a.queue_max_raw = max(a.queue_max_raw, s.queue_max_raw);
+    a.n_qtime += s.n_qtime;
+    a.n_qtime_overflow += s.n_qtime_overflow;
     a.resp_min_ticks = min(a.resp_min_ticks, s.resp_min_ticks);
     a.resp_max_ticks = max(a.resp_max_ticks, s.resp_max_ticks);
     a.max_pending = max(a.max_pending, (int64_t)s.max_pending);
     a.busy_s += s.busy_s;
     a.energy_j = __dadd_rn(a.energy_j, s.energy_j);
-    add192(a.queue_sum, s.queue_sum_lo, s.queue_sum_hi, 0u);
-    add192(a.queue_sq, s.queue_sq_lo, s.queue_sq_hi, 0u);
+    add192(a.queue_sum, s.queue_sum_lo, s.queue_sum_hi, (int64_t)s.queue_sum_hi < 0 ? ~(uint64_t)0 : 0u);  // signed
+    add192(a.queue_sq, s.queue_sq_lo, s.queue_sq_hi, s.queue_sq_top);
     add192(a.resp_sum, s.resp_sum_lo, s.resp_sum_hi, 0u);
     add192(a.resp_sq, s.resp_sq_lo, s.resp_sq_hi, 0u);
   }

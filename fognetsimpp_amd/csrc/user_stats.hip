@@ -6,7 +6,8 @@
 // (ComputeBrokerApp3.cc:284-289, 310-313) and status 6 at its completion
 // (:228-233); node acks reach the broker one uplink later and are relayed
 // (BrokerBaseApp3.cc:164-198) to the user, one user downlink later.  The user
-// emits (simTime() - created) for each (mqttApp2.cc:252-291), created = the
+// emits (simTime() - created) * 1000 for each (mqttApp2.cc:252-291; raw
+// simtime_t values, fognet_hip.h "Reference signal values"), created = the
 // publish's send time = its broker arrival - the user uplink.  Acks carry no
 // state back into the decision loop, so every signal is a closed form of the
 // replay outputs; tests/oracle_lib restates them as real FES events.
@@ -20,26 +21,36 @@ namespace {
 constexpr int kUserThreads = 256;
 constexpr int kSignals = 4;  // delay, latency, latencyH1, taskTime
 
+// moments of raw emitted values (fognet_hip.h "Reference signal values")
 struct Mom {
-  uint64_t n, s_lo, s_hi, q_lo, q_hi;
+  uint64_t n, s_lo, s_hi, q_lo, q_hi, q_top, ovf;
   int64_t mn, mx;
 };
 
 __device__ __forceinline__ void mom_init(Mom& m) {
-  m = Mom{0u, 0u, 0u, 0u, 0u, INT64_MAX, INT64_MIN};
+  m = Mom{0u, 0u, 0u, 0u, 0u, 0u, 0u, INT64_MAX, INT64_MIN};
 }
 
-__device__ __forceinline__ void mom_add(Mom& m, int64_t v) {
+__device__ __forceinline__ void mom_add(Mom& m, int64_t raw) {
   m.n += 1u;
-  add_moment(m.s_lo, m.s_hi, m.q_lo, m.q_hi, (uint64_t)v);
-  m.mn = min(m.mn, v);
-  m.mx = max(m.mx, v);
+  add_moment_signed(m.s_lo, m.s_hi, m.q_lo, m.q_hi, m.q_top, raw);
+  m.mn = min(m.mn, raw);
+  m.mx = max(m.mx, raw);
+}
+
+// emit(signal, (simTime() - created) * 1000) (mqttApp2.cc:260,272,282); an
+// overflowing product throws and mqttApp2's catch drops the emission
+__device__ __forceinline__ void mom_add_ms(Mom& m, int64_t d) {
+  int64_t raw;
+  if (ms_raw(d, raw)) mom_add(m, raw);
+  else m.ovf += 1u;
 }
 
 __device__ __forceinline__ void mom_merge(Mom& a, const Mom& b) {
   a.n += b.n;
+  a.ovf += b.ovf;
   add128(a.s_lo, a.s_hi, b.s_lo, b.s_hi);
-  add128(a.q_lo, a.q_hi, b.q_lo, b.q_hi);
+  add192(a.q_lo, a.q_hi, a.q_top, b.q_lo, b.q_hi, b.q_top);
   a.mn = min(a.mn, b.mn);
   a.mx = max(a.mx, b.mx);
 }
@@ -63,15 +74,15 @@ __global__ __launch_bounds__(kUserThreads) void user_stats_kernel(ReplayArgs A, 
     const int64_t uu = uul[uo], ud = udl[uo];
     const int64_t created = t - uu;
     const int64_t relay = A.ul[nbase + k] + ud;  // node -> broker -> user
-    mom_add(m[0], uu);                            // delay: at the broker (:143)
-    mom_add(m[2], t + ud - created);              // broker pubAck status 4 -> latencyH1
+    mom_add(m[0], uu);                            // delay: at the broker (:143), a simtime_t (s)
+    mom_add_ms(m[2], t + ud - created);           // broker pubAck status 4 -> latencyH1
     const int64_t at_arrival = t + A.dl[nbase + k] + relay - created;  // node ack sent at the task's arrival
     if (st == 5u)
-      mom_add(m[1], at_arrival);  // "task assigned" -> latency
+      mom_add_ms(m[1], at_arrival);  // "task assigned" -> latency
     else if (st == 4u)
-      mom_add(m[2], at_arrival);  // "task queued" -> latencyH1
+      mom_add_ms(m[2], at_arrival);  // "task queued" -> latencyH1
     // (status 9: the task reached a crashed node, which sends no ack)
-    if (done >= 0) mom_add(m[3], done + relay - created);  // status 6 -> taskTime (-1: never completed)
+    if (done >= 0) mom_add_ms(m[3], done + relay - created);  // status 6 -> taskTime (-1: never completed)
   }
   fognet_moments* dst[kSignals] = {&out[r].delay, &out[r].latency, &out[r].latencyH1, &out[r].taskTime};
   for (int s = 0; s < kSignals; ++s) {
@@ -83,7 +94,7 @@ __global__ __launch_bounds__(kUserThreads) void user_stats_kernel(ReplayArgs A, 
     }
     if (threadIdx.x == 0) {
       const Mom& b = sh[0];
-      *dst[s] = fognet_moments{(int64_t)b.n, b.mn, b.mx, b.s_lo, b.s_hi, b.q_lo, b.q_hi, 0};
+      *dst[s] = fognet_moments{(int64_t)b.n, b.mn, b.mx, b.s_lo, b.s_hi, b.q_lo, b.q_hi, b.q_top, (int64_t)b.ovf};
     }
     __syncthreads();
   }

@@ -318,17 +318,31 @@ def run_v2(ctx: Context, trace: dict, broker_mips, stop_tick, required_time_s=0.
     return out
 
 
-def summarize_moments(m) -> dict:
-    """count/mean/stddev/sum/sqrsum/min/max in ms (the reference's signal unit) of one
-    tick-moments record, like cStdDev's `.sca` fields."""
-    n = int(m["count"])
+def _signed(v: int, bits: int) -> int:
+    return v - (1 << bits) if v >> (bits - 1) else v
+
+
+def _fields(n, s, q, lo, hi, unit) -> dict:
+    """cStdDev's `.sca` fields (count/mean/stddev/sum/sqrsum/min/max) of n values
+    with exact sum s and sum of squares q, in units of ``unit`` ms."""
     if n == 0:
         return dict(count=0)
-    s = int(m["sum_lo"]) | (int(m["sum_hi"]) << 64)
-    q = int(m["sq_lo"]) | (int(m["sq_hi"]) << 64)
     var = (q - s * s / n) / (n - 1) if n > 1 else 0.0
-    return dict(count=n, mean=s / n / 1e9, stddev=max(var, 0.0) ** 0.5 / 1e9, sum=s / 1e9, sqrsum=q / 1e18,
-                min=int(m["min_ticks"]) / 1e9, max=int(m["max_ticks"]) / 1e9)
+    return dict(count=n, mean=s / n * unit, stddev=max(var, 0.0) ** 0.5 * unit, sum=s * unit, sqrsum=q * unit * unit,
+                min=int(lo) * unit, max=int(hi) * unit)
+
+
+def summarize_moments(m, raw_ms: bool = True) -> dict:
+    """count/mean/stddev/sum/sqrsum/min/max of one signal-moments record
+    (fognet_moments) like cStdDev's `.sca` fields.  ``raw_ms``: the values are
+    raw emitted simtime_t of a ms signal (recorded value raw * 1e-12 ms); False
+    for ``delay`` (raw ticks, reported in ms)."""
+    n = int(m["count"])
+    s = _signed(int(m["sum_lo"]) | (int(m["sum_hi"]) << 64), 128)
+    q = int(m["sq_lo"]) | (int(m["sq_hi"]) << 64) | (int(m["sq_top"]) << 128)
+    d = _fields(n, s, q, m["min_raw"], m["max_raw"], 1e-12 if raw_ms else 1e-9)
+    d["overflow"] = int(m["overflow"])
+    return d
 
 
 def reduce_stats(ctx: Context, stats: torch.Tensor, R: int) -> np.ndarray:
@@ -367,25 +381,18 @@ def _u192(limbs) -> int:
 
 
 def summarize(job) -> dict:
-    """`.sca`-style fields (count/mean/stddev/sum/sqrsum/min/max, ms) of a job record,
-    mirroring cStdDev's output for queueTime (ComputeBrokerApp3.ned:45-46)."""
-    def block(n, s, q, lo, hi):
-        n = int(n)
-        s, q = _u192(s), _u192(q)
-        if n == 0:
-            return dict(count=0)
-        mean = s / n
-        var = (q - s * s / n) / (n - 1) if n > 1 else 0.0
-        return dict(count=n, mean=mean / 1e9, stddev=max(var, 0.0) ** 0.5 / 1e9, sum=s / 1e9,
-                    sqrsum=q / 1e18, min=int(lo) / 1e9, max=int(hi) / 1e9)
-
+    """`.sca`-style fields (count/mean/stddev/sum/sqrsum/min/max, ms) of a job record:
+    queueTime as the reference records it (ComputeBrokerApp3.cc:238,
+    ComputeBrokerApp3.ned:45-46; raw values * 1e-12), response in ticks / 1e9."""
+    qs = _signed(_u192(job["queue_sum"]), 192)
+    queue = _fields(int(job["n_qtime"]), qs, _u192(job["queue_sq"]), job["queue_min_raw"], job["queue_max_raw"], 1e-12)
+    queue["overflow"] = int(job["n_qtime_overflow"])
     return {
         "replications": int(job["n_reps"]), "failed": int(job["n_failed"]),
         "decisions": int(job["n_tasks"]), "queued": int(job["n_queued"]), "started": int(job["n_started"]),
-        "queueTime_ms": block(job["n_queued"], job["queue_sum"], job["queue_sq"], job["queue_min_ticks"],
-                              job["queue_max_ticks"]),
-        "response_ms": block(job["n_tasks"], job["resp_sum"], job["resp_sq"], job["resp_min_ticks"],
-                             job["resp_max_ticks"]),
+        "queueTime_ms": queue,
+        "response_ms": _fields(int(job["n_tasks"]), _u192(job["resp_sum"]), _u192(job["resp_sq"]),
+                               job["resp_min_ticks"], job["resp_max_ticks"], 1e-9),
         "max_pending": int(job["max_pending"]),
         "busy_s": int(job["busy_s"]),
         "energy_j": float(job["energy_j"]),

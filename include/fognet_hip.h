@@ -40,15 +40,17 @@
 extern "C" {
 #endif
 
-#define FOGNET_ABI_VERSION 6
+#define FOGNET_ABI_VERSION 7
 #define FOGNET_TICKS_PER_SECOND 1000000000000LL
 
 /* Latency histograms (device-side statistics, summed over replications; the
  * only data the multi-GPU path all-reduces over RCCL together with energy).
- * Metric 0 = queueTime (ComputeBrokerApp3.cc:238, queued tasks only),
- * metric 1 = response (completion tick - publish tick at the broker).
- * A value of v ticks has q = v / 10^9 whole milliseconds and falls in bin
- * 0 if q == 0, else min(63, floor(log2 q) + 1): bin b >= 1 holds [2^(b-1), 2^b) ms. */
+ * Metric 0 = queueTime (ComputeBrokerApp3.cc:238, queued tasks only): q = the
+ * whole part of the recorded value in ms (the emitted raw simtime_t * 1e-12,
+ * see "Reference signal values" below); metric 1 = response (completion tick -
+ * publish tick at the broker): q = ticks / 10^9 whole milliseconds.  A value
+ * falls in bin 0 if q < 1, else min(63, floor(log2 q) + 1): bin b >= 1 holds
+ * [2^(b-1), 2^b) ms. */
 #define FOGNET_HIST_METRICS 2
 #define FOGNET_HIST_BINS 64
 
@@ -88,16 +90,40 @@ typedef enum fognet_v2_action {
     FOGNET_V2_NO_NODES = 6   /* no compute broker registered: "no compute resource available" puback   */
 } fognet_v2_action;
 
-/* Per-replication statistics.  Times are kept in exact ticks; 128-bit sums are
- * split into (lo, hi) uint64 halves so results are bit-reproducible. */
+/* Reference signal values.  The reference emits its latency signals as
+ * simtime_t values (OMNeT++ 4.6, scale 1e-12: a raw int64 t, recorded as the
+ * double dbl() = t * 1e-12), and computes them with SimTime's double round
+ * trips: SimTime(double d) = toInt64(1e12 * d), SimTime * double =
+ * toInt64(t * d), toInt64(x) = floor(x + 0.5), a cRuntimeError outside int64.
+ * The statistics keep exact moments of those RAW emitted values ("raw"):
+ *   queueTime  (simTime() - SimTime(queueStartTime)) * 1000, queueStartTime =
+ *              simTime().dbl() of the enqueue, a double (ComputeBrokerApp3.cc:238,
+ *              306, Request.cc:26): raw = toInt64((double)(now -
+ *              toInt64(1e12 * (a * 1e-12))) * 1000.0) for a task enqueued at tick a
+ *              and started at tick now (the recorded value, raw * 1e-12, is in ms;
+ *              it can be a few ulps off the exact tick difference, even negative
+ *              for a task queued and started in the same tick);
+ *   latency / latencyH1 / taskTime  (simTime() - timeCreated) * 1000 with
+ *              timeCreated a simtime_t (mqttApp2.cc:260,272,282): raw = toInt64(d * 1000.0);
+ *   delay      simTime() - creationTime (BrokerBaseApp3.cc:143): raw = d ticks (s).
+ * An emission whose product leaves the int64 range (a queue time above ~9223 s)
+ * throws in the reference: at queueTime the run aborts (releaseResource has no
+ * handler), at the user signals the exception is swallowed by mqttApp2's catch
+ * and the emission is lost.  Such emissions are counted (n_qtime_overflow,
+ * fognet_moments.overflow) and left out of the moments and histograms; the replay
+ * itself goes on.  Signed sums are two's complement. */
+
+/* Per-replication statistics.  Exact integer moments, split into uint64 limbs
+ * ([lo, hi, top] = bits 0-63, 64-127, 128-191) so results are bit-reproducible. */
 typedef struct fognet_rep_stats {
     int64_t n_tasks;          /* decisions made                                                   */
-    int64_t n_queued;         /* node acks with status 4 (= queueTime emissions, :238)             */
+    int64_t n_queued;         /* node acks with status 4 ("task queued", :310-313)                 */
     int64_t n_started;        /* node acks with status 5                                          */
     int64_t last_tick;        /* latest RELEASERESOURCE tick (makespan)                           */
-    int64_t queue_min_ticks, queue_max_ticks; /* over queued tasks: start - arrival at node        */
+    int64_t queue_min_raw, queue_max_raw;     /* queueTime emissions: raw values (see above)       */
     int64_t resp_min_ticks, resp_max_ticks;   /* over all tasks: done - arrival at broker          */
-    uint64_t queue_sum_lo, queue_sum_hi, queue_sq_lo, queue_sq_hi;
+    uint64_t queue_sum_lo, queue_sum_hi;      /* signed 128-bit sum of queueTime raw values        */
+    uint64_t queue_sq_lo, queue_sq_hi;        /* bits 0-127 of the sum of their squares            */
     uint64_t resp_sum_lo, resp_sum_hi, resp_sq_lo, resp_sq_hi;
     int64_t events;           /* reference FES events this replay stands for (2N + 4 per task)    */
     int32_t max_pending;      /* max tasks assigned to one node whose completion advert had not
@@ -109,23 +135,29 @@ typedef struct fognet_rep_stats {
                                  P_busy_j * B_j + P_idle_j * ((H - B_j * 1e12) / 1e12), with
                                  B_j = node j's service seconds, H = last_tick (0 if no task);
                                  IEEE fp64, no fused multiply-add                                 */
+    uint64_t queue_sq_top;    /* bits 128-191 of the queueTime sum of squares                     */
+    int64_t n_qtime;          /* queueTime emissions in the moments (queued tasks that started)   */
+    int64_t n_qtime_overflow; /* queueTime emissions the reference cannot make (simtime overflow) */
 } fognet_rep_stats;
 
 /* Job-level statistics: the exact sum of any set of fognet_rep_stats.  Sums
- * are 192-bit unsigned integers (limbs [0] = least significant), so combining
- * is associative and the result does not depend on how replications were
- * sharded over GPUs.  Mean/stddev in ms follow as sum / n / 1e9 etc. */
+ * are 192-bit integers (limbs [0] = least significant; queue_sum two's
+ * complement), so combining is associative and the integer fields do not
+ * depend on how replications were sharded over GPUs.  Mean/stddev in ms:
+ * queueTime sum * 1e-12 / n_qtime, response sum / n_tasks / 1e9, etc. */
 typedef struct fognet_job_stats {
     int64_t n_reps, n_failed;
     int64_t n_tasks, n_queued, n_started;
     int64_t last_tick;
-    int64_t queue_min_ticks, queue_max_ticks, resp_min_ticks, resp_max_ticks;
+    int64_t queue_min_raw, queue_max_raw, resp_min_ticks, resp_max_ticks;
     uint64_t queue_sum[3], queue_sq[3], resp_sum[3], resp_sq[3];
     int64_t events;
     int64_t max_pending;
     int64_t busy_s;
-    double energy_j;          /* fp64 sum over replications (fixed tree order on one device;
-                                 across GPUs within 1e-9 relative)                               */
+    double energy_j;          /* fp64 sum over replications: fixed tree order on one device, rank
+                                 order across GPUs; differs from another sharding's sum by
+                                 rounding only (within 1e-9 relative)                            */
+    int64_t n_qtime, n_qtime_overflow;
 } fognet_job_stats;
 
 /* R trace replays of T tasks over N fog nodes, SoA, row-major [R][T] / [R|1][N]. */
@@ -172,16 +204,18 @@ typedef struct fognet_batch_out {
                                  (the caller zeroes it; nullable)                                 */
 } fognet_batch_out;
 
-/* count / min / max / exact 128-bit sum and sum of squares of values in ticks
- * (min_ticks = INT64_MAX, max_ticks = INT64_MIN when count == 0). */
+/* count / min / max / exact signed 128-bit sum and 192-bit sum of squares of a
+ * signal's raw emitted values (min_raw = INT64_MAX, max_raw = INT64_MIN when
+ * count == 0); overflow: emissions lost to the simtime_t range (see above). */
 typedef struct fognet_moments {
-    int64_t count, min_ticks, max_ticks;
-    uint64_t sum_lo, sum_hi, sq_lo, sq_hi;
-    int64_t pad;
+    int64_t count, min_raw, max_raw;
+    uint64_t sum_lo, sum_hi, sq_lo, sq_hi, sq_top;
+    int64_t overflow;
 } fognet_moments;
 
-/* User-side signals of one replication, in ticks
- * (the reference emits (simTime() - created) * 1000 ms, i.e. ticks / 1e9):
+/* User-side signals of one replication, as raw emitted
+ * values (see "Reference signal values"): delay in ticks (s), the others the
+ * raw simtime_t of (simTime() - created) * 1000 (recorded value raw * 1e-12 ms):
  *   delay      broker `delay` (BrokerBaseApp3.cc:143): publish arrival at the
  *              broker - creation at the user, every publish
  *   latency    mqttApp2 on the relayed status-5 ack ("task assigned",

@@ -17,6 +17,7 @@
  */
 #include "fognet_oracle.h"
 
+#include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -124,10 +125,23 @@ static void acc128(uint64_t *lo, uint64_t *hi, uint64_t v_lo, uint64_t v_hi) {
 }
 
 static void acc_moment(uint64_t *sum_lo, uint64_t *sum_hi, uint64_t *sq_lo, uint64_t *sq_hi, int64_t v) {
-    /* v >= 0 for queue/response times */
+    /* v >= 0 for response times */
     unsigned __int128 sq = (unsigned __int128)(uint64_t)v * (uint64_t)v;
     acc128(sum_lo, sum_hi, (uint64_t)v, 0);
     acc128(sq_lo, sq_hi, (uint64_t)sq, (uint64_t)(sq >> 64));
+}
+
+/* signed value: two's complement 128-bit sum, 192-bit sum of squares */
+static void acc_moment_signed(uint64_t *sum_lo, uint64_t *sum_hi, uint64_t *sq_lo, uint64_t *sq_hi,
+                              uint64_t *sq_top, int64_t v) {
+    uint64_t m = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+    unsigned __int128 sq = (unsigned __int128)m * m;
+    acc128(sum_lo, sum_hi, (uint64_t)v, v < 0 ? ~(uint64_t)0 : 0);
+    unsigned __int128 q = ((unsigned __int128)*sq_hi << 64) | *sq_lo;
+    unsigned __int128 n = q + sq;
+    *sq_lo = (uint64_t)n;
+    *sq_hi = (uint64_t)(n >> 64);
+    *sq_top += n < q; /* carry out of bit 127 */
 }
 
 int orc_hist_bin(int64_t ticks) {
@@ -138,8 +152,40 @@ int orc_hist_bin(int64_t ticks) {
     return b > ORC_HIST_BINS - 1 ? ORC_HIST_BINS - 1 : b;
 }
 
+/* ---- OMNeT++ 4.6 SimTime arithmetic (fognet_oracle.h) */
+
+static double simtime_dbl(int64_t t) { return (double)t * 1e-12; } /* dbl() = t * invfscale */
+
+static int simtime_toint64(double x, int64_t *out) { /* SimTime::toInt64 */
+    double f = floor(x + 0.5);
+    if (!(fabs(f) < 9223372036854775808.0)) return 0; /* cRuntimeError: out of range */
+    *out = (int64_t)f;
+    return 1;
+}
+
+int orc_qtime_raw(int64_t now, int64_t qstart, int64_t *raw) {
+    int64_t qs = 0;
+    simtime_toint64(1e12 * simtime_dbl(qstart), &qs); /* simTime() - (double)queueStartTime: SimTime(double) */
+    return simtime_toint64((double)(now - qs) * 1000.0, raw); /* ... * 1000 (ComputeBrokerApp3.cc:238) */
+}
+
+int orc_ms_raw(int64_t diff_ticks, int64_t *raw) { return simtime_toint64((double)diff_ticks * 1000.0, raw); }
+
+int orc_hist_bin_raw(int64_t raw) {
+    /* the recorded double (dbl() of the emitted value), in whole "ms" */
+    double v = simtime_dbl(raw);
+    if (!(v >= 1.0)) return 0;
+    uint64_t q = (uint64_t)v;
+    int b = 64 - __builtin_clzll(q);
+    return b > ORC_HIST_BINS - 1 ? ORC_HIST_BINS - 1 : b;
+}
+
 static void hist_add(sim_t *s, int metric, int64_t ticks) {
     if (s->out->hist) s->out->hist[metric * ORC_HIST_BINS + orc_hist_bin(ticks)]++;
+}
+
+static void hist_add_raw(sim_t *s, int metric, int64_t raw) {
+    if (s->out->hist) s->out->hist[metric * ORC_HIST_BINS + orc_hist_bin_raw(raw)]++;
 }
 
 static int schedule(sim_t *s, ev_t *e) {
@@ -154,9 +200,18 @@ static int64_t user_dl(const sim_t *s, int64_t t) { return s->in->user_dl_tick[s
 
 static void moment_add(orc_moments *m, int64_t v) {
     m->count++;
-    if (v < m->min_ticks) m->min_ticks = v;
-    if (v > m->max_ticks) m->max_ticks = v;
-    acc_moment(&m->sum_lo, &m->sum_hi, &m->sq_lo, &m->sq_hi, v);
+    if (v < m->min_raw) m->min_raw = v;
+    if (v > m->max_raw) m->max_raw = v;
+    acc_moment_signed(&m->sum_lo, &m->sum_hi, &m->sq_lo, &m->sq_hi, &m->sq_top, v);
+}
+
+/* emit(signal, (simTime() - created) * 1000): dropped when the simtime_t
+ * product overflows (the cRuntimeError is swallowed by the handler's
+ * catch (std::exception&), mqttApp2.cc:253,293) */
+static void moment_add_ms(orc_moments *m, int64_t diff_ticks) {
+    int64_t raw;
+    if (orc_ms_raw(diff_ticks, &raw)) moment_add(m, raw);
+    else m->overflow++;
 }
 
 /* socket.sendTo(MqttMsgPuback{status}) towards task t's user: from the broker
@@ -175,14 +230,14 @@ static int send_ack(sim_t *s, int at_broker, int32_t k, int64_t t, int32_t statu
 }
 
 /* mqttApp2::processPacket, MqttMsgPuback branch (mqttApp2.cc:252-291): the
- * signal is (simTime() - timeCreated) * 1000 ms, kept in exact ticks here. */
+ * signal is (simTime() - timeCreated) * 1000, timeCreated a simtime_t (raw emitted value). */
 static void user_ack(sim_t *s, const ev_t *e) {
     orc_user_stats *u = s->out->user;
     int64_t created = s->in->arrive_tick[e->task] - user_ul(s, e->task); /* sendMqttData: created at the user */
     int64_t v = s->now - created;
-    if (e->mips == 5) moment_add(&u->latency, v);        /* :257-265 */
-    else if (e->mips == 4) moment_add(&u->latencyH1, v); /* :269-277 */
-    else if (e->mips == 6) moment_add(&u->taskTime, v);  /* :279-291 */
+    if (e->mips == 5) moment_add_ms(&u->latency, v);        /* :257-265 */
+    else if (e->mips == 4) moment_add_ms(&u->latencyH1, v); /* :269-277 */
+    else if (e->mips == 6) moment_add_ms(&u->taskTime, v);  /* :279-291 */
 }
 
 /* cSimpleModule::scheduleAt for a node's selfMsg. */
@@ -247,12 +302,19 @@ static int node_release(sim_t *s, int32_t k) {
     if (nd->qn > 0) { /* :236-252 */
         nd->resourceStatus = 1;
         req_t *h = &nd->q[nd->qh];
-        /* emit(queueTimeSignal, (simTime() - queueStartTime) * 1000) (:238), kept in exact ticks */
-        int64_t qt = s->now - h->qstart_tick;
-        acc_moment(&s->st.queue_sum_lo, &s->st.queue_sum_hi, &s->st.queue_sq_lo, &s->st.queue_sq_hi, qt);
-        if (qt < s->st.queue_min_ticks) s->st.queue_min_ticks = qt;
-        if (qt > s->st.queue_max_ticks) s->st.queue_max_ticks = qt;
-        hist_add(s, 0, qt);
+        /* emit(queueTimeSignal, (simTime() - queueStartTime) * 1000) (:238): the raw
+         * emitted simtime_t; an overflow is a cRuntimeError in the reference (counted) */
+        int64_t qt;
+        if (orc_qtime_raw(s->now, h->qstart_tick, &qt)) {
+            acc_moment_signed(&s->st.queue_sum_lo, &s->st.queue_sum_hi, &s->st.queue_sq_lo, &s->st.queue_sq_hi,
+                              &s->st.queue_sq_top, qt);
+            if (qt < s->st.queue_min_raw) s->st.queue_min_raw = qt;
+            if (qt > s->st.queue_max_raw) s->st.queue_max_raw = qt;
+            s->st.n_qtime++;
+            hist_add_raw(s, 0, qt);
+        } else {
+            s->st.n_qtime_overflow++;
+        }
         nd->currentTask = *h; /* :240-244 */
         nd->qh = (nd->qh + 1) % nd->qcap; /* requests.erase(begin) (:246) */
         nd->qn--;
@@ -471,17 +533,17 @@ int orc_run_rep(const orc_rep_in *in, orc_rep_out *out) {
     s.out = out;
     int32_t N = in->n_nodes;
     int64_t T = in->n_tasks;
-    s.st.queue_min_ticks = INT64_MAX;
+    s.st.queue_min_raw = INT64_MAX;
     s.st.resp_min_ticks = INT64_MAX;
-    s.st.queue_max_ticks = INT64_MIN;
+    s.st.queue_max_raw = INT64_MIN;
     s.st.resp_max_ticks = INT64_MIN;
     s.st.last_tick = INT64_MIN;
     if (out->user) {
         orc_moments *ms[4] = {&out->user->delay, &out->user->latency, &out->user->latencyH1, &out->user->taskTime};
         for (int i = 0; i < 4; i++) {
             memset(ms[i], 0, sizeof *ms[i]);
-            ms[i]->min_ticks = INT64_MAX;
-            ms[i]->max_ticks = INT64_MIN;
+            ms[i]->min_raw = INT64_MAX;
+            ms[i]->max_raw = INT64_MIN;
         }
     }
     int rc = ORC_OK;

@@ -72,11 +72,13 @@ typedef struct {
 /* Task status of a task that reached a crashed node (no ack, never served). */
 #define ORC_TASK_LOST 9
 
-/* count / min / max / exact 128-bit sum and sum of squares of values in ticks */
+/* count / min / max / exact sum (signed 128-bit) and sum of squares (192-bit,
+ * sq_top = bits 128..191) of a signal's raw emitted simtime_t values; overflow
+ * counts emissions the reference drops (simtime_t range, orc_ms_raw). */
 typedef struct {
-    int64_t count, min_ticks, max_ticks;
-    uint64_t sum_lo, sum_hi, sq_lo, sq_hi;
-    int64_t pad;
+    int64_t count, min_raw, max_raw;
+    uint64_t sum_lo, sum_hi, sq_lo, sq_hi, sq_top;
+    int64_t overflow;
 } orc_moments;
 
 /* The user-side signals of the offload loop: broker `delay` (BrokerBaseApp3.cc:143)
@@ -87,11 +89,15 @@ typedef struct {
     orc_moments delay, latency, latencyH1, taskTime;
 } orc_user_stats;
 
+/* Per-replication statistics (byte layout = fognet_rep_stats, fognet_hip.h).
+ * queueTime moments are over the raw simtime_t value the reference emits
+ * (orc_qtime_raw), response moments over exact ticks. */
 typedef struct {
     int64_t n_tasks, n_queued, n_started;
     int64_t last_tick;
-    int64_t queue_min_ticks, queue_max_ticks, resp_min_ticks, resp_max_ticks;
-    /* exact 128-bit accumulators (two's complement halves) */
+    int64_t queue_min_raw, queue_max_raw, resp_min_ticks, resp_max_ticks;
+    /* exact accumulators: queue sum signed two's complement 128-bit, squares 192-bit
+     * (queue_sq_top = bits 128..191), response sums unsigned 128-bit */
     uint64_t queue_sum_lo, queue_sum_hi, queue_sq_lo, queue_sq_hi;
     uint64_t resp_sum_lo, resp_sum_hi, resp_sq_lo, resp_sq_hi;
     int64_t events;               /* FES events processed (diagnostic) */
@@ -99,7 +105,27 @@ typedef struct {
     int32_t status;
     int64_t busy_s;               /* sum of service seconds over all tasks             */
     double energy_j;              /* builder-defined node energy (fognet_hip.h)        */
+    uint64_t queue_sq_top;
+    int64_t n_qtime;              /* queueTime emissions in the moments                */
+    int64_t n_qtime_overflow;     /* emissions at which the reference's simtime_t
+                                     arithmetic leaves the int64 range (orc_qtime_raw) */
 } orc_rep_stats;
+
+/* OMNeT++ 4.6 SimTime at the default scale 1e-12 (include/simtime.h, not in the
+ * reference tree; restated): raw int64 t, dbl() = t * 1e-12, SimTime(double d) =
+ * toInt64(1e12 * d), SimTime * double = toInt64(t * d), with toInt64(x) =
+ * floor(x + 0.5) and a cRuntimeError when that is outside the int64 range.
+ *
+ * orc_qtime_raw: the raw simtime_t the node emits as queueTime
+ * (ComputeBrokerApp3.cc:238) for a task enqueued at tick qstart (queueStartTime
+ * = simTime().dbl(), :306, a double) and started at tick now:
+ *   (simTime() - SimTime(queueStartTime)) * 1000.
+ * Returns 0 when the reference throws there (|...| >= 2^63: a queue time of
+ * more than ~9223 s); the recorded value is raw * 1e-12 (dbl()) "ms". */
+int orc_qtime_raw(int64_t now, int64_t qstart, int64_t *raw);
+/* (simTime() - t0) * 1000 with t0 a simtime_t (mqttApp2.cc:260,272,282): the
+ * raw simtime_t of the user-side ms signals; 0 on overflow. */
+int orc_ms_raw(int64_t diff_ticks, int64_t *raw);
 
 typedef struct {
     int32_t *node;       /* [T] chosen node index, -1 if never decided (nullable) */
@@ -199,8 +225,10 @@ typedef struct {
 } orc_v2_batch;
 int orc_run_v2_batch(const orc_v2_batch *b, int threads);
 
-/* Histogram bin of a duration in ticks (fognet_hip.h FOGNET_HIST_BINS rule). */
+/* Histogram bin of a duration in ticks (fognet_hip.h FOGNET_HIST_BINS rule) and of a
+ * raw emitted ms signal (bin of the recorded double raw * 1e-12 ms). */
 int orc_hist_bin(int64_t ticks);
+int orc_hist_bin_raw(int64_t raw);
 
 /* Batch of R replications sharing T and N; node params have stride node_stride
  * (0 = shared).  Runs on `threads` pthreads, one replication per thread at a time. */

@@ -69,3 +69,29 @@ def replay_down_cases():
         e["done"] = [x * ms if x >= 0 else -1 for x in e.pop("done_ms")]
         out.append((c["name"], tr, e))
     return out
+
+
+def qtime_cases():
+    """tests/golden/kat_qtime.json (make_kat_qtime.py): the reference's queueTime value."""
+    d = json.load(open(os.path.join(GOLDEN, "kat_qtime.json")))
+    out = []
+    for c in d["cases"]:
+        tr = dict(arrive=np.array(c["arrive"], np.int64)[None], req=np.array(c["req"], np.int32)[None],
+                  mips=np.array(c["mips"], np.int32), dl=np.array(c["dl"], np.int64),
+                  ul=np.array(c["ul"], np.int64), init=np.array(c["init"], np.int64))
+        out.append((c["name"], tr, c["expect"]))
+    return out
+
+
+def check_qtime_record(st, exp):
+    """Compare a fognet_rep_stats / orc_rep_stats record with a kat_qtime expectation."""
+    assert st["status"] == 0
+    assert int(st["n_qtime"]) == exp["n_qtime"] and int(st["n_qtime_overflow"]) == exp["n_qtime_overflow"]
+    s = int(st["queue_sum_lo"]) | (int(st["queue_sum_hi"]) << 64)
+    s = s - (1 << 128) if s >> 127 else s
+    q = int(st["queue_sq_lo"]) | (int(st["queue_sq_hi"]) << 64) | (int(st["queue_sq_top"]) << 128)
+    assert s == exp["queue_sum"] and q == exp["queue_sq"]
+    if exp["queue_min"] is not None:
+        assert int(st["queue_min_raw"]) == exp["queue_min"] and int(st["queue_max_raw"]) == exp["queue_max"]
+    else:
+        assert int(st["queue_min_raw"]) == np.iinfo(np.int64).max

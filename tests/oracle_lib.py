@@ -19,7 +19,7 @@ class OrcRepStats(C.Structure):
     _fields_ = [
         ("n_tasks", C.c_int64), ("n_queued", C.c_int64), ("n_started", C.c_int64),
         ("last_tick", C.c_int64),
-        ("queue_min_ticks", C.c_int64), ("queue_max_ticks", C.c_int64),
+        ("queue_min_raw", C.c_int64), ("queue_max_raw", C.c_int64),
         ("resp_min_ticks", C.c_int64), ("resp_max_ticks", C.c_int64),
         ("queue_sum_lo", C.c_uint64), ("queue_sum_hi", C.c_uint64),
         ("queue_sq_lo", C.c_uint64), ("queue_sq_hi", C.c_uint64),
@@ -27,15 +27,16 @@ class OrcRepStats(C.Structure):
         ("resp_sq_lo", C.c_uint64), ("resp_sq_hi", C.c_uint64),
         ("events", C.c_int64), ("max_pending", C.c_int32), ("status", C.c_int32),
         ("busy_s", C.c_int64), ("energy_j", C.c_double),
+        ("queue_sq_top", C.c_uint64), ("n_qtime", C.c_int64), ("n_qtime_overflow", C.c_int64),
     ]
 
 
 _NP = {C.c_int64: np.int64, C.c_uint64: np.uint64, C.c_int32: np.int32, C.c_double: np.float64}
 ORC_STATS_DTYPE = np.dtype([(n, _NP[t]) for n, t in OrcRepStats._fields_])
 assert ORC_STATS_DTYPE.itemsize == C.sizeof(OrcRepStats)
-MOMENTS_DTYPE = np.dtype([("count", np.int64), ("min_ticks", np.int64), ("max_ticks", np.int64),
+MOMENTS_DTYPE = np.dtype([("count", np.int64), ("min_raw", np.int64), ("max_raw", np.int64),
                           ("sum_lo", np.uint64), ("sum_hi", np.uint64), ("sq_lo", np.uint64), ("sq_hi", np.uint64),
-                          ("pad", np.int64)])
+                          ("sq_top", np.uint64), ("overflow", np.int64)])
 USER_SIGNALS = ("delay", "latency", "latencyH1", "taskTime")
 USER_STATS_DTYPE = np.dtype([(n, MOMENTS_DTYPE) for n in USER_SIGNALS])
 POLICY_REF_V3, POLICY_EXT_LAT = 1, 16
@@ -70,6 +71,12 @@ def lib():
         _lib.orc_decide_ext_lat.restype = C.c_int
         _lib.orc_hist_bin.argtypes = [C.c_int64]
         _lib.orc_hist_bin.restype = C.c_int
+        _lib.orc_hist_bin_raw.argtypes = [C.c_int64]
+        _lib.orc_hist_bin_raw.restype = C.c_int
+        _lib.orc_qtime_raw.argtypes = [C.c_int64, C.c_int64, C.POINTER(C.c_int64)]
+        _lib.orc_qtime_raw.restype = C.c_int
+        _lib.orc_ms_raw.argtypes = [C.c_int64, C.POINTER(C.c_int64)]
+        _lib.orc_ms_raw.restype = C.c_int
         _lib.orc_decide_v3.argtypes = [C.c_int32, p, p, C.c_int32, C.POINTER(C.c_int32)]
         _lib.orc_decide_v3.restype = C.c_int
         _lib.orc_decide_v2.argtypes = [C.c_int32, p, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
@@ -81,6 +88,18 @@ def lib():
 
 def _ptr(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def qtime_raw(now: int, qstart: int):
+    """Raw simtime_t the node emits as queueTime (ComputeBrokerApp3.cc:238), or None
+    where the reference's simtime_t arithmetic throws (orc_qtime_raw)."""
+    out = C.c_int64(0)
+    return out.value if lib().orc_qtime_raw(int(now), int(qstart), C.byref(out)) else None
+
+
+def ms_raw(diff_ticks: int):
+    out = C.c_int64(0)
+    return out.value if lib().orc_ms_raw(int(diff_ticks), C.byref(out)) else None
 
 
 def decide_v3(adv_busy, adv_mips, req):

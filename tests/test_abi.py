@@ -4,6 +4,7 @@ import ctypes
 import glob
 import os
 import re
+import subprocess
 
 import pytest
 import torch
@@ -37,17 +38,35 @@ def test_library_exports_every_declared_symbol():
     assert set(declared_functions()) == set(abi.SIGNATURES), "ctypes mirror out of sync with the header"
 
 
-def test_struct_sizes_match_header():
-    # sizes fixed by the header's field lists (all naturally aligned)
-    assert ctypes.sizeof(abi.RepStats) == 8 * 17 + 4 * 2 + 8 * 2
-    assert ctypes.sizeof(abi.JobStats) == 8 * 10 + 8 * 12 + 8 * 2 + 8 * 2
-    assert ctypes.sizeof(abi.BatchIn) == 4 * 6 + 8 * 9
-    assert ctypes.sizeof(abi.BatchOut) == 8 * 7
+def test_struct_layouts_match_header(tmp_path):
+    """sizeof/offsetof of every struct field as the C compiler lays out
+    include/fognet_hip.h, against the ctypes mirror."""
+    structs = {"fognet_rep_stats": abi.RepStats, "fognet_job_stats": abi.JobStats, "fognet_moments": abi.Moments,
+               "fognet_user_stats": abi.UserStats, "fognet_batch_in": abi.BatchIn, "fognet_batch_out": abi.BatchOut,
+               "fognet_gen_params": abi.GenParams, "fognet_v2_in": abi.V2In, "fognet_v2_stats": abi.V2Stats,
+               "fognet_v2_out": abi.V2Out}
+    lines = []
+    for cname, st in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in st._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    src = tmp_path / "layout.c"
+    src.write_text("#include <stdio.h>\n#include <stddef.h>\n#include \"fognet_hip.h\"\nint main(void){" +
+                   "\n".join(lines) + "return 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    got = dict(ln.split() for ln in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                    text=True).stdout.splitlines())
+    for cname, st in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(st), cname
+        for f, _ in st._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(st, f).offset, f"{cname}.{f}"
 
 
 def test_status_strings_and_version():
     lib = abi.load()
-    assert lib.fognet_abi_version() == abi.ABI_VERSION == 6
+    assert lib.fognet_abi_version() == abi.ABI_VERSION == 7
     assert lib.fognet_status_string(abi.FOGNET_ERR_CAPACITY) == b"pending-task ring capacity exceeded"
     assert lib.fognet_status_string(99) == b"unknown status"
 
@@ -59,12 +78,12 @@ def test_job_stats_merge_is_exact_host_code():
     lib.fognet_job_stats_init(ctypes.byref(b))
     b.n_reps, b.n_tasks = 3, 10
     b.queue_sum[0], b.queue_sum[1] = 2**64 - 1, 5
-    b.queue_min_ticks, b.queue_max_ticks = 7, 9
+    b.queue_min_raw, b.queue_max_raw = 7, 9
     lib.fognet_job_stats_merge(ctypes.byref(a), ctypes.byref(b))
     lib.fognet_job_stats_merge(ctypes.byref(a), ctypes.byref(b))
     assert a.n_reps == 6 and a.n_tasks == 20
     assert (a.queue_sum[0], a.queue_sum[1], a.queue_sum[2]) == (2**64 - 2, 11, 0)
-    assert a.queue_min_ticks == 7 and a.queue_max_ticks == 9
+    assert a.queue_min_raw == 7 and a.queue_max_raw == 9
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU refusal")

@@ -26,14 +26,21 @@ def job_from_rep_stats(st):
     rec["energy_j"] = float(np.sum(ok["energy_j"]))
     big = np.iinfo(np.int64)
     rec["last_tick"] = int(ok["last_tick"].max()) if len(ok) else big.min
-    rec["queue_min_ticks"] = int(ok["queue_min_ticks"].min()) if len(ok) else big.max
+    rec["queue_min_raw"] = int(ok["queue_min_raw"].min()) if len(ok) else big.max
     rec["resp_min_ticks"] = int(ok["resp_min_ticks"].min()) if len(ok) else big.max
-    rec["queue_max_ticks"] = int(ok["queue_max_ticks"].max()) if len(ok) else big.min
+    rec["queue_max_raw"] = int(ok["queue_max_raw"].max()) if len(ok) else big.min
+    rec["n_qtime"] = int(ok["n_qtime"].sum())
+    rec["n_qtime_overflow"] = int(ok["n_qtime_overflow"].sum())
     rec["resp_max_ticks"] = int(ok["resp_max_ticks"].max()) if len(ok) else big.min
     rec["max_pending"] = int(ok["max_pending"].max()) if len(ok) else 0
     for name, lo, hi in (("queue_sum", "queue_sum_lo", "queue_sum_hi"), ("queue_sq", "queue_sq_lo", "queue_sq_hi"),
                          ("resp_sum", "resp_sum_lo", "resp_sum_hi"), ("resp_sq", "resp_sq_lo", "resp_sq_hi")):
-        tot = sum(int(a) | (int(b) << 64) for a, b in zip(ok[lo], ok[hi]))
+        vals = [int(a) | (int(b) << 64) for a, b in zip(ok[lo], ok[hi])]
+        if name == "queue_sum":  # signed two's complement
+            vals = [v - (1 << 128) if v >> 127 else v for v in vals]
+        if name == "queue_sq":
+            vals = [v | (int(t) << 128) for v, t in zip(vals, ok["queue_sq_top"])]
+        tot = sum(vals) % (1 << 192)
         rec[name] = [(tot >> (64 * i)) & (2**64 - 1) for i in range(3)]
     return rec
 

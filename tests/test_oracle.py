@@ -198,14 +198,16 @@ def test_user_side_known_answer():
     7 (BrokerBaseApp3.cc:143); its status-4 pubAck reaches the user at 111,
     created at 93 -> latencyH1 18; the node's status-5 ack leaves at 103,
     reaches the broker at 108, the user at 119 -> latency 26; status 6 leaves
-    at 103 + 2e12 -> taskTime 2e12 + 26 (mqttApp2.cc:257-291)."""
+    at 103 + 2e12 -> taskTime 2e12 + 26 (mqttApp2.cc:257-291).  The ms signals
+    are emitted as (simTime() - created) * 1000: raw = 1000 x ticks here (exact
+    in double below 2^53); delay is emitted unscaled (raw = ticks)."""
     tr = dict(arrive=np.array([[100]], np.int64), req=np.array([[2000]], np.int32), mips=np.array([1000], np.int32),
               dl=np.array([3], np.int64), ul=np.array([5], np.int64), init=np.array([5], np.int64))
     o = ol.run_batch(**tr, user_ul=np.array([7]), user_dl=np.array([11]))
     u = o["user"][0]
-    got = {n: (int(u[n]["count"]), int(u[n]["min_ticks"]), int(u[n]["max_ticks"])) for n in ol.USER_SIGNALS}
-    assert got == {"delay": (1, 7, 7), "latencyH1": (1, 18, 18), "latency": (1, 26, 26),
-                   "taskTime": (1, 2 * 10**12 + 26, 2 * 10**12 + 26)}
+    got = {n: (int(u[n]["count"]), int(u[n]["min_raw"]), int(u[n]["max_raw"])) for n in ol.USER_SIGNALS}
+    assert got == {"delay": (1, 7, 7), "latencyH1": (1, 18000, 18000), "latency": (1, 26000, 26000),
+                   "taskTime": (1, (2 * 10**12 + 26) * 1000, (2 * 10**12 + 26) * 1000)}
 
 
 def test_user_side_events_do_not_change_decisions():
@@ -280,7 +282,8 @@ def test_replay_down_known_answers(case):
     for k in ("n_queued", "n_started", "busy_s", "events", "max_pending"):
         assert st[k] == exp[k], k
     assert st["n_tasks"] == len(exp["node"])
-    assert st["queue_sum_lo"] == exp["queue_sum_ms"] * 10**9 and st["queue_sum_hi"] == 0
+    # queueTime raw values = 1000 x the tick difference at these small ticks (exact round trip)
+    assert st["queue_sum_lo"] == exp["queue_sum_ms"] * 10**12 and st["queue_sum_hi"] == 0
     assert st["resp_sum_lo"] == exp["resp_sum_ms"] * 10**9 and st["resp_sum_hi"] == 0
 
 
@@ -331,3 +334,30 @@ def test_udiv_magic_exact():
         t = (m * nn) >> np.uint64(32)
         q = (t + ((nn - t) >> sh1)) >> sh2
         np.testing.assert_array_equal(q, nn // d)
+
+
+@pytest.mark.parametrize("case", golden_io.qtime_cases(), ids=lambda c: c[0])
+def test_qtime_known_answers(case):
+    """queueTime as the reference emits it (ComputeBrokerApp3.cc:238, 306): the
+    queueStartTime double round trip above 2^53 ticks, a negative value for a
+    task queued and started in one tick, and the simtime_t overflow above ~9223 s."""
+    name, tr, exp = case
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], hist=True)
+    for k in ("node", "status", "start", "done"):
+        np.testing.assert_array_equal(o[k][0], exp[k], err_msg=k)
+    golden_io.check_qtime_record(o["stats"][0], exp)
+    assert o["hist"][0][0].sum() == exp["n_qtime"]
+
+
+def test_qtime_raw_function():
+    # below 2^51 ticks the round trip is exact: raw = 1000 x the tick difference
+    assert ol.qtime_raw(5 * 10**12 + 7, 10**12) == (4 * 10**12 + 7) * 1000
+    assert ol.qtime_raw(2**54 + 3, 2**54 + 3) == -1000
+    assert ol.qtime_raw(10**16, 0) is None  # 10^4 s: (simTime() - qst) * 1000 leaves simtime_t's range
+    assert ol.ms_raw(26) == 26000 and ol.ms_raw(9224 * 10**12) is None
+
+
+def test_oracle_stats_layout_is_the_abi_layout():
+    from fognetsimpp_amd import _abi
+    assert ol.ORC_STATS_DTYPE.descr == _abi.REP_STATS_DTYPE.descr
+    assert ol.MOMENTS_DTYPE.descr == _abi.MOMENTS_DTYPE.descr

@@ -30,8 +30,9 @@ def assert_parity(tr, g, o):
     np.testing.assert_array_equal(st_g["status"], st_o["status"])
     for k in ("node", "status", "start", "done"):
         np.testing.assert_array_equal(g[k], o[k], err_msg=k)
-    for f in ("n_tasks", "n_queued", "n_started", "last_tick", "queue_min_ticks", "queue_max_ticks",
+    for f in ("n_tasks", "n_queued", "n_started", "last_tick", "queue_min_raw", "queue_max_raw",
               "resp_min_ticks", "resp_max_ticks", "queue_sum_lo", "queue_sum_hi", "queue_sq_lo", "queue_sq_hi",
+              "queue_sq_top", "n_qtime", "n_qtime_overflow",
               "resp_sum_lo", "resp_sum_hi", "resp_sq_lo", "resp_sq_hi", "events", "max_pending"):
         np.testing.assert_array_equal(st_g[f], st_o[f], err_msg=f)
 
@@ -242,11 +243,16 @@ def test_device_tracegen_sharding_offset(ctx):
 def job_from_reps(st):
     """Exact host reduction of rep stats (test-side), for comparison with the device."""
     ok = st[st["status"] == 0]
-    def u128(lo, hi):
-        return sum(int(a) | (int(b) << 64) for a, b in zip(lo, hi))
+    def u128(lo, hi, top=None):
+        return sum(int(a) | (int(b) << 64) | ((int(top[i]) << 128) if top is not None else 0)
+                   for i, (a, b) in enumerate(zip(lo, hi)))
+    def s128(lo, hi):  # two's complement 128-bit values, summed as Python ints, returned mod 2^192
+        v = sum((x - (1 << 128) if x >> 127 else x) for x in (int(a) | (int(b) << 64) for a, b in zip(lo, hi)))
+        return v % (1 << 192)
     return dict(n_reps=len(st), n_failed=int((st["status"] != 0).sum()), n_tasks=int(ok["n_tasks"].sum()),
-                n_queued=int(ok["n_queued"].sum()), queue_sum=u128(ok["queue_sum_lo"], ok["queue_sum_hi"]),
-                queue_sq=u128(ok["queue_sq_lo"], ok["queue_sq_hi"]), resp_sq=u128(ok["resp_sq_lo"], ok["resp_sq_hi"]),
+                n_queued=int(ok["n_queued"].sum()), queue_sum=s128(ok["queue_sum_lo"], ok["queue_sum_hi"]),
+                queue_sq=u128(ok["queue_sq_lo"], ok["queue_sq_hi"], ok["queue_sq_top"]),
+                resp_sq=u128(ok["resp_sq_lo"], ok["resp_sq_hi"]),
                 resp_max=int(ok["resp_max_ticks"].max()), max_pending=int(ok["max_pending"].max()))
 
 
@@ -303,6 +309,80 @@ def test_full_size_sweep_properties(ctx):
     np.testing.assert_array_equal(out.node[r].cpu().numpy(), o["node"][0])
     np.testing.assert_array_equal(out.done_tick[r].cpu().numpy(), o["done"][0])
     assert st[r].tobytes() == o["stats"][0].tobytes()
+
+
+@pytest.mark.parametrize("kernel", ["register", "wide"])
+@pytest.mark.parametrize("case", golden_io.qtime_cases(), ids=lambda c: c[0])
+def test_qtime_known_answers_gpu(ctx, monkeypatch, case, kernel):
+    """queueTime as the reference emits it (tests/golden/kat_qtime.json): the
+    queueStartTime double round trip above 2^53 ticks, a negative value, the
+    simtime_t overflow; both replay kernels, fused statistics and histogram."""
+    if kernel == "wide":
+        monkeypatch.setenv("FOGNET_REPLAY_KERNEL", "wide")
+    name, tr, exp = case
+    dev = torch.device("cuda", ctx.device)
+    out = fa.run_batch(ctx, fa.as_device_trace(tr, dev), hist=True)
+    torch.cuda.synchronize()
+    for k, g in (("node", out.node), ("status", out.status), ("start", out.start_tick), ("done", out.done_tick)):
+        np.testing.assert_array_equal(g[0].cpu().numpy(), exp[k], err_msg=k)
+    golden_io.check_qtime_record(out.rep_stats()[0], exp)
+    assert int(out.hist[0].sum()) == exp["n_qtime"]
+
+
+def _sharded_sample(ctx, seed, R_total, T, N, reps, ring, params):
+    """Replications `reps` (global indices) of a device-generated sweep job,
+    generated exactly as the bench's shards generate them (r0 = global index)."""
+    dev = torch.device("cuda", ctx.device)
+    outs = []
+    for r in reps:
+        mg, sc = params(np.array([r]), N)
+        d = fa.generate_trace(ctx, seed, 1, T, N, mg, sc, r0=int(r))
+        o = fa.run_batch(ctx, d, ring_capacity=ring, hist=False)
+        outs.append((d, o))
+    torch.cuda.synchronize()
+    return outs
+
+
+def test_c3_full_length_replications_bit_exact(ctx):
+    """Config C3 at its full length (T = 100,000, N = 256, seed 0x5EED0003,
+    ring 2048 as bench.py): 24 replications spread over the 4096-replication
+    sweep (every rho x latency class), all outputs and records bit-exact
+    against the oracle."""
+    T, N = 100_000, 256
+    reps = list(range(9)) + [1000, 1001, 1002, 2047, 2048, 2049, 3000, 3001, 3002, 4087, 4088, 4089, 4093, 4094, 4095]
+    outs = _sharded_sample(ctx, 0x5EED0003, 4096, T, N, reps, 2048, fa.sweep_params)
+    for r, (d, o) in zip(reps, outs):
+        h = {k: d[k][0].cpu().numpy() for k in ("arrive", "req", "mips", "dl", "ul", "init")}
+        ref = ol.run_batch(h["arrive"], h["req"], h["mips"], h["dl"], h["ul"], h["init"])
+        for k_gpu, k_ref in (("node", "node"), ("status", "status"), ("start_tick", "start"), ("done_tick", "done")):
+            np.testing.assert_array_equal(getattr(o, k_gpu)[0].cpu().numpy(), ref[k_ref][0], err_msg=f"{k_gpu} r={r}")
+        assert o.rep_stats()[0].tobytes() == ref["stats"][0].tobytes(), f"stats r={r}"
+
+
+def test_c4_workload_shape_matches_oracle(ctx):
+    """Config C4 (BASELINE.json configs[3]): T = 10,000, N = 256, seed
+    0x5EED0004, the sweep recipe, replications drawn from the whole
+    1,000,000-replication job (as the 8 GPU shards generate them), in one
+    batch of 256 like a bench block; every output and record against the oracle."""
+    T, N = 10_000, 256
+    rng = np.random.default_rng(4)
+    reps = np.sort(np.concatenate([np.arange(128), rng.choice(np.arange(128, 1_000_000), 128, replace=False)]))
+    dev = torch.device("cuda", ctx.device)
+    d = fa.allocate_trace(len(reps), T, N, dev)
+    for i, r in enumerate(reps):  # generate each at its global index, then replay them as one block
+        mg, sc = fa.sweep_params(np.array([r]), N)
+        one = fa.generate_trace(ctx, 0x5EED0004, 1, T, N, mg, sc, r0=int(r))
+        for k in ("arrive", "req", "mips", "dl", "ul", "init"):
+            d[k][i].copy_(one[k][0])
+    tr = {k: v for k, v in d.items() if not k.startswith("_")}
+    out = fa.run_batch(ctx, tr, ring_capacity=2048, hist=True)
+    torch.cuda.synchronize()
+    h = {k: tr[k].cpu().numpy() for k in tr}
+    ref = ol.run_batch(h["arrive"], h["req"], h["mips"], h["dl"], h["ul"], h["init"], threads=8, hist=True)
+    for k_gpu, k_ref in (("node", "node"), ("status", "status"), ("start_tick", "start"), ("done_tick", "done")):
+        np.testing.assert_array_equal(getattr(out, k_gpu).cpu().numpy(), ref[k_ref], err_msg=k_gpu)
+    assert out.rep_stats().tobytes() == ref["stats"].tobytes()
+    np.testing.assert_array_equal(out.hist.cpu().numpy(), ref["hist"].sum(axis=0))
 
 
 # ------------------------------------------------------------------ a10/a11 statistics and the EXT_LAT policy
@@ -498,7 +578,7 @@ def test_c5_large_topology_sample(ctx):
 
 def assert_user_parity(g_user, o_user):
     for n in ol.USER_SIGNALS:
-        for f in ("count", "min_ticks", "max_ticks", "sum_lo", "sum_hi", "sq_lo", "sq_hi"):
+        for f in ("count", "min_raw", "max_raw", "sum_lo", "sum_hi", "sq_lo", "sq_hi", "sq_top", "overflow"):
             np.testing.assert_array_equal(g_user[n][f], o_user[n][f], err_msg=f"{n}.{f}")
 
 

@@ -21,13 +21,13 @@ _abi.LIB_PATH = os.path.join(ROOT, "build", "prof2" if MODE == "time" else "prof
 import fognetsimpp_amd as fa  # noqa: E402
 
 FIELDS = [("n_queued", "iterations"), ("n_started", "advert_loop_iters"), ("last_tick", "adverts"),
-          ("queue_min_ticks", "scan_loads_lane"), ("queue_max_ticks", "run_end_node_k"),
+          ("queue_min_raw", "scan_loads_lane"), ("queue_max_raw", "run_end_node_k"),
           ("resp_min_ticks", "horizon_slots"), ("resp_max_ticks", "refills"), ("queue_sum_lo", "nh_reads_young"),
           ("queue_sum_hi", "nh_reads"), ("queue_sq_lo", "chunks"), ("queue_sq_hi", "run_end_horizon"),
           ("resp_sum_lo", "runs_pend0"), ("resp_sum_hi", "run_end_chunk"),
           ("resp_sq_lo", "resumed_runs"), ("busy_s", "fresh_same_k"), ("resp_sq_hi", "horizon_end_then_same_k")]
 TIME_FIELDS = [("n_queued", "cyc_chunk"), ("n_started", "cyc_adverts"), ("last_tick", "cyc_argmin"),
-               ("queue_min_ticks", "cyc_horizon"), ("queue_max_ticks", "cyc_run_scan"),
+               ("queue_min_raw", "cyc_horizon"), ("queue_max_raw", "cyc_run_scan"),
                ("resp_min_ticks", "cyc_stores"), ("resp_max_ticks", "cyc_node_update"),
                ("queue_sum_lo", "cyc_tail"), ("queue_sum_hi", "cyc_total"), ("queue_sq_lo", "cyc_advert_nh_wait"),
                ("queue_sq_hi", "cyc_horizon_nh_wait")]
