@@ -24,6 +24,13 @@ struct fognet_ctx {
 
 namespace {
 
+constexpr int kDefaultRing = 2048;
+// Workspace slots of the wide kernel when it replays the replications the
+// register kernel hands over (at most one wave per SIMD of the chip).
+constexpr int32_t kWideFallbackSlots = 1024;
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 int fail(fognet_ctx* c, int rc, const std::string& msg) {
   if (c) c->err = msg;
   return rc;
@@ -70,7 +77,7 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
     return fail(c, FOGNET_ERR_UNSUPPORTED, "the power model assumes nodes that stay up (down_tick with p_busy_w)");
   if (in->node_stride != 0 && in->node_stride != in->N)
     return fail(c, FOGNET_ERR_ARG, "node_stride must be 0 or N");
-  int q = in->ring_capacity ? in->ring_capacity : 1024;
+  int q = in->ring_capacity ? in->ring_capacity : kDefaultRing;
   if (q < 2 || (q & (q - 1)) != 0 || q > (1 << 15)) return fail(c, FOGNET_ERR_ARG, "ring_capacity must be a power of two in [2, 2^15]");
   int qlog = 0;
   while ((1 << qlog) < q) ++qlog;
@@ -126,7 +133,7 @@ const char* fognet_status_string(int s) {
     case FOGNET_ERR_STATE: return "self-message already scheduled";
     case FOGNET_ERR_DEVICE: return "HIP device error";
     case FOGNET_ERR_OOM: return "out of device memory";
-    case FOGNET_ERR_CAPACITY: return "pending-task ring capacity exceeded";
+    case FOGNET_ERR_CAPACITY: return "capacity exceeded";
     case FOGNET_ERR_UNSUPPORTED: return "unsupported configuration";
   }
   return "unknown status";
@@ -284,19 +291,33 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N);
     rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ws, "wide replay workspace");
     if (rc) return rc;
-    e = fognet::launch_replay_wide(a, c->ring, (hipStream_t)stream);
+    e = fognet::launch_replay_wide(a, c->ring, a.R, (hipStream_t)stream);
     return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "wide replay launch");
   }
   // both stages: the replay kernel runs the statistics pass as its epilogue
   a.fuse_stats = which == 3 ? 1 : 0;
   if (a.fuse_stats) which = 1;
   if (which & 1) {
+    // workspace: [hand-over counter | hand-over list [R] | pending-task rings, reused by the wide kernel's
+    // replay of the handed-over replications once the register kernel is done (stream order)]
     const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
-    rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ring_bytes, "ring workspace");
+    const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
+    const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
+    const size_t head = align256(256 + (size_t)a.R * sizeof(int32_t));
+    rc = ensure(c, (void**)&c->ring, &c->ring_bytes, head + (ring_bytes > fb_bytes ? ring_bytes : fb_bytes),
+                "ring workspace");
     if (rc) return rc;
-    a.ring = c->ring;
+    unsigned char* const base = reinterpret_cast<unsigned char*>(c->ring);
+    a.wide_count = reinterpret_cast<int32_t*>(base);
+    a.wide_list = reinterpret_cast<int32_t*>(base + 256);
+    a.ring = reinterpret_cast<fognet::RingEntry*>(base + head);
+    e = hipMemsetAsync(a.wide_count, 0, sizeof(int32_t), (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(c, e, "hand-over counter");
     e = fognet::launch_replay(a, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "replay launch");
+    // the handed-over replications (usually none: every workgroup leaves at once)
+    e = fognet::launch_replay_wide(a, base + head, slots, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(c, e, "wide hand-over launch");
   }
   if (which & 2) {
     e = fognet::launch_rep_stats(a, (hipStream_t)stream);

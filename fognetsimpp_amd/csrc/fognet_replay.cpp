@@ -537,6 +537,8 @@ Options parse_args(int argc, char** argv) {
   if (o.world < 1 || o.rank < 0 || o.rank >= o.world) die("--world / --rank: need 0 <= rank < world");
   if (o.world > 1 && o.comm_id.empty()) die("--world > 1 needs --comm-id FILE (the communicator id's rendezvous)");
   if (o.reps < o.world) die("--reps must be >= --world (every rank replays a block of replications)");
+  if (o.ring != 0 && (o.ring < 2 || o.ring > (1 << 15) || (o.ring & (o.ring - 1)) != 0))
+    die("--ring must be a power of two in [2, 32768]");
   return o;
 }
 
@@ -546,6 +548,46 @@ Options parse_args(int argc, char** argv) {
 // The job record of all ranks (fognet_allreduce_stats over the library's RCCL
 // communicator); the 128-byte id goes from rank 0 to the others through the
 // file o.comm_id (written atomically, removed once every rank has joined).
+// Before any rank enters RCCL (whose communicator set-up waits for every rank
+// without a timeout), the ranks agree through files o.comm_id + ".rank<k>"
+// that every one of them finished its replay: a rank that failed (no device,
+// a library error) writes "fail" instead of dying, and then no rank calls a
+// collective.  Returns false if a rank failed or did not report within 300 s.
+bool ranks_ready(const Options& o, bool local_ok) {
+  auto name = [&](int k) { return o.comm_id + ".rank" + std::to_string(k); };
+  const std::string tmp = name(o.rank) + ".tmp";
+  FILE* f = std::fopen(tmp.c_str(), "w");
+  if (!f || std::fputs(local_ok ? "ok" : "fail", f) < 0 || std::fclose(f) != 0 ||
+      std::rename(tmp.c_str(), name(o.rank).c_str()) != 0)
+    die("cannot write " + name(o.rank));
+  bool all_ok = local_ok;
+  for (int k = 0; k < o.world; ++k) {
+    char buf[8] = {0};
+    for (int waited = 0;; waited += 50) {
+      FILE* g = std::fopen(name(k).c_str(), "r");
+      if (g) {
+        const size_t got = std::fread(buf, 1, sizeof buf - 1, g);
+        std::fclose(g);
+        if (got > 0) break;
+      }
+      if (waited > 300000) {
+        std::fprintf(stderr, "fognet_replay: rank %d: no report from rank %d after 300 s\n", o.rank, k);
+        return false;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+    if (std::strcmp(buf, "ok") != 0) {
+      std::fprintf(stderr, "fognet_replay: rank %d: rank %d failed; skipping the statistics exchange\n", o.rank, k);
+      all_ok = false;
+    }
+  }
+  return all_ok;
+}
+
+void remove_rank_files(const Options& o) {
+  for (int k = 0; k < o.world; ++k) std::remove((o.comm_id + ".rank" + std::to_string(k)).c_str());
+}
+
 void exchange_stats(const Options& o, fognet_ctx* ctx, fognet_job_stats* job, std::vector<int64_t>& hist) {
   uint8_t id[FOGNET_COMM_ID_BYTES];
   if (o.rank == 0) {
@@ -568,7 +610,10 @@ void exchange_stats(const Options& o, fognet_ctx* ctx, fognet_job_stats* job, st
   }
   fognet_comm* comm = nullptr;
   check_ctx(ctx, fognet_comm_create(ctx, o.world, o.rank, id, &comm), "fognet_comm_create");
-  if (o.rank == 0) std::remove(o.comm_id.c_str());  // every rank has joined
+  if (o.rank == 0) {  // every rank has joined (and read every rank's report)
+    std::remove(o.comm_id.c_str());
+    remove_rank_files(o);
+  }
   int64_t* d_hist = nullptr;
   const size_t hb = hist.size() * sizeof(int64_t);
   hip_check(hipMalloc((void**)&d_hist, hb), "hipMalloc");
@@ -586,10 +631,29 @@ int run_v3(const Options& o, fognet_batch_in in, const std::string& network, con
   std::vector<int64_t> start(RT), done(RT), hist((size_t)FOGNET_HIST_METRICS * FOGNET_HIST_BINS, 0);
   std::vector<fognet_rep_stats> stats(in.R);
   fognet_batch_out out{node.data(), status.data(), start.data(), done.data(), stats.data(), nullptr, hist.data()};
+  // status -1: "not replayed"; fognet_run_batch fails before any replay
+  // (invalid batch, device error) or reports the first failed replication
+  for (fognet_rep_stats& s : stats) s.status = -1;
   fognet_ctx* ctx = nullptr;
-  if (fognet_create(&ctx, o.device) != FOGNET_OK) die("fognet_create: no gfx950 device " + std::to_string(o.device));
-  const int rc = fognet_run_batch(ctx, &in, &out);
-  if (rc != FOGNET_OK && rc != FOGNET_ERR_ARG && rc != FOGNET_ERR_CAPACITY) check_ctx(ctx, rc, "fognet_run_batch");
+  std::string local_err;
+  if (fognet_create(&ctx, o.device) != FOGNET_OK) {
+    local_err = "fognet_create: no gfx950 device " + std::to_string(o.device);
+    ctx = nullptr;
+  } else {
+    const int rc = fognet_run_batch(ctx, &in, &out);
+    bool replayed = true;
+    for (const fognet_rep_stats& s : stats) replayed = replayed && s.status != -1;
+    if (rc != FOGNET_OK && !replayed)
+      local_err = std::string("fognet_run_batch: ") + fognet_status_string(rc) + ": " + fognet_last_error(ctx);
+  }
+  if (o.comm_id.empty() && !local_err.empty()) die(local_err);
+  if (!o.comm_id.empty()) {  // a failed rank reports instead of dying: no rank may be left in RCCL
+    if (!local_err.empty()) std::fprintf(stderr, "fognet_replay: rank %d: %s\n", o.rank, local_err.c_str());
+    if (!ranks_ready(o, local_err.empty())) {
+      if (ctx) fognet_destroy(ctx);
+      return 1;
+    }
+  }
   fognet_job_stats job;
   fognet_job_stats_init(&job);
   for (const fognet_rep_stats& s : stats) fognet_job_stats_add_rep(&job, &s);
@@ -600,17 +664,24 @@ int run_v3(const Options& o, fognet_batch_in in, const std::string& network, con
     return local_failed ? 1 : 0;
   }
   if (!o.sca.empty()) check(fognet_write_sca(o.sca.c_str(), run_id.c_str(), network.c_str(), &job, hist.data()), "sca");
-  if (!o.vec.empty())
+  if (!o.vec.empty()) {  // replication 0's vectors (a failed replication has no complete outputs)
+    if (stats[0].status != FOGNET_OK)
+      die(std::string("--vec: replication 0 failed: ") + fognet_status_string(stats[0].status));
     check(fognet_write_vec(o.vec.c_str(), run_id.c_str(), network.c_str(), in.T, in.N, in.arrive_tick, in.dl_tick,
                            node.data(), status.data(), start.data(), nullptr),
           "vec");
+  }
   if (!o.quiet) {
     std::printf("policy=%s R=%d T=%d N=%d decisions=%" PRId64 " queued=%" PRId64 " started=%" PRId64
                 " failed_reps=%" PRId64 " makespan_ticks=%" PRId64 " max_pending=%" PRId64 "\n",
                 in.policy == FOGNET_POLICY_EXT_LAT ? "EXT_LAT" : "REF_V3", in.R, in.T, in.N, job.n_tasks, job.n_queued,
                 job.n_started, job.n_failed, job.last_tick, job.max_pending);
-    std::vector<int64_t> per(in.N, 0);
-    for (int32_t k : node) ++per[k];
+    std::vector<int64_t> per(in.N, 0);  // completed replications only (a failed one stops mid-trace)
+    for (int32_t r = 0; r < in.R; ++r) {
+      if (stats[r].status != FOGNET_OK) continue;
+      for (size_t i = (size_t)r * in.T; i < (size_t)(r + 1) * in.T; ++i)
+        if (node[i] >= 0 && node[i] < in.N) ++per[node[i]];
+    }
     std::printf(o.world > 1 ? "tasks_per_node(rank 0)=" : "tasks_per_node=");
     for (int k = 0; k < in.N; ++k) std::printf("%s%" PRId64, k ? "," : "", per[k]);
     std::printf("\n");

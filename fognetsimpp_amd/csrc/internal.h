@@ -175,7 +175,17 @@ struct ReplayArgs {
   double* out_energy;     // [R][N] (nullable)
   int64_t* hist;          // [FOGNET_HIST_METRICS][FOGNET_HIST_BINS], added to (nullable)
   const int64_t* down;    // [R|1][N] node crash ticks (nullable; wide kernel only)
+  // Replications the register kernel hands to the wide kernel (a node past the
+  // ring capacity, or a service time past max_s): the register kernel appends
+  // r to wide_list (wide_count: device counter, zeroed before it); the wide
+  // kernel, launched with wide_list set, replays exactly the listed ones.
+  int32_t* wide_list;     // [R] (nullable: no hand-over, kNeedsWide stays the status)
+  int32_t* wide_count;
 };
+
+// Internal per-replication status between the two replay kernels (never
+// returned: the wide kernel overwrites the record of every listed replication).
+constexpr int32_t kNeedsWide = 0x57494445;
 
 // FOGNET_HIST_BINS rule (fognet_hip.h): whole milliseconds, log2 bins.
 __device__ __forceinline__ int hist_bin(int64_t ticks) {
@@ -223,7 +233,10 @@ constexpr int kWideMaxNodes = 65536;  // LDS: 82 KiB of group minima
 size_t replay_wide_lds_bytes(int32_t N);
 // workspace: R*T WideEntry followed by R*N WideNode
 size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N);
-hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, hipStream_t s);
+// slots: workspace slots (workgroups).  With a.wide_list unset, slots == R and
+// workgroup r replays replication r; with it set, the workgroups take the
+// listed replications in turn (slots <= R bounds the workspace).
+hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slots, hipStream_t s);
 
 hipError_t launch_replay(const ReplayArgs& a, hipStream_t s);
 hipError_t launch_rep_stats(const ReplayArgs& a, hipStream_t s);

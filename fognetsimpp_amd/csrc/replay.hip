@@ -825,12 +825,13 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
       //    shifts and row broadcasts fill invalid sources with them.
       uint32_t S = 0u;
       int64_t a = 0, dd = 0;
-      bool lerr = false;
+      bool lerr = false, lwide = false;
       if (in_run) {
         S = udiv((uint32_t)cr, div_k);  // double tskTime = requiredMIPS / MIPS (:276)
         a = ca + dl_k;
         dd = (int64_t)S * kTicksPerSecond;
-        lerr = S > A.max_s || a > kMaxTick;
+        lerr = a > kMaxTick;
+        lwide = S > A.max_s;  // beyond this kernel's 24-bit busy key: the wide kernel replays it
       }
       //    Unrolled: with P_m = sum_{i<=m} S_i 1e12 (a prefix sum) and
       //    X_m = a_m - P_{m-1},  done_m = max(done_before_run, max_{i<=m} X_i) + P_m,
@@ -873,8 +874,11 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
         err = FOGNET_ERR_ARG;
         break;
       }
-      if (pend_k + (uint32_t)L - 1u > qmask) {
-        err = FOGNET_ERR_CAPACITY;
+      // a node with more than ring-capacity pending tasks, or a service time
+      // the 24-bit busy key cannot hold: hand the replication to the wide
+      // kernel (unbounded per-node chains), which replays it from the start
+      if (ballot(lwide) || pend_k + (uint32_t)L - 1u > qmask) {
+        err = kNeedsWide;
         break;
       }
       TMARK(4)
@@ -951,6 +955,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
   uint64_t p_scan = 0;
   for (int l = 0; l < kWave; ++l) p_scan += readlane_u32(scan, l);
 #endif
+  if (lane == 0 && err == kNeedsWide && A.wide_list) A.wide_list[atomicAdd(A.wide_count, 1)] = r;
   if (lane == 0 && A.out_stats) {
     fognet_rep_stats* S = A.out_stats + r;
     S->n_tasks = n_done;
@@ -990,7 +995,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
 #endif
   }
 #if !defined(FOGNET_REPLAY_PROFILE) || FOGNET_REPLAY_PROFILE == 0
-  if (A.fuse_stats && A.out_stats) {
+  if (A.fuse_stats && A.out_stats && err != kNeedsWide) {
     // ---- statistics epilogue (rep_stats_kernel's pass, fused).  The wave
     // re-reads its own replication's outputs; task c0 + l was stored by lane
     // l, and lane l reads tasks l, l + 64, ... (its own stores).  The loop's

@@ -190,11 +190,33 @@ __host__ __device__ __forceinline__ WideWs wide_ws(int32_t R, int32_t T, int32_t
 }
 
 template <int POL>
+__device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
+                                                int64_t* VN, uint32_t* VB, unsigned char* w_lds);
+
+// One replication per workgroup (r = blockIdx.x), or, with A.wide_list set,
+// the replications the register kernel handed over, taken in turn by the
+// workgroups (workspace slot = blockIdx.x); every workgroup leaves when the
+// list (complete before this launch, stream order) is exhausted.
+template <int POL>
 __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry* E, WideNode* ND, int64_t* VN,
                                                          uint32_t* VB) {
-  constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
   extern __shared__ __align__(16) unsigned char w_lds[];
-  const int r = blockIdx.x;
+  if (A.wide_list == nullptr) {
+    replay_wide_rep<POL>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, w_lds);
+    return;
+  }
+  const int n = *A.wide_count;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    replay_wide_rep<POL>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, w_lds);
+    __syncthreads();  // LDS reuse by the next replication
+  }
+}
+
+// Replication r with workspace slot wr.
+template <int POL>
+__device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
+                                                int64_t* VN, uint32_t* VB, unsigned char* w_lds) {
+  constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
   const int lane = threadIdx.x;
   const int T = A.T, N = A.N;
   WideLds L;
@@ -204,11 +226,11 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
   L.g_j = reinterpret_cast<int32_t*>(L.g_key + L.G * kWave);
   L.hist = reinterpret_cast<uint32_t*>(L.g_j + L.G * kWave);
   const int SP = L.G * kWideGroupSlots;
-  const WideView V{VN + ((size_t)r * kWave + lane) * SP, VB + ((size_t)r * kWave + lane) * SP};
+  const WideView V{VN + ((size_t)wr * kWave + lane) * SP, VB + ((size_t)wr * kWave + lane) * SP};
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)T;
-  WideEntry* const e = E + tbase;
-  WideNode* const nd = ND + (size_t)r * (size_t)N;
+  WideEntry* const e = E + (size_t)wr * (size_t)T;
+  WideNode* const nd = ND + (size_t)wr * (size_t)N;
   const bool hist = A.hist != nullptr;
   const int64_t arrive0 = T > 0 ? A.arrive[tbase] : kNever;
 
@@ -470,9 +492,9 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
 }
 
 template <int POL>
-void launch_wide_pol(const ReplayArgs& a, WideEntry* e, WideNode* nd, int64_t* vn, uint32_t* vb, size_t lds,
-                     hipStream_t s) {
-  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(a.R), dim3(kWave), lds, s, a, e, nd, vn, vb);
+void launch_wide_pol(const ReplayArgs& a, int32_t slots, WideEntry* e, WideNode* nd, int64_t* vn, uint32_t* vb,
+                     size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb);
 }
 
 }  // namespace
@@ -485,8 +507,8 @@ size_t replay_wide_lds_bytes(int32_t N) {
 
 size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N) { return wide_ws(R, T, N).bytes; }
 
-hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, hipStream_t s) {
-  const WideWs w = wide_ws(a.R, a.T, a.N);
+hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slots, hipStream_t s) {
+  const WideWs w = wide_ws(slots, a.T, a.N);
   unsigned char* const base = static_cast<unsigned char*>(workspace);
   WideEntry* const e = reinterpret_cast<WideEntry*>(base + w.e_off);
   WideNode* const nd = reinterpret_cast<WideNode*>(base + w.nd_off);
@@ -494,9 +516,9 @@ hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, hipStream_t 
   uint32_t* const vb = reinterpret_cast<uint32_t*>(base + w.busy_off);
   const size_t lds = replay_wide_lds_bytes(a.N);
   if (a.policy == FOGNET_POLICY_EXT_LAT)
-    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, e, nd, vn, vb, lds, s);
+    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, slots, e, nd, vn, vb, lds, s);
   else
-    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, e, nd, vn, vb, lds, s);
+    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, slots, e, nd, vn, vb, lds, s);
   return hipGetLastError();
 }
 

@@ -65,7 +65,7 @@ typedef enum fognet_status {
     FOGNET_ERR_STATE = 4,       /* selfMsg already scheduled: ComputeBrokerApp3.cc:301 cRuntimeError   */
     FOGNET_ERR_DEVICE = 5,      /* HIP runtime failure or no gfx950 device                             */
     FOGNET_ERR_OOM = 6,
-    FOGNET_ERR_CAPACITY = 7,    /* a node had more than ring_capacity tasks pending                    */
+    FOGNET_ERR_CAPACITY = 7,    /* v2 queue_capacity exceeded, or an advertised busy time past 2^32 - 1 s */
     FOGNET_ERR_UNSUPPORTED = 8  /* configuration not implemented (e.g. N > 256, unknown policy)        */
 } fognet_status;
 
@@ -165,7 +165,12 @@ typedef struct fognet_batch_in {
     int32_t R, T, N;
     int32_t policy;           /* fognet_policy                                                    */
     int32_t node_stride;      /* 0: node params shared by all replications; N: one row each       */
-    int32_t ring_capacity;    /* per-node pending capacity, power of two (0 = default 1024)      */
+    int32_t ring_capacity;    /* per-node pending-task ring of the register-resident replay kernel
+                                 (N <= 256), power of two in [2, 2^15] (0 = default 2048).  Not a
+                                 limit on the inputs: a replication with a node past it (or with a
+                                 service time past 2^24 / ring_capacity s) is replayed again from
+                                 the start by the wide kernel, whose per-node chains are unbounded,
+                                 inside the same call.  Only sizes the workspace and the common path. */
     const int64_t *arrive_tick;   /* [R][T] publish arrival at the broker, nondecreasing          */
     const int32_t *req_mips;      /* [R][T] MqttMsgPublish.MIPSRequired, >= 0                      */
     const int32_t *mips;          /* [R|1][N] node MIPS (> 0), CONNECT order = index order         */

@@ -179,3 +179,36 @@ def test_driver_stats_exchange_world1(ctx, tmp_path):
     drive("-f", INI, "--users", "user[10]", "--reps", "4", "--sca", b, "--comm-id", cid)
     assert open(a).read() == open(b).read()
     assert not os.path.exists(cid)
+
+
+def test_ring_must_be_power_of_two():
+    p = drive("-f", INI, "--users", "user[2]", "--ring", "1000", "--dry-run", check=False)
+    assert p.returncode == 2 and "--ring must be a power of two" in p.stderr
+
+
+@pytest.mark.skipif(__import__("torch").cuda.is_available(), reason="needs ranks that cannot open a device")
+def test_failed_ranks_do_not_hang(tmp_path):
+    """world 2 where no rank can open a gfx950 device (this CPU container): each
+    rank reports the failure through the rendezvous files instead of entering
+    RCCL, and both exit 1 promptly (no rank is left waiting in a collective)."""
+    cid = str(tmp_path / "comm.id")
+    procs = [subprocess.Popen([DRIVER, "-f", INI, "--users", "user[2]", "--reps", "2", "--world", "2", "--rank", str(k),
+                               "--comm-id", cid], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for k in range(2)]
+    for p in procs:
+        _, err = p.communicate(timeout=60)
+        assert p.returncode == 1, err
+        assert "failed; skipping the statistics exchange" in err
+
+
+@pytest.mark.gpu
+def test_driver_tiny_ring_same_results(ctx, tmp_path):
+    """--ring 4: replications with a node past 4 pending tasks are handed to the
+    wide kernel; the run completes with the same .sca as the default ring."""
+    a, b = str(tmp_path / "a.sca"), str(tmp_path / "b.sca")
+    out_a = drive("-f", INI, "--users", "user[10]", "--reps", "4", "--sca", a).stdout
+    out_b = drive("-f", INI, "--users", "user[10]", "--reps", "4", "--sca", b, "--ring", "4").stdout
+    assert "failed_reps=0" in out_b
+    assert open(a).read() == open(b).read()
+    mp = int(out_a.split("max_pending=")[1].split()[0])
+    assert mp > 4, "the scenario must overflow a 4-entry ring"

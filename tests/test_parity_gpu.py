@@ -177,13 +177,41 @@ def test_shared_node_params_and_empty_trace(ctx):
     assert (g["stats"]["status"] == 0).all() and (g["stats"]["n_tasks"] == 0).all()
 
 
-def test_ring_capacity_exceeded(ctx):
-    tr = tg.make_batch(11, 1, 4, 2000, rho=3.0)  # overload: queues grow without bound
-    g = run_gpu(ctx, tr, ring_capacity=16)
-    assert g["stats"]["status"][0] == _abi.FOGNET_ERR_CAPACITY
-    g = run_gpu(ctx, tr, ring_capacity=4096)
-    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"])
+@pytest.mark.parametrize("ring", [4, 16, 4096])
+def test_ring_capacity_exceeded(ctx, ring):
+    """An overloaded trace (queues grow without bound) completes whatever the
+    ring capacity: replications past it are replayed by the wide kernel inside
+    the same call.  A mixed batch (3 overloaded replications among light ones),
+    bit-exact against the oracle, histogram included."""
+    over = tg.make_batch(11, 3, 4, 2000, rho=3.0)
+    light = tg.make_batch(12, 5, 4, 2000, rho=0.3)
+    tr = {k: np.concatenate([light[k][:2], over[k], light[k][2:]]) for k in over}
+    g = run_gpu_full(ctx, tr, ring_capacity=ring)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8, hist=True)
+    assert (g["stats"]["status"] == 0).all()
+    assert g["stats"]["max_pending"].max() > ring or ring == 4096
     assert_parity(tr, g, o)
+    np.testing.assert_array_equal(g["hist"], o["hist"].sum(axis=0))
+
+
+def test_service_past_register_kernel_bound(ctx):
+    """Service times past the register kernel's bound (2^24 / ring capacity s,
+    8191 s at the default ring) up to the wide kernel's 65535 s: handed over,
+    same results as the oracle; the separate statistics pass agrees."""
+    tr = tg.make_batch(13, 4, 8, 600, rho=0.5)
+    tr = {k: v.copy() for k, v in tr.items()}
+    tr["req"][1, 10] = 9000 * int(tr["mips"][1, 0])  # 9000 s on node 0
+    tr["req"][3, ::50] = 60000 * 1000  # up to 60,000 s
+    g = run_gpu_full(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=4, hist=True)
+    assert (g["stats"]["status"] == 0).all()
+    assert_parity(tr, g, o)
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(tr, dev)
+    sep = fa.run_batch(ctx, d, stage="replay")
+    fa.run_batch(ctx, d, out=sep, stage="stats")
+    torch.cuda.synchronize()
+    assert sep.rep_stats().tobytes() == g["stats"].tobytes()
 
 
 @pytest.mark.parametrize("N", [16, 300])  # register-resident and wide kernel
