@@ -159,7 +159,8 @@ def main():
         job_buf = torch.zeros(_abi.JOB_STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         ctx.check(ctx._lib.fognet_reduce_stats_dev(ctx.handle, fa.engine._ptr(out.stats), R,
                                                    fa.engine._ptr(job_buf), fa.engine._stream_ptr(dev)), "reduce")
-        energy = job_buf[-8:].view(torch.float64).clone()  # fognet_job_stats.energy_j (last field)
+        eo = _abi.JOB_STATS_DTYPE.fields["energy_j"][1]
+        energy = job_buf[eo:eo + 8].view(torch.float64).clone()  # fognet_job_stats.energy_j
         if dist is not None:
             gathered = [torch.empty_like(job_buf) for _ in range(world)]
             dist.all_gather(gathered, job_buf)
@@ -246,6 +247,7 @@ def main():
             "cpu_baseline": cpu,
             "failed_replications": failed,
             "stats": {"queueTime_ms_mean": summary["queueTime_ms"].get("mean"),
+                      "queueTime_overflows": summary["queueTime_ms"].get("overflow"),
                       "response_ms_mean": summary["response_ms"].get("mean"),
                       "max_pending": summary["max_pending"], "decisions": summary["decisions"],
                       "energy_j": float(energy[0]), "busy_s": summary["busy_s"],
@@ -498,12 +500,14 @@ def cpu_baseline(trace, args, R, T, N, out=None):
 
     reps = min(args.cpu_reps, R)
     h = {k: trace[k][:reps].cpu().numpy() for k in ("arrive", "req", "mips", "dl", "ul", "init")}
+    # the power model rides along when the device run used it (energy_j is part of the record compared)
+    pw = {k: trace[k][:reps].cpu().numpy() for k in ("p_busy", "p_idle")} if "p_busy" in trace else {}
     model, nproc, avail, cores = host_cpu_info()
     threads = max(1, min(args.cpu_threads, cores)) if args.cpu_threads > 0 else cores
     log(f"cpu baseline: {reps} replications on {threads} threads (host {nproc} CPUs, {avail} in this job's mask) ...")
     t0 = time.perf_counter()
     o = oracle_lib.run_batch(h["arrive"], h["req"], h["mips"], h["dl"], h["ul"], h["init"], threads=threads,
-                             outputs=True)
+                             outputs=True, **pw)
     dt = time.perf_counter() - t0
     ok = int((o["stats"]["status"] == 0).sum())
     parity = None

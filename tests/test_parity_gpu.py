@@ -444,7 +444,9 @@ def test_energy_and_histograms_match_oracle(ctx, shared):
     np.testing.assert_array_equal(g["energy"], o["node_energy"])
     assert g["stats"].tobytes() == o["stats"].tobytes()
     np.testing.assert_array_equal(g["hist"], o["hist"].sum(axis=0))
-    assert g["hist"][0].sum() == o["stats"]["n_queued"].sum() and g["hist"][1].sum() == 12 * 3000
+    # queueTime: one count per emission the reference can make (the rest overflow simtime_t)
+    assert g["hist"][0].sum() == o["stats"]["n_qtime"].sum() and g["hist"][1].sum() == 12 * 3000
+    assert (o["stats"]["n_qtime"] + o["stats"]["n_qtime_overflow"] == o["stats"]["n_queued"]).all()
     job = fa.reduce_stats(ctx, g["raw"].stats, 12)
     assert int(job["busy_s"]) == int(o["stats"]["busy_s"].sum())
     np.testing.assert_allclose(float(job["energy_j"]), float(o["stats"]["energy_j"].sum()), rtol=1e-12)
