@@ -173,6 +173,7 @@ SIGNATURES = {
     "fognet_destroy": (None, [P]),
     "fognet_last_error": (C.c_char_p, [P]),
     "fognet_decide": (C.c_int, [P, C.c_int, C.c_int32, P, P, C.c_int32, C.POINTER(C.c_int32)]),
+    "fognet_decide_window": (C.c_int, [P, C.c_int, C.c_int32, P, P, C.c_int32, P, P]),
     "fognet_decide_batch_dev": (C.c_int, [P, C.c_int, C.c_int64, C.c_int32, P, P, P, P, P, P]),
     "fognet_decide_v2": (C.c_int, [P, C.c_int32, P, C.c_int32, C.c_int32, C.POINTER(C.c_int32),
                                    C.POINTER(C.c_int32)]),

@@ -16,9 +16,14 @@ struct fognet_ctx {
   hipStream_t stream = nullptr;  // private stream for the host-buffer entry points
   fognet::RingEntry* ring = nullptr;
   size_t ring_bytes = 0;
-  // scratch for fognet_decide
+  // scratch for the v2 scalar decision
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  // mapped, coherent host memory for fognet_decide / fognet_decide_window:
+  // inputs the kernel reads and results it writes without copies
+  void* host_stage = nullptr;
+  void* host_stage_dev = nullptr;
+  size_t host_stage_bytes = 0;
   std::string err;
 };
 
@@ -54,6 +59,25 @@ int ensure(fognet_ctx* c, void** p, size_t* have, size_t want, const char* what)
                 std::string("hipMalloc ") + what + ": " + hipGetErrorString(e));
   }
   *have = want;
+  return FOGNET_OK;
+}
+
+int ensure_host(fognet_ctx* c, size_t want) {
+  if (c->host_stage_bytes >= want) return FOGNET_OK;
+  if (c->host_stage) {
+    (void)hipHostFree(c->host_stage);
+    c->host_stage = c->host_stage_dev = nullptr;
+    c->host_stage_bytes = 0;
+  }
+  want = want < 4096 ? 4096 : want;
+  hipError_t e = hipHostMalloc(&c->host_stage, want, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(&c->host_stage_dev, c->host_stage, 0);
+  if (e != hipSuccess) {
+    if (c->host_stage) (void)hipHostFree(c->host_stage);
+    c->host_stage = c->host_stage_dev = nullptr;
+    return fail(c, FOGNET_ERR_OOM, std::string("hipHostMalloc decide stage: ") + hipGetErrorString(e));
+  }
+  c->host_stage_bytes = want;
   return FOGNET_OK;
 }
 
@@ -165,6 +189,7 @@ void fognet_destroy(fognet_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->ring) (void)hipFree(c->ring);
   if (c->scratch) (void)hipFree(c->scratch);
+  if (c->host_stage) (void)hipHostFree(c->host_stage);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -189,37 +214,92 @@ int fognet_decide_batch_dev(fognet_ctx* c, int policy, int64_t m, int32_t n, con
     return fail(c, FOGNET_ERR_ARG, "null pointer");
   int rc = set_device(c);
   if (rc) return rc;
-  hipError_t e = fognet::launch_decide(m, n, adv_busy, adv_mips, req, out_node, out_status, (hipStream_t)stream);
+  hipError_t e = fognet::launch_decide(m, n, n, adv_busy, adv_mips, req, out_node, out_status, (hipStream_t)stream);
   return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "decide launch");
 }
 
 int fognet_decide(fognet_ctx* c, int policy, int32_t n, const double* adv_busy, const int32_t* adv_mips,
                   int32_t req_mips, int32_t* out_node) {
   if (!c || !out_node) return FOGNET_ERR_ARG;
+  if (policy != FOGNET_POLICY_REF_V3) return fail(c, FOGNET_ERR_UNSUPPORTED, "fognet_decide: policy REF_V3 only");
   if (n <= 0) return fail(c, FOGNET_ERR_NO_NODES, "n <= 0 (BrokerBaseApp3.cc:268 reads brokers[0])");
   if (!adv_busy || !adv_mips) return fail(c, FOGNET_ERR_ARG, "null view");
   int rc = set_device(c);
   if (rc) return rc;
-  const size_t nb = (size_t)n * sizeof(double), nm = (size_t)n * sizeof(int32_t);
-  const size_t off_m = (nb + 255) & ~(size_t)255, off_r = (off_m + nm + 255) & ~(size_t)255;
-  const size_t off_o = off_r + 256, total = off_o + 256;
-  rc = ensure(c, &c->scratch, &c->scratch_bytes, total, "decide scratch");
+  // result words at the stage's start; a view too large for the kernel arguments follows them and is
+  // moved to device scratch by one DMA copy (the kernel would read it over the link at one wave's pace)
+  const size_t far = n > fognet::kDecideArgNodes ? (size_t)n * sizeof(double) : 0;
+  rc = ensure_host(c, 256 + far);
   if (rc) return rc;
-  char* s = (char*)c->scratch;
-  hipError_t e;
-  if ((e = hipMemcpyAsync(s, adv_busy, nb, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
-      (e = hipMemcpyAsync(s + off_m, adv_mips, nm, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
-      (e = hipMemcpyAsync(s + off_r, &req_mips, sizeof(int32_t), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+  if (far) {
+    rc = ensure(c, &c->scratch, &c->scratch_bytes, far, "decide scratch");
+    if (rc) return rc;
+  }
+  fognet::DecideArgs a;
+  a.n = n;
+  a.mips0 = adv_mips[0];  // the policy reads brokers[0]->getMips() only (BrokerBaseApp3.cc:268,273)
+  a.req = req_mips;
+  a.pad = 0;
+  unsigned char* const h = static_cast<unsigned char*>(c->host_stage);
+  unsigned char* const d = static_cast<unsigned char*>(c->host_stage_dev);
+  if (far) memcpy(h + 256, adv_busy, far);
+  else memcpy(a.busy, adv_busy, (size_t)n * sizeof(double));
+  volatile int32_t* res = reinterpret_cast<volatile int32_t*>(h);
+  res[0] = -1;
+  res[1] = FOGNET_ERR_DEVICE;
+  hipError_t e = hipSuccess;
+  if (far && (e = hipMemcpyAsync(c->scratch, h + 256, far, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
     return hip_fail(c, e, "decide copy-in");
-  e = fognet::launch_decide(1, n, (const double*)s, (const int32_t*)(s + off_m), (const int32_t*)(s + off_r),
-                            (int32_t*)(s + off_o), (int32_t*)(s + off_o + 4), c->stream);
+  e = fognet::launch_decide_args(a, static_cast<const double*>(c->scratch), reinterpret_cast<int32_t*>(d), c->stream);
   if (e != hipSuccess) return hip_fail(c, e, "decide launch");
-  int32_t res[2] = {-1, FOGNET_ERR_DEVICE};
-  if ((e = hipMemcpyAsync(res, s + off_o, sizeof res, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-      (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-    return hip_fail(c, e, "decide copy-out");
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e, "decide sync");
   if (res[1] != FOGNET_OK) return fail(c, res[1], fognet_status_string(res[1]));
   *out_node = res[0];
+  return FOGNET_OK;
+}
+
+int fognet_decide_window(fognet_ctx* c, int policy, int32_t n, const double* adv_busy, const int32_t* adv_mips,
+                         int32_t m, const int32_t* req_mips, int32_t* out_node) {
+  if (!c || m < 0 || (m > 0 && (!out_node || !req_mips))) return fail(c, FOGNET_ERR_ARG, "decide_window: bad argument");
+  if (policy != FOGNET_POLICY_REF_V3) return fail(c, FOGNET_ERR_UNSUPPORTED, "decide_window: policy REF_V3 only");
+  if (m == 0) return FOGNET_OK;
+  if (n <= 0) return fail(c, FOGNET_ERR_NO_NODES, "n <= 0 (BrokerBaseApp3.cc:268 reads brokers[0])");
+  if (!adv_busy || !adv_mips) return fail(c, FOGNET_ERR_ARG, "null view");
+  int rc = set_device(c);
+  if (rc) return rc;
+  // stage: [node m][status m][mips0][req m][busy n], 256-B aligned parts
+  const size_t o_st = align256((size_t)m * 4), o_m0 = o_st + align256((size_t)m * 4), o_rq = o_m0 + 256;
+  const size_t o_b = o_rq + align256((size_t)m * 4), total = o_b + (size_t)n * sizeof(double);
+  rc = ensure_host(c, total);
+  if (rc) return rc;
+  unsigned char* const h = static_cast<unsigned char*>(c->host_stage);
+  unsigned char* const d = static_cast<unsigned char*>(c->host_stage_dev);
+  memcpy(h + o_m0, adv_mips, sizeof(int32_t));
+  memcpy(h + o_rq, req_mips, (size_t)m * 4);
+  memcpy(h + o_b, adv_busy, (size_t)n * sizeof(double));
+  const double* view = reinterpret_cast<const double*>(d + o_b);  // small views: read in place over the link
+  hipError_t e = hipSuccess;
+  if (n > fognet::kDecideArgNodes) {
+    rc = ensure(c, &c->scratch, &c->scratch_bytes, (size_t)n * sizeof(double), "decide scratch");
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(c->scratch, h + o_b, (size_t)n * sizeof(double), hipMemcpyHostToDevice, c->stream)) !=
+        hipSuccess)
+      return hip_fail(c, e, "decide_window copy-in");
+    view = static_cast<const double*>(c->scratch);
+  }
+  e = fognet::launch_decide(m, n, 0, view,
+                                       reinterpret_cast<const int32_t*>(d + o_m0), reinterpret_cast<const int32_t*>(d + o_rq),
+                                       reinterpret_cast<int32_t*>(d), reinterpret_cast<int32_t*>(d + o_st), c->stream);
+  if (e != hipSuccess) return hip_fail(c, e, "decide_window launch");
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e, "decide_window sync");
+  memcpy(out_node, h, (size_t)m * 4);
+  const int32_t* st = reinterpret_cast<const int32_t*>(h + o_st);
+  for (int32_t i = 0; i < m; ++i)
+    if (st[i] != FOGNET_OK) {
+      char buf[96];
+      snprintf(buf, sizeof buf, "request %d: %s", i, fognet_status_string(st[i]));
+      return fail(c, st[i], buf);
+    }
   return FOGNET_OK;
 }
 

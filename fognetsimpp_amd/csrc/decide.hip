@@ -29,52 +29,76 @@ __device__ __forceinline__ bool better(const Cand& a, const Cand& b) {
   return a.c < b.c || (a.c == b.c && a.j < b.j);
 }
 
-__global__ __launch_bounds__(kDecideThreads) void decide_kernel(int64_t m, int32_t n, const double* busy,
-                                                                 const int32_t* mips, const int32_t* req,
-                                                                 int32_t* node, int32_t* status) {
+// One decision by one wavefront: rc / out as the reference's scan
+// (busy: the advertised view b[0..n), mips0 = brokers[0]->getMips()).
+template <class Busy>
+__device__ __forceinline__ void decide_one(int32_t n, Busy b, int32_t m0, int32_t rq, int lane, int32_t& out,
+                                           int32_t& rc) {
+  rc = FOGNET_OK;
+  out = -1;
+  if (n <= 0) {
+    rc = FOGNET_ERR_NO_NODES;
+  } else if (m0 == 0) {
+    rc = FOGNET_ERR_DIV0;
+  } else if (m0 == -1 && rq == INT32_MIN) {
+    rc = FOGNET_ERR_ARG;  // INT_MIN / -1 overflows in the reference
+  } else {
+    const double tsk = (double)(rq / m0);
+    const double c0 = b(0) + tsk;
+    if (c0 != c0) {
+      out = 0;  // tempp is NaN: no candidate can replace node 0
+    } else {
+      Cand best = {0.0, -1};
+      for (int32_t j = lane; j < n; j += kWave) {
+        const double c = b(j) + tsk;
+        if (c == c) {
+          const Cand cj = {c, j};
+          if (better(cj, best)) best = cj;
+        }
+      }
+      // wave reduction, butterfly over xor distances
+      for (int off = 32; off > 0; off >>= 1) {
+        Cand o;
+        o.c = __shfl_xor(best.c, off);
+        o.j = __shfl_xor(best.j, off);
+        if (better(o, best)) best = o;
+      }
+      out = best.j;  // node 0 is a non-NaN candidate, so best.j >= 0
+    }
+  }
+}
+
+// view_stride: n (one view per query) or 0 (one view shared by all queries:
+// the publishes of one window between two adverts, fognet_decide_window).
+__global__ __launch_bounds__(kDecideThreads) void decide_kernel(int64_t m, int32_t n, int64_t view_stride,
+                                                                 const double* busy, const int32_t* mips,
+                                                                 const int32_t* req, int32_t* node, int32_t* status) {
   const int64_t q = (int64_t)blockIdx.x * (kDecideThreads / kWave) + threadIdx.x / kWave;
   const int lane = threadIdx.x % kWave;
   if (q >= m) return;  // whole wave exits together
-  int32_t rc = FOGNET_OK;
-  int32_t out = -1;
-  if (n <= 0) {
-    rc = FOGNET_ERR_NO_NODES;
-  } else {
-    const double* b = busy + q * (int64_t)n;
-    const int32_t m0 = mips[q * (int64_t)n];
-    const int32_t rq = req[q];
-    if (m0 == 0) {
-      rc = FOGNET_ERR_DIV0;
-    } else if (m0 == -1 && rq == INT32_MIN) {
-      rc = FOGNET_ERR_ARG;  // INT_MIN / -1 overflows in the reference
-    } else {
-      const double tsk = (double)(rq / m0);
-      const double c0 = b[0] + tsk;
-      if (c0 != c0) {
-        out = 0;  // tempp is NaN: no candidate can replace node 0
-      } else {
-        Cand best = {0.0, -1};
-        for (int32_t j = lane; j < n; j += kWave) {
-          const double c = b[j] + tsk;
-          if (c == c) {
-            const Cand cj = {c, j};
-            if (better(cj, best)) best = cj;
-          }
-        }
-        // wave reduction, butterfly over xor distances
-        for (int off = 32; off > 0; off >>= 1) {
-          Cand o;
-          o.c = __shfl_xor(best.c, off);
-          o.j = __shfl_xor(best.j, off);
-          if (better(o, best)) best = o;
-        }
-        out = best.j;  // node 0 is a non-NaN candidate, so best.j >= 0
-      }
-    }
-  }
+  int32_t rc, out;
+  const double* b = busy + q * view_stride;
+  decide_one(n, [&](int32_t j) { return b[j]; }, n > 0 ? mips[q * view_stride] : 0, req[q], lane, out, rc);
   if (lane == 0) {
     node[q] = out;
     if (status) status[q] = rc;
+  }
+}
+
+// The scalar drop-in (fognet_decide): the view travels in the kernel
+// arguments (n <= kDecideArgNodes) or is read from mapped host memory, and the
+// result is written straight to mapped host memory: one launch and one stream
+// synchronisation per decision, no copies.
+__global__ __launch_bounds__(kWave) void decide_arg_kernel(DecideArgs a, const double* far_busy, int32_t* res) {
+  int32_t rc, out;
+  if (a.n <= kDecideArgNodes)
+    decide_one(a.n, [&](int32_t j) { return a.busy[j]; }, a.mips0, a.req, threadIdx.x, out, rc);
+  else
+    decide_one(a.n, [&](int32_t j) { return far_busy[j]; }, a.mips0, a.req, threadIdx.x, out, rc);
+  if (threadIdx.x == 0) {
+    res[0] = out;
+    res[1] = rc;
+    __threadfence_system();
   }
 }
 
@@ -121,13 +145,18 @@ hipError_t launch_decide_v2(int64_t m, int32_t n, const int32_t* mips, const int
   return hipGetLastError();
 }
 
-hipError_t launch_decide(int64_t m, int32_t n, const double* busy, const int32_t* mips, const int32_t* req,
-                         int32_t* node, int32_t* status, hipStream_t s) {
+hipError_t launch_decide(int64_t m, int32_t n, int64_t view_stride, const double* busy, const int32_t* mips,
+                         const int32_t* req, int32_t* node, int32_t* status, hipStream_t s) {
   if (m <= 0) return hipSuccess;
   const int per = kDecideThreads / kWave;
   const int64_t blocks = (m + per - 1) / per;
-  hipLaunchKernelGGL(decide_kernel, dim3((unsigned)blocks), dim3(kDecideThreads), 0, s, m, n, busy, mips, req,
-                     node, status);
+  hipLaunchKernelGGL(decide_kernel, dim3((unsigned)blocks), dim3(kDecideThreads), 0, s, m, n, view_stride, busy, mips,
+                     req, node, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_decide_args(const DecideArgs& a, const double* far_busy, int32_t* res, hipStream_t s) {
+  hipLaunchKernelGGL(decide_arg_kernel, dim3(1), dim3(kWave), 0, s, a, far_busy, res);
   return hipGetLastError();
 }
 

@@ -242,8 +242,15 @@ hipError_t launch_replay(const ReplayArgs& a, hipStream_t s);
 hipError_t launch_rep_stats(const ReplayArgs& a, hipStream_t s);
 hipError_t launch_reduce_stats(const fognet_rep_stats* st, int32_t R, fognet_job_stats* out,
                                hipStream_t s);
-hipError_t launch_decide(int64_t m, int32_t n, const double* busy, const int32_t* mips,
+hipError_t launch_decide(int64_t m, int32_t n, int64_t view_stride, const double* busy, const int32_t* mips,
                          const int32_t* req, int32_t* node, int32_t* status, hipStream_t s);
+// fognet_decide's kernel arguments: the view of up to kDecideArgNodes nodes by value
+constexpr int kDecideArgNodes = 256;
+struct DecideArgs {
+  int32_t n, mips0, req, pad;
+  double busy[kDecideArgNodes];
+};
+hipError_t launch_decide_args(const DecideArgs& a, const double* far_busy, int32_t* res, hipStream_t s);
 hipError_t launch_decide_v2(int64_t m, int32_t n, const int32_t* mips, const int32_t* local, const int32_t* req,
                             int32_t* node, int32_t* action, hipStream_t s);
 hipError_t launch_user_stats(const ReplayArgs& a, const int64_t* user_ul, const int64_t* user_dl, int32_t per_task,

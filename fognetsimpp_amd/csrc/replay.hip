@@ -433,8 +433,8 @@ __device__ __forceinline__ uint32_t view_min(const Slot (&st)[NPL]) {
 // The saturation never changes an admissible decision (service <= max_s < 2^16).
 
 template <int NPL>
-__device__ __forceinline__ uint32_t ext_argmin(const Slot (&st)[NPL], uint32_t req, const int32_t* s_mips,
-                                               const int64_t* s_dl, int N, int lane) {
+__device__ __forceinline__ uint32_t ext_argmin(const Slot (&st)[NPL], uint32_t req, const uint32_t* s_dvm,
+                                               const uint8_t* s_dvs, const int64_t* s_dl, int N, int lane) {
   uint64_t c[NPL];
   uint64_t m = ~0ull;
 #pragma unroll
@@ -442,7 +442,8 @@ __device__ __forceinline__ uint32_t ext_argmin(const Slot (&st)[NPL], uint32_t r
     const int j = s * kWave + lane;
     c[s] = ~0ull;
     if (j < N) {
-      const uint32_t S = min(req / (uint32_t)s_mips[j], kExtSatS);
+      const uint32_t dvs = s_dvs[j];
+      const uint32_t S = min(udiv(req, UDiv{s_dvm[j], (dvs & 1u) | ((dvs >> 1) << 8)}), kExtSatS);
       c[s] = (uint64_t)s_dl[j] + (uint64_t)((st[s].vkey >> 8) + S) * (uint64_t)kTicksPerSecond;
     }
     m = c[s] < m ? c[s] : m;
@@ -561,15 +562,16 @@ __device__ __forceinline__ void stats_finish(const ReplayArgs& A, int r, int64_t
 }
 
 template <int NPL, int POL>
-// 4 waves per SIMD (<= 128 VGPRs): 16 replications resident per CU, so the
-// 4096-replication sweep runs in a single wave of workgroups on 256 CUs.
+// 4 waves per SIMD (<= 128 VGPRs) and <= 10 KiB of LDS (160 KiB / 16): 16
+// replications resident per CU, so the 4096-replication sweep runs in a single
+// wave of workgroups on 256 CUs.  (11 KiB of LDS admits only 14 per CU, and
+// the last 512 replications then run as a second, mostly idle round.)
 __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))) void replay_kernel(ReplayArgs A) {
   constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
   __shared__ int64_t s_dl[NPL * kWave];
   __shared__ int64_t s_ul[NPL * kWave];
-  __shared__ int32_t s_mips[NPL * kWave];
   __shared__ uint32_t s_dvm[NPL * kWave];  // division by the node's MIPS (udiv_magic): multiplier
   __shared__ uint8_t s_dvs[NPL * kWave];   //   and shifts sh1 | sh2 << 1 (sh1 <= 1, sh2 <= 31)
   __shared__ int64_t s_tld[NPL * kWave];   // tail completion tick (INT64_MIN: node never used)
@@ -604,7 +606,6 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     }
     s_dl[k] = d;
     s_ul[k] = u;
-    s_mips[k] = m;
     const UDiv dv = udiv_magic((uint32_t)(m > 0 ? m : 1));
     s_dvm[k] = dv.m;
     s_dvs[k] = (uint8_t)((dv.sh & 1u) | ((dv.sh >> 8) << 1));
@@ -732,7 +733,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
         TMARK(1)
         if constexpr (kExt) {
           // 2') per-publish argmin of the extension cost; every run is one publish
-          best = ext_argmin<NPL>(st, readlane_u32((uint32_t)cr, jp), s_mips, s_dl, N, lane);
+          best = ext_argmin<NPL>(st, readlane_u32((uint32_t)cr, jp), s_dvm, s_dvs, s_dl, N, lane);
         } else {
         // 2) argmin over the advertised view (ties -> lowest index)
         if (dirty) {

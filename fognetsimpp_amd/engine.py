@@ -111,6 +111,22 @@ class BrokerBaseApp3:
         self.ctx.check(rc, "sendPubAck")
         return out.value
 
+    def sendPubAck_window(self, adv_busy, adv_mips, MIPSRequired) -> np.ndarray:  # noqa: N802,N803
+        """The publishes of one window (no advert in between: one view) decided
+        together (fognet_decide_window); equals one sendPubAck per request."""
+        busy = np.ascontiguousarray(adv_busy, dtype=np.float64)
+        mips = np.ascontiguousarray(adv_mips, dtype=np.int32)
+        req = np.ascontiguousarray(MIPSRequired, dtype=np.int32).reshape(-1)
+        if busy.shape != mips.shape or busy.ndim != 1:
+            raise FognetError(_abi.FOGNET_ERR_ARG, "adv_busy/adv_mips must be 1-D and equal length")
+        out = np.empty(len(req), np.int32)
+        rc = self.ctx._lib.fognet_decide_window(self.ctx.handle, _abi.FOGNET_POLICY_REF_V3, len(busy),
+                                                busy.ctypes.data_as(C.c_void_p), mips.ctypes.data_as(C.c_void_p),
+                                                len(req), req.ctypes.data_as(C.c_void_p),
+                                                out.ctypes.data_as(C.c_void_p))
+        self.ctx.check(rc, "sendPubAck_window")
+        return out
+
     def sendPubAck_batch(self, adv_busy: torch.Tensor, adv_mips: torch.Tensor, req: torch.Tensor):  # noqa: N802
         """M independent decisions on device tensors [M, n]; returns (node, status) int32 [M]."""
         m, n = adv_busy.shape

@@ -313,10 +313,23 @@ int fognet_create(fognet_ctx **out, int hip_device);
 void fognet_destroy(fognet_ctx *ctx);
 const char *fognet_last_error(const fognet_ctx *ctx);
 
-/* Scalar drop-in for BrokerBaseApp3.cc:267-281 (the OMNeT++ adapter's call):
- * host arrays of the broker's advertised view; evaluated on the device. */
+/* Scalar drop-in for BrokerBaseApp3.cc:267-281 (the OMNeT++ adapter's call,
+ * INTEGRATION.md §1): host arrays of the broker's advertised view
+ * (Broker::busyTime, Broker::MIPS in CONNECT order); evaluated on the device
+ * with the reference's exact fp64 arithmetic.  policy: FOGNET_POLICY_REF_V3.
+ * One kernel launch per call (views of <= 256 nodes travel in the kernel
+ * arguments, larger ones in one DMA copy; the result is written to mapped
+ * host memory) and one stream synchronisation. */
 int fognet_decide(fognet_ctx *ctx, int policy, int32_t n, const double *adv_busy,
                   const int32_t *adv_mips, int32_t req_mips, int32_t *out_node);
+
+/* The publishes of one window decided together: m requests against ONE view
+ * (the broker's view only changes when an advert arrives, BrokerBaseApp3.cc:
+ * 123-130, so every publish between two adverts sees the same view).  Equals
+ * m fognet_decide calls on that view; one launch, one synchronisation.
+ * out_node [m] (host).  Returns the first failing request's status. */
+int fognet_decide_window(fognet_ctx *ctx, int policy, int32_t n, const double *adv_busy,
+                         const int32_t *adv_mips, int32_t m, const int32_t *req_mips, int32_t *out_node);
 
 /* M independent decisions, device pointers: adv_busy/adv_mips [M][n], req [M],
  * out_node [M], out_status [M] (fognet_status per query, nullable). */

@@ -92,3 +92,28 @@ def test_create_refuses_without_gpu():
     h = ctypes.c_void_p()
     assert lib.fognet_create(ctypes.byref(h), 0) == abi.FOGNET_ERR_DEVICE
     assert not h.value
+
+
+def build_c_client():
+    """tests/c/abi_c_client.c: plain C99 against include/fognet_hip.h, linked to the library."""
+    exe = os.path.join(ROOT, "build", "abi_c_client")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    subprocess.run(["gcc", "-std=c99", "-pedantic", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "c", "abi_c_client.c"), "-o", exe,
+                    "-L", os.path.join(ROOT, "fognetsimpp_amd"), "-lfognet_hip", "-L/opt/rocm/lib", "-lamdhip64",
+                    "-Wl,-rpath," + os.path.join(ROOT, "fognetsimpp_amd"), "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    return exe
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="the no-GPU path of the C client")
+def test_plain_c_client_builds_and_refuses_without_gpu():
+    p = subprocess.run([build_c_client(), "--no-gpu"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+
+
+@pytest.mark.gpu
+def test_plain_c_client_on_gpu():
+    """fognet_decide / fognet_decide_window / fognet_run_batch called from C."""
+    p = subprocess.run([build_c_client()], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "all checks passed" in p.stdout

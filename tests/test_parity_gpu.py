@@ -71,6 +71,54 @@ def test_decide_batch_matches_oracle(ctx):
                 assert node[q] == k, (n, q)
 
 
+def test_decide_window_and_large_views_match_oracle(ctx):
+    """fognet_decide_window (one view, m requests) and fognet_decide on views past
+    the kernel-argument size (mapped host memory) against the reference scan."""
+    rng = np.random.default_rng(8)
+    broker = fa.BrokerBaseApp3(ctx)
+    for n in (1, 4, 64, 256, 257, 3000):
+        for _ in range(3):
+            busy = rng.integers(0, 5, size=n).astype(np.float64) + rng.choice([0.0, 0.5, 1e-16, np.nan], size=n)
+            mips = rng.integers(1, 3000, size=n).astype(np.int32)
+            reqs = rng.integers(0, 10**6, size=50).astype(np.int32)
+            got = broker.sendPubAck_window(busy, mips, reqs)
+            want = [ol.decide_v3(busy, mips, int(q))[1] for q in reqs]
+            np.testing.assert_array_equal(got, want)
+            assert broker.sendPubAck(busy, mips, int(reqs[0])) == want[0]
+
+
+def test_decide_latency(ctx):
+    """Per-call latency of the scalar drop-in (one launch + one synchronisation,
+    no copies) and of a window of 64 publishes; written to
+    gpurun_out/decide_latency.json.  The bound only catches regressions."""
+    import json
+    import os
+    import time
+    broker = fa.BrokerBaseApp3(ctx)
+    res = {}
+    for n in (5, 256, 10_000):
+        busy = np.arange(n, dtype=np.float64)[::-1].copy()
+        mips = np.full(n, 1000, np.int32)
+        for _ in range(50):
+            broker.sendPubAck(busy, mips, 4000)
+        k = 2000
+        t0 = time.perf_counter()
+        for _ in range(k):
+            broker.sendPubAck(busy, mips, 4000)
+        res[f"decide_n{n}_us"] = (time.perf_counter() - t0) / k * 1e6
+        reqs = np.full(64, 4000, np.int32)
+        t0 = time.perf_counter()
+        for _ in range(200):
+            broker.sendPubAck_window(busy, mips, reqs)
+        res[f"window64_n{n}_us"] = (time.perf_counter() - t0) / 200 * 1e6
+    os.makedirs(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out"), exist_ok=True)
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out",
+                           "decide_latency.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(res)
+    assert res["decide_n5_us"] < 2000
+
+
 @pytest.mark.parametrize("case", golden_io.decide_v2_cases(), ids=lambda c: c[0])
 def test_v2_sendPubAck_known_answers(ctx, case):
     name, mips, local, req, action, node = case
