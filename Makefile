@@ -53,3 +53,30 @@ prof: $(SRCS) $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DFOGNET_REPLAY_PROFILE=2 -Iinclude -shared -o build/prof2/libfognet_hip.so $(SRCS) $(SRC_DIR)/io.cpp
 
 .PHONY: prof
+
+# Host code under AddressSanitizer + UBSan: the CPU oracle, the
+# trace / result-file I/O and the command-line driver, each driven through its
+# paths by a standalone program (no Python, no GPU: the driver runs --dry-run
+# and its error paths).  `make asan` builds and runs them; any report fails it.
+ASAN_FLAGS := -fsanitize=address,undefined -fno-sanitize-recover=all -fno-omit-frame-pointer -g -O1
+ASAN_DIR := build/asan
+asan:
+	@mkdir -p $(ASAN_DIR)
+	gcc $(ASAN_FLAGS) -std=gnu11 -ffp-contract=off -pthread tests/c/oracle_check.c oracle/fognet_oracle.c \
+	  oracle/fognet_oracle_v2.c -lm -o $(ASAN_DIR)/oracle_check
+	$(HOSTCXX) $(ASAN_FLAGS) -std=c++17 -ffp-contract=off -Iinclude tests/c/io_check.cpp $(SRC_DIR)/io.cpp \
+	  -o $(ASAN_DIR)/io_check
+	$(HOSTCXX) $(ASAN_FLAGS) -std=c++17 -ffp-contract=off -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
+	  $(SRC_DIR)/fognet_replay.cpp $(SRC_DIR)/io.cpp -o $(ASAN_DIR)/fognet_replay \
+	  -Lfognetsimpp_amd -lfognet_hip -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,$(CURDIR)/fognetsimpp_amd -Wl,-rpath,/opt/rocm/lib
+	ASAN_OPTIONS=detect_leaks=1 $(ASAN_DIR)/oracle_check
+	ASAN_OPTIONS=detect_leaks=1 $(ASAN_DIR)/io_check $(ASAN_DIR)
+	ASAN_OPTIONS=detect_leaks=0 $(ASAN_DIR)/fognet_replay -f tests/scenarios/fog5.ini --users 'user[10]' --reps 3 \
+	  --dry-run --show --trace-out $(ASAN_DIR)/drv.fogntrc > /dev/null
+	ASAN_OPTIONS=detect_leaks=0 $(ASAN_DIR)/fognet_replay -f tests/scenarios/fog5.ini -c Example --nodes 5 --dry-run > /dev/null
+	! ASAN_OPTIONS=detect_leaks=0 $(ASAN_DIR)/fognet_replay -f tests/scenarios/fog5.ini -c Early --users 'user[2]' --dry-run 2> $(ASAN_DIR)/err.txt
+	grep -q "divide by the unadvertised MIPS 0" $(ASAN_DIR)/err.txt
+	! ASAN_OPTIONS=detect_leaks=0 $(ASAN_DIR)/fognet_replay -f tests/scenarios/fog5.ini --users 'user[2]' --ring 1000 --dry-run 2> $(ASAN_DIR)/err.txt
+	@echo "asan: oracle, io and driver clean"
+
+.PHONY: asan

@@ -95,3 +95,20 @@ def check_qtime_record(st, exp):
         assert int(st["queue_min_raw"]) == exp["queue_min"] and int(st["queue_max_raw"]) == exp["queue_max"]
     else:
         assert int(st["queue_min_raw"]) == np.iinfo(np.int64).max
+
+
+def general0_v2_node():
+    """tests/golden/general0_v2_node.json (make_general0_fixture.py): the fog node
+    of the reference's recorded example run (ComputeBrokerApp2 timing)."""
+    d = json.load(open(os.path.join(GOLDEN, "general0_v2_node.json")))
+    ms = 10**9
+    arr_node = np.array(d["task_arrival_ticks"], np.int64)
+    n = d["ini"]["nodes"]
+    # The recorded broker is older code (SURVEY.md §4): the fixture feeds the node the
+    # same four tasks by forwarding every publish (a broker pool of 0 MIPS) over a
+    # 1-ms link; MIPSRequired 100 (the v1 user of that run, mqttApp.cc:330).
+    tr = dict(arrive=(arr_node - ms)[None], req=np.full((1, len(arr_node)), 100, np.int32),
+              broker_mips=0, mips=np.full(n, d["ini"]["node_mips"], np.int32), dl=np.full(n, ms, np.int64),
+              ul=np.full(n, ms, np.int64), first_adv=np.full(n, d["connack_tick"] + 10 * ms, np.int64),
+              stop=3_360_000_000_000)
+    return tr, d

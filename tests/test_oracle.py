@@ -361,3 +361,22 @@ def test_oracle_stats_layout_is_the_abi_layout():
     from fognetsimpp_amd import _abi
     assert ol.ORC_STATS_DTYPE.descr == _abi.REP_STATS_DTYPE.descr
     assert ol.MOMENTS_DTYPE.descr == _abi.MOMENTS_DTYPE.descr
+
+
+def test_v2_node_reproduces_general0_recording():
+    """Weak pin against the reference's own recorded run (General-0.sca/.vec,
+    older user code): the fog node (ComputeBrokerApp2) receives the 4 forwarded
+    tasks at the recorded ticks and releases them at the recorded double-send
+    ticks of its 10-ms timer (one release + advert per firing after the last
+    arrival re-armed it, ComputeBrokerApp2.cc:219-237, 290-293); every
+    forwarded task goes to node 0 (CB1 received 5 packets, CB2-5 one each)."""
+    tr, d = golden_io.general0_v2_node()
+    assert d["packets_received"] == {"ComputeBroker1": 5, "ComputeBroker2": 1, "ComputeBroker3": 1,
+                                     "ComputeBroker4": 1, "ComputeBroker5": 1}
+    o = ol.run_v2(tr["arrive"], tr["req"], tr["broker_mips"], tr["mips"], tr["dl"], tr["ul"], tr["first_adv"],
+                  tr["stop"], 0.01)
+    assert (o["node"][0] == 0).all()
+    assert (o["status"][0] == ol.V2_ST_ACCEPTED).all()
+    np.testing.assert_array_equal(o["start"][0], d["task_arrival_ticks"])
+    np.testing.assert_array_equal(o["done"][0], d["release_ticks"])
+    assert o["stats"]["n_released_node"][0] == 4

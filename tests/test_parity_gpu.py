@@ -775,6 +775,20 @@ def test_v2_random_matches_oracle(ctx, seed, N):
     assert_v2_parity(g, o)
 
 
+def test_v2_node_reproduces_general0_recording_gpu(ctx):
+    """The device v2 replay on the General-0 recording fixture (see test_oracle)."""
+    tr, d = golden_io.general0_v2_node()
+    dev = torch.device("cuda", ctx.device)
+    dt = fa.as_device_trace(dict(arrive=tr["arrive"], req=tr["req"], mips=tr["mips"], dl=tr["dl"], ul=tr["ul"],
+                                 first_adv=tr["first_adv"]), dev)
+    out = fa.run_v2(ctx, dt, tr["broker_mips"], tr["stop"], 0.01)
+    torch.cuda.synchronize()
+    assert (out.node[0].cpu().numpy() == 0).all()
+    np.testing.assert_array_equal(out.start_tick[0].cpu().numpy(), d["task_arrival_ticks"])
+    np.testing.assert_array_equal(out.done_tick[0].cpu().numpy(), d["release_ticks"])
+    assert out.rep_stats()["n_released_node"][0] == 4
+
+
 def test_v2_c1_as_shipped(ctx):
     """Config C1 (BASELINE.json configs[0]) with the modules its ini names:
     one user (mqttApp2's timer chain + glibc rand()), broker and 5 nodes at 1000
