@@ -350,8 +350,12 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
   int rc = prepare(c, in, &a);
   if (rc) return rc;
   if (!out->stats) return fail(c, FOGNET_ERR_ARG, "stats output is required (per-replication status)");
-  if (a.T > 0 && (!out->node || !out->status || !out->start_tick || !out->done_tick))
-    return fail(c, FOGNET_ERR_UNSUPPORTED, "per-task outputs are required (stats-only mode not implemented)");
+  const int n_null = !out->node + !out->status + !out->start_tick + !out->done_tick;
+  if (n_null != 0 && n_null != 4)
+    return fail(c, FOGNET_ERR_ARG, "per-task outputs: give all four arrays, or none (statistics only)");
+  const bool stats_only = n_null == 4 && a.T > 0;
+  if (stats_only && which != 3)
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "statistics-only replays run through fognet_run_batch_dev");
   if (a.R == 0) return FOGNET_OK;
   rc = set_device(c);
   if (rc) return rc;
@@ -368,6 +372,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     // crashes are only modelled by the wide kernel; it accumulates the statistics while it replays, so the
     // statistics-only stage has nothing left to do
     if (!(which & 1)) return FOGNET_OK;
+    a.no_task_out = stats_only ? 1 : 0;
     const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N);
     rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ws, "wide replay workspace");
     if (rc) return rc;
@@ -380,17 +385,27 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
   if (which & 1) {
     // workspace: [hand-over counter | hand-over list [R] | pending-task rings, reused by the wide kernel's
     // replay of the handed-over replications once the register kernel is done (stream order)]
+    // + for a statistics-only replay the per-task outputs the fused statistics epilogue reads back
     const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
     const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
     const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
     const size_t head = align256(256 + (size_t)a.R * sizeof(int32_t));
-    rc = ensure(c, (void**)&c->ring, &c->ring_bytes, head + (ring_bytes > fb_bytes ? ring_bytes : fb_bytes),
-                "ring workspace");
+    const size_t body = ring_bytes > fb_bytes ? ring_bytes : fb_bytes;
+    const size_t RT = stats_only ? (size_t)a.R * (size_t)a.T : 0;
+    const size_t o_node = head + align256(body), o_st = o_node + align256(RT * 4), o_start = o_st + align256(RT),
+                 o_done = o_start + align256(RT * 8), total = o_done + align256(RT * 8);
+    rc = ensure(c, (void**)&c->ring, &c->ring_bytes, total, "ring workspace");
     if (rc) return rc;
     unsigned char* const base = reinterpret_cast<unsigned char*>(c->ring);
     a.wide_count = reinterpret_cast<int32_t*>(base);
     a.wide_list = reinterpret_cast<int32_t*>(base + 256);
     a.ring = reinterpret_cast<fognet::RingEntry*>(base + head);
+    if (stats_only) {
+      a.out_node = reinterpret_cast<int32_t*>(base + o_node);
+      a.out_status = reinterpret_cast<uint8_t*>(base + o_st);
+      a.out_start = reinterpret_cast<int64_t*>(base + o_start);
+      a.out_done = reinterpret_cast<int64_t*>(base + o_done);
+    }
     e = hipMemsetAsync(a.wide_count, 0, sizeof(int32_t), (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "hand-over counter");
     e = fognet::launch_replay(a, (hipStream_t)stream);
@@ -448,6 +463,7 @@ int fognet_run_batch(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out*
     const size_t sz = i < 9 ? isz[i] : osz[i - 9];
     if (i >= 6 && i < 8 && !pw) continue;
     if (i == 8 && !dn) continue;
+    if (i >= 9 && i < 13 && !hdst[i - 9]) continue;  // statistics only: no per-task outputs
     if (i >= 14 && !hdst[i - 9]) continue;
     hipError_t e = hipMalloc(&d[i], sz ? sz : 8);
     if (e != hipSuccess) {

@@ -181,6 +181,11 @@ struct ReplayArgs {
   // kernel, launched with wide_list set, replays exactly the listed ones.
   int32_t* wide_list;     // [R] (nullable: no hand-over, kNeedsWide stays the status)
   int32_t* wide_count;
+  // Statistics-only replays (fognet_batch_out per-task arrays null): the wide
+  // kernel, which accumulates its statistics inline, then writes nothing per
+  // task; the register kernel writes to an internal [R][T] scratch instead
+  // (its fused statistics epilogue reads the outputs back).
+  int32_t no_task_out;
 };
 
 // Internal per-replication status between the two replay kernels (never

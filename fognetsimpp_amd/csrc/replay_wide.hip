@@ -417,10 +417,12 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           ch = h;
           max_pend = max(max_pend, (uint32_t)h.npend);
           const size_t o = tbase + (size_t)i;
-          A.out_node[o] = (int32_t)k;
-          A.out_status[o] = (uint8_t)status;
-          A.out_start[o] = start == kNever ? -1 : start;
-          A.out_done[o] = done == kNever ? -1 : done;
+          if (!A.no_task_out) {  // (statistics-only replays keep no per-task outputs)
+            A.out_node[o] = (int32_t)k;
+            A.out_status[o] = (uint8_t)status;
+            A.out_start[o] = start == kNever ? -1 : start;
+            A.out_done[o] = done == kNever ? -1 : done;
+          }
           if (done != kNever) {
             acc_task(acc, t, a, start, done, S, status, hist ? L.hist : nullptr);
             if (hist) atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - t)], 1u);

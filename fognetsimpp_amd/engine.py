@@ -179,10 +179,10 @@ class BrokerBaseApp2:
 
 @dataclass
 class BatchResult:
-    node: torch.Tensor        # [R, T] int32
-    status: torch.Tensor      # [R, T] uint8 (5 started / 4 queued)
-    start_tick: torch.Tensor  # [R, T] int64
-    done_tick: torch.Tensor   # [R, T] int64
+    node: torch.Tensor | None        # [R, T] int32 (None: statistics only)
+    status: torch.Tensor | None      # [R, T] uint8 (5 started / 4 queued)
+    start_tick: torch.Tensor | None  # [R, T] int64
+    done_tick: torch.Tensor | None   # [R, T] int64
     stats: torch.Tensor       # [R * sizeof(fognet_rep_stats)] uint8 (device)
     node_energy: torch.Tensor | None = None  # [R, N] float64 (power model only)
     hist: torch.Tensor | None = None         # [2, 64] int64 job histogram (queueTime, response), added to
@@ -192,12 +192,15 @@ class BatchResult:
 
 
 def allocate_outputs(R: int, T: int, device, N: int | None = None, energy: bool = False,
-                     hist: bool = False) -> BatchResult:
+                     hist: bool = False, per_task: bool = True) -> BatchResult:
+    """Output buffers; ``per_task=False``: statistics only (no per-task arrays:
+    the replay writes nothing per task, fognet_batch_out)."""
+    mk = (lambda shape, dt: torch.empty(shape, dtype=dt, device=device)) if per_task else (lambda shape, dt: None)
     return BatchResult(
-        node=torch.empty((R, T), dtype=torch.int32, device=device),
-        status=torch.empty((R, T), dtype=torch.uint8, device=device),
-        start_tick=torch.empty((R, T), dtype=torch.int64, device=device),
-        done_tick=torch.empty((R, T), dtype=torch.int64, device=device),
+        node=mk((R, T), torch.int32),
+        status=mk((R, T), torch.uint8),
+        start_tick=mk((R, T), torch.int64),
+        done_tick=mk((R, T), torch.int64),
         stats=torch.zeros(R * _abi.REP_STATS_DTYPE.itemsize, dtype=torch.uint8, device=device),
         node_energy=torch.zeros((R, N), dtype=torch.float64, device=device) if energy else None,
         hist=torch.zeros((_abi.HIST_METRICS, _abi.HIST_BINS), dtype=torch.int64, device=device) if hist else None,
@@ -246,7 +249,8 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
             raise FognetError(_abi.FOGNET_ERR_ARG, f"{k} has shape {tuple(trace[k].shape)}, mips {tuple(mips.shape)}")
     if tuple(req.shape) != (R, T) or (mips.dim() == 2 and mips.shape[0] != R):
         raise FognetError(_abi.FOGNET_ERR_ARG, "trace arrays disagree on R/T")
-    if out is not None and (tuple(out.node.shape) != (R, T) or out.stats.numel() < R * _abi.REP_STATS_DTYPE.itemsize):
+    if out is not None and ((out.node is not None and tuple(out.node.shape) != (R, T))
+                            or out.stats.numel() < R * _abi.REP_STATS_DTYPE.itemsize):
         raise FognetError(_abi.FOGNET_ERR_ARG, "output buffers too small for the trace")
     if out is None:
         out = allocate_outputs(R, T, arrive.device, N=N, energy=energy, hist=hist)

@@ -202,8 +202,12 @@ typedef struct fognet_batch_out {
     uint8_t *status;          /* [R][T] fognet_task_status: 5 started on arrival, 4 queued, 9 lost */
     int64_t *start_tick;      /* [R][T] service start (-1: never started, node-down only)         */
     int64_t *done_tick;       /* [R][T] completion (RELEASERESOURCE) tick (-1: never, node-down)  */
-    fognet_rep_stats *stats;  /* [R] (all five arrays are required; a stats-only mode that skips
-                                 the per-task arrays is not implemented yet: ERR_UNSUPPORTED)    */
+    fognet_rep_stats *stats;  /* [R], required.  node/status/start_tick/done_tick: all four, or all
+                                 NULL for a statistics-only replay (fognet_run_batch_dev /
+                                 fognet_run_batch only): the caller gets the records and the
+                                 histogram; N > 256 (wide kernel) then writes nothing per task,
+                                 N <= 256 keeps the per-task outputs in the context's workspace
+                                 for its fused statistics pass                                 */
     double *node_energy_j;    /* [R][N] per-node energy (nullable; needs the power model)         */
     int64_t *hist;            /* [FOGNET_HIST_METRICS][FOGNET_HIST_BINS] job histogram, ADDED to
                                  (the caller zeroes it; nullable)                                 */

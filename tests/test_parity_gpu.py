@@ -461,6 +461,35 @@ def test_c4_workload_shape_matches_oracle(ctx):
     np.testing.assert_array_equal(out.hist.cpu().numpy(), ref["hist"].sum(axis=0))
 
 
+@pytest.mark.parametrize("kind", ["register", "wide", "handover", "ext_lat", "short"])
+def test_stats_only_equals_full_outputs(ctx, monkeypatch, kind):
+    """Statistics-only replays (no per-task arrays: the statistics are
+    accumulated while the replay runs, C4's mode) give the same records and
+    histogram as the replay with full outputs."""
+    ring, policy = 0, "REF_V3"
+    if kind == "wide":
+        monkeypatch.setenv("FOGNET_REPLAY_KERNEL", "wide")
+    tr = tg.make_batch(41, 6, 64, 5000, sweep=True)
+    if kind == "handover":
+        ring = 4
+    if kind == "ext_lat":
+        policy = "EXT_LAT"
+    if kind == "short":  # T below one flush window and not a multiple of 64
+        tr = tg.make_batch(42, 5, 17, 333, rho=0.9)
+    pb, pi = fa.power_model(tr["mips"])
+    tr = dict(tr, p_busy=pb, p_idle=pi)
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(tr, dev)
+    R, T = tr["arrive"].shape
+    full = fa.run_batch(ctx, d, ring_capacity=ring, policy=policy, hist=True)
+    so = fa.allocate_outputs(R, T, dev, hist=True, per_task=False)
+    fa.run_batch(ctx, d, out=so, ring_capacity=ring, policy=policy)
+    torch.cuda.synchronize()
+    assert (full.rep_stats()["status"] == 0).all()
+    assert so.rep_stats().tobytes() == full.rep_stats().tobytes()
+    assert torch.equal(so.hist, full.hist)
+
+
 # ------------------------------------------------------------------ a10/a11 statistics and the EXT_LAT policy
 # Builder-defined rows (include/fognet_hip.h): parity against the oracle's
 # restatement of the same definitions (not pinned by the reference).
