@@ -1,6 +1,9 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run, no tracing domains mixed in)
 # over one timed step of the bench workload: C3 (default) or WORKLOAD=c5.
+# Plus the FETCH_SIZE calibration: the standalone statistics pass
+# (rep_stats_kernel) streams a known byte count (29 B per task of the C3
+# outputs + trace) with the element widths the replay's own loads use.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/pmc
@@ -10,7 +13,6 @@ else
   BARGS=""; KERNEL=replay_kernel; DEC=409600000; OUT=pmc_traffic.json; CFG=4096,100000,256
 fi
 export TMPDIR=/tmp
-rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE" \
@@ -21,4 +23,14 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_W
   echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/p$i.log; exit $rc; fi
 done
-python3 tools/pmc_summary.py $KERNEL $DEC gpurun_out/pmc/$OUT 2048 $CFG > /dev/null
+python3 tools/pmc_summary.py $KERNEL $DEC gpurun_out/pmc/$OUT 2048 $CFG > /dev/null || exit 1
+if [ "${WORKLOAD:-c3}" = c3 ]; then
+  for grp in "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    FOGNET_STAGES=replay,stats timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc/c$i -o c$i -- \
+      python3 tools/stage_timing.py > gpurun_out/pmc/c$i.log 2>&1; rc=$?
+    echo "calibration pass $i ($grp) rc=$rc"
+    if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/c$i.log; exit $rc; fi
+  done
+  python3 tools/pmc_calibrate.py gpurun_out/pmc gpurun_out/pmc/$OUT || exit 1
+fi
