@@ -43,6 +43,37 @@ __device__ __forceinline__ double add_rn(double a, double b) {
   return a + b;
 }
 
+// ---------------------------------------------------------------- wave scans
+// Inclusive prefix sum (u32) and prefix maximum (i64) over the 64 lanes: DPP
+// row shifts, then the row broadcasts.  Lanes outside the scanned range must
+// hold the identities (0, INT64_MIN).
+__device__ __forceinline__ uint32_t wave_scan_add_u32(uint32_t v) {
+  v += dpp_or_u32<0x111, 0xF>(0u, v);  // row_shr:1
+  v += dpp_or_u32<0x112, 0xF>(0u, v);  // row_shr:2
+  v += dpp_or_u32<0x114, 0xF>(0u, v);  // row_shr:4
+  v += dpp_or_u32<0x118, 0xF>(0u, v);  // row_shr:8
+  v += dpp_or_u32<0x142, 0xA>(0u, v);  // row_bcast:15
+  v += dpp_or_u32<0x143, 0xC>(0u, v);  // row_bcast:31
+  return v;
+}
+
+// `tmp` carries the DPP destination from level to level: a lane whose source
+// is invalid keeps a value of an earlier lane its running maximum covers.
+__device__ __forceinline__ int64_t wave_scan_max_i64(int64_t v) {
+  int64_t t = INT64_MIN;
+#define FOGNET_MAX_LEVEL(C, M)         \
+  t = dpp_or_i64<C, M>(t, v);          \
+  v = t > v ? t : v;
+  FOGNET_MAX_LEVEL(0x111, 0xF)
+  FOGNET_MAX_LEVEL(0x112, 0xF)
+  FOGNET_MAX_LEVEL(0x114, 0xF)
+  FOGNET_MAX_LEVEL(0x118, 0xF)
+  FOGNET_MAX_LEVEL(0x142, 0xA)
+  FOGNET_MAX_LEVEL(0x143, 0xC)
+#undef FOGNET_MAX_LEVEL
+  return v;
+}
+
 // ---------------------------------------------------------------- OMNeT++ SimTime
 // The reference's signal arithmetic on simtime_t (OMNeT++ 4.6, scale 1e-12;
 // fognet_hip.h "Reference signal values"): dbl() = t * 1e-12, SimTime(double)

@@ -278,6 +278,11 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   int32_t c_mips = 1;
   int64_t c_dl = 0, c_ul = 0, c_down = kNever;
 
+  // the decision is recomputed only after an advert changed the view
+  // (adverts are the only view updates, BrokerBaseApp3.cc:123-130)
+  bool view_changed = true;
+  uint32_t k = 0u;
+
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
     const bool live = lane < cnt;
@@ -291,12 +296,13 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     }
     prev_t = readlane_i64(ca, cnt - 1);
 
-    for (int jp = 0; jp < cnt; ++jp) {
+    int jp = 0;
+    while (jp < cnt) {
       const int64_t t = readlane_i64(ca, jp);
-      const uint32_t rq = readlane_u32((uint32_t)cr, jp);
 
       // 1) completion adverts that reached the broker strictly before t
       bool lerr = false;
+      if (ballot(mn < t)) view_changed = true;
       while (ballot(mn < t)) {
         if (mn < t) {
           const int j = mj;
@@ -324,9 +330,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       }
 
       // 2) the decision over the advertised view
-      uint32_t k;
       if constexpr (kExt) {
-        // north-star cost (fognet_hip.h FOGNET_POLICY_EXT_LAT), first index on ties
+        // north-star cost (fognet_hip.h FOGNET_POLICY_EXT_LAT), first index on ties; per publish
+        const uint32_t rq = readlane_u32((uint32_t)cr, jp);
         uint64_t mc = ~0ull;
         uint32_t mjj = ~0u;
         for (int j = lane; j < N; j += kWave) {
@@ -339,112 +345,171 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         }
         const uint64_t m = wave_min_u64(mc);
         k = wave_min_u32(mc == m ? mjj : ~0u);
-      } else {
+      } else if (view_changed) {
         // BrokerBaseApp3.cc:267-281: busy_j + req/mips_0 < tempp over exact
         // integer busy values <=> the smallest (busy, j)
         k = (uint32_t)wave_min_u64(mk);
+        view_changed = false;
       }
+      const int kl = (int)(k % kWave);
 
-      // 3) node k: task arrival (ComputeBrokerApp3.cc:269-320), owner lane
-      if (lane == (int)(k % kWave)) {
-        if ((int)k != cj) {
-          if (cj >= 0) nd[cj] = ch;  // write back the previous node's record
-          cj = (int)k;
-          ch = nd[k];
-          c_mips = A.mips[nbase + k];
-          c_dl = A.dl[nbase + k];
-          c_ul = A.ul[nbase + k];
-          c_down = A.down ? A.down[nbase + k] : kNever;
-        }
-        WideNode h = ch;
-        const int32_t mips_k = c_mips;
-        const int64_t dl_k = c_dl, ul_k = c_ul;
-        const uint32_t S = rq / (uint32_t)mips_k;  // double tskTime = requiredMIPS / MIPS (:276)
-        const int64_t down_k = c_down;
-        const int64_t a = t + dl_k;
-        // the previous task on node k is its tail (FIFO single server); its
-        // done is kNever if the node crashed before completing it
-        const int64_t prev_done = h.tl >= 0 ? h.tl_done : INT64_MIN;
-        const uint32_t prev_S = h.tl_S;
-        int64_t start = kNever, done = kNever;
-        uint32_t status = FOGNET_TASK_LOST;  // reaches a crashed host: dropped, no ack
-        if (a < down_k) {
-          start = a > prev_done ? a : prev_done;
-          if (prev_done < a) {
-            status = 5u;  // idle: "task assigned" (:282-301)
-          } else if (prev_done > a) {
-            status = 4u;  // busy: "task queued" (:304-313)
-          } else {        // the previous task completes at the same tick
-            status = dl_k < (int64_t)prev_S * kTicksPerSecond ? 5u : 4u;
-          }
-          if (start != kNever) {  // start < down_k: prev_done is kNever or < down_k
-            done = start + ticks_of(min(S, kWideMaxS));
-            if (done >= down_k) done = kNever;  // the crash cancels its RELEASERESOURCE
-          }
-        }
-        lerr = (status != FOGNET_TASK_LOST && S > kWideMaxS) || a > kMaxTick || (done != kNever && done > kMaxTick);
-        if (!lerr) {
-          const int i = c0 + jp;
-          const uint64_t C = h.tl_C + S;
-          e[i] = WideEntry{a, done, C, S, h.tl, -1, 0};
-          if (h.npend == 0) {  // its completion advert is the node's next one
-            h.hd = i;
-            h.hd_done = done;
-            h.hd_C = C;
-            h.hd_S = S;
-            const int64_t x = done == kNever ? kNever : done + ul_k;
-            const int g = ((int)k / kWave) / kWideGroupSlots;
-            V.nxt[k / kWave] = x;
-            if (x < L.g_nxt[g * kWave + lane]) {
-              L.g_nxt[g * kWave + lane] = x;
-              L.g_j[g * kWave + lane] = (int)k;
-            }
-            if (x < mn) {
-              mn = x;
-              mj = (int)k;
-            }
-          } else if (h.npend == 1) {
-            h.hd_next = i;  // the tail is the head
-          } else {
-            e[h.tl].next = i;
-          }
-          h.tl = i;
-          h.tl_a = a;
-          h.tl_done = done;
-          h.tl_C = C;
-          h.tl_S = S;
-          h.npend += 1;
-          ch = h;
-          max_pend = max(max_pend, (uint32_t)h.npend);
-          const size_t o = tbase + (size_t)i;
-          if (!A.no_task_out) {  // (statistics-only replays keep no per-task outputs)
-            A.out_node[o] = (int32_t)k;
-            A.out_status[o] = (uint8_t)status;
-            A.out_start[o] = start == kNever ? -1 : start;
-            A.out_done[o] = done == kNever ? -1 : done;
-          }
-          if (done != kNever) {
-            acc_task(acc, t, a, start, done, S, status, hist ? L.hist : nullptr);
-            if (hist) atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - t)], 1u);
-          } else {
-            // node-down: acked at arrival (status 4/5) or lost; a queued task that
-            // started before the crash still emitted its queueTime (:238)
-            n_short += 1;
-            if (status == 5u) acc.n5 += 1u;
-            if (status == 4u) {
-              acc.n4 += 1u;
-              if (start != kNever)
-                acc_qtime(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, acc.qq_top, acc.qmin, acc.qmax, acc.nqt,
-                          acc.nqo, start, a, hist ? L.hist : nullptr);
-            }
-          }
-        }
+      // 3) node k's record and parameters, in its owner lane (cached there)
+      if (lane == kl && (int)k != cj) {
+        if (cj >= 0) nd[cj] = ch;  // write back the previous node's record
+        cj = (int)k;
+        ch = nd[k];
+        c_mips = A.mips[nbase + k];
+        c_dl = A.dl[nbase + k];
+        c_ul = A.ul[nbase + k];
+        c_down = A.down ? A.down[nbase + k] : kNever;
       }
-      if (ballot(lerr)) {
+      const int32_t mips_k = (int32_t)readlane_u32((uint32_t)c_mips, kl);
+      const int64_t dl_k = readlane_i64(c_dl, kl), ul_k = readlane_i64(c_ul, kl), down_k = readlane_i64(c_down, kl);
+      const int32_t tl = (int32_t)readlane_u32((uint32_t)ch.tl, kl);
+      const int32_t npend0 = (int32_t)readlane_u32((uint32_t)ch.npend, kl);
+      const int64_t tl_done = readlane_i64(ch.tl_done, kl);
+      const uint64_t tl_C = (uint64_t)readlane_i64((int64_t)ch.tl_C, kl);
+      const uint32_t tl_S = readlane_u32(ch.tl_S, kl);
+      const int64_t base_done = tl >= 0 ? tl_done : INT64_MIN;  // kNever: the node crashed with work left
+
+      // 4) the run: publishes jp .. jq-1 up to the earliest pending advert E
+      //    (an advert of any node may change the view) all go to node k; when
+      //    k has nothing pending, the run's first task becomes its head and
+      //    that task's advert bounds the run too
+      int jq = jp + 1;
+      if constexpr (!kExt) {
+        int64_t E = (int64_t)wave_min_u64((uint64_t)mn);
+        if (npend0 == 0) {
+          const uint32_t S0 = readlane_u32((uint32_t)cr, jp) / (uint32_t)mips_k;
+          const int64_t a0 = t + dl_k;
+          int64_t x0 = kNever;
+          if (a0 < down_k && base_done != kNever) {
+            const int64_t st0 = a0 > base_done ? a0 : base_done;
+            const int64_t d0 = st0 + ticks_of(min(S0, kWideMaxS));
+            if (st0 < down_k && d0 < down_k) x0 = d0 + ul_k;
+          }
+          E = x0 < E ? x0 : E;
+        }
+        const uint64_t run_mask = ballot((lane >= jp && lane < cnt && ca <= E) || lane == jp);
+        // the run is the contiguous lanes from jp (ticks are nondecreasing)
+        jq = jp + __popcll(run_mask >> jp);
+      }
+      const bool in_run = lane >= jp && lane < jq;
+      const int Lr = jq - jp;
+
+      // 5) task arrivals at node k (ComputeBrokerApp3.cc:269-320), one lane per
+      //    task: FIFO single server, done_m = max(a_m, done_{m-1}) + S_m
+      uint32_t S = 0u;
+      int64_t a = 0;
+      bool lerr2 = false;
+      if (in_run) {
+        S = (uint32_t)cr / (uint32_t)mips_k;  // double tskTime = requiredMIPS / MIPS (:276)
+        a = ca + dl_k;
+      }
+      const uint32_t Sd = min(S, kWideMaxS);  // (a larger service time is an error unless the task is lost)
+      const uint32_t Cs = wave_scan_add_u32(in_run ? Sd : 0u);  // service seconds of the run up to this task
+      const uint64_t C = tl_C + (uint64_t)Cs;                    // cumulative assigned service
+      int64_t start = kNever, done = kNever;
+      uint32_t status = FOGNET_TASK_LOST;
+      if (base_done != kNever) {
+        int64_t X = in_run ? (int64_t)((uint64_t)a - (uint64_t)ticks_of(Cs - Sd)) : INT64_MIN;
+        X = wave_scan_max_i64(X);
+        const int64_t dmax = base_done > X ? base_done : X;
+        const int64_t dn = (int64_t)((uint64_t)dmax + (uint64_t)ticks_of(Cs));  // unclamped
+        const int64_t st = dn - ticks_of(Sd);
+        const int64_t dn_up = dpp_or_i64<kDppWaveShr1>(0, dn);
+        const uint32_t S_up = dpp_or_u32<kDppWaveShr1>(0u, Sd);
+        const int64_t prev_done = lane == jp ? base_done : dn_up;
+        const uint32_t prev_S = lane == jp ? tl_S : S_up;
+        if (in_run && a < down_k) {
+          if (prev_done < a) status = 5u;       // idle: "task assigned" (:282-301)
+          else if (prev_done > a) status = 4u;  // busy: "task queued" (:304-313)
+          else status = dl_k < (int64_t)prev_S * kTicksPerSecond ? 5u : 4u;  // same-tick completion
+          start = st < down_k ? st : kNever;   // the crash cancels its RELEASERESOURCE
+          done = dn < down_k ? dn : kNever;
+        }
+      } else if (in_run && a < down_k) {
+        status = 4u;  // queued behind a task the crashed node never completes
+      }
+      lerr2 = in_run && ((status != FOGNET_TASK_LOST && S > kWideMaxS) || a > kMaxTick ||
+                         (done != kNever && done > kMaxTick));
+      if (ballot(lerr2)) {
         err = FOGNET_ERR_ARG;
         break;
       }
-      ++n_done;
+      // task entries: chained in publish order (consecutive task indices)
+      const int i = c0 + lane;
+      if (in_run) {
+        const int32_t prev = lane == jp ? tl : i - 1;
+        e[i] = WideEntry{a, done, C, S, prev, lane + 1 < jq ? i + 1 : -1, 0};
+        if (!A.no_task_out) {  // (statistics-only replays keep no per-task outputs)
+          const size_t o = tbase + (size_t)i;
+          A.out_node[o] = (int32_t)k;
+          A.out_status[o] = (uint8_t)status;
+          A.out_start[o] = start == kNever ? -1 : start;
+          A.out_done[o] = done == kNever ? -1 : done;
+        }
+        if (done != kNever) {
+          acc_task(acc, ca, a, start, done, S, status, hist ? L.hist : nullptr);
+          if (hist) atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - ca)], 1u);
+        } else {
+          // node-down: acked at arrival (status 4/5) or lost; a queued task that
+          // started before the crash still emitted its queueTime (:238)
+          n_short += 1;
+          if (status == 5u) acc.n5 += 1u;
+          if (status == 4u) {
+            acc.n4 += 1u;
+            if (start != kNever)
+              acc_qtime(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, acc.qq_top, acc.qmin, acc.qmax, acc.nqt,
+                        acc.nqo, start, a, hist ? L.hist : nullptr);
+          }
+        }
+      }
+
+      // 6) node k's record after the run (owner lane)
+      const int lz = jq - 1;
+      const int64_t a_z = readlane_i64(a, lz), done_z = readlane_i64(done, lz);
+      const uint64_t C_z = (uint64_t)readlane_i64((int64_t)C, lz);
+      const uint32_t S_z = readlane_u32(S, lz);
+      const int64_t done_f = readlane_i64(done, jp);
+      const uint64_t C_f = (uint64_t)readlane_i64((int64_t)C, jp);
+      const uint32_t S_f = readlane_u32(S, jp);
+      if (lane == kl) {
+        WideNode h = ch;
+        const int i0 = c0 + jp, iz = c0 + lz;
+        if (h.npend == 0) {  // the run's first task is the node's head: its advert is the node's next one
+          h.hd = i0;
+          h.hd_done = done_f;
+          h.hd_C = C_f;
+          h.hd_S = S_f;
+          const int64_t x = done_f == kNever ? kNever : done_f + ul_k;
+          const int g = ((int)k / kWave) / kWideGroupSlots;
+          V.nxt[k / kWave] = x;
+          if (x < L.g_nxt[g * kWave + lane]) {
+            L.g_nxt[g * kWave + lane] = x;
+            L.g_j[g * kWave + lane] = (int)k;
+          }
+          if (x < mn) {
+            mn = x;
+            mj = (int)k;
+          }
+          if (Lr > 1) h.hd_next = i0 + 1;
+        } else if (h.npend == 1) {
+          h.hd_next = i0;  // the tail is the head
+        } else {
+          e[h.tl].next = i0;
+        }
+        h.tl = iz;
+        h.tl_a = a_z;
+        h.tl_done = done_z;
+        h.tl_C = C_z;
+        h.tl_S = S_z;
+        h.npend += Lr;
+        ch = h;
+        max_pend = max(max_pend, (uint32_t)h.npend);
+      }
+      n_done += Lr;
+      jp = jq;
     }
   }
 

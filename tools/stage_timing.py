@@ -7,12 +7,13 @@ if os.environ.get("FOGNET_LIB"):  # time a variant build (tools/build_variant.sh
     _abi.LIB_PATH = os.environ["FOGNET_LIB"]
 import fognetsimpp_amd as fa
 
-R = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-T, N = 100_000, 256
+C5 = os.environ.get("WORKLOAD") == "c5"
+R = int(sys.argv[1]) if len(sys.argv) > 1 else (1024 if C5 else 4096)
+T, N = (10_000, 10_000) if C5 else (100_000, 256)
 dev = torch.device("cuda", 0)
 ctx = fa.Context(0)
-mg, sc = fa.sweep_params(np.arange(R), N)
-tr = fa.generate_trace(ctx, 0x5EED0003, R, T, N, mg, sc)
+mg, sc = (fa.c5_params if C5 else fa.sweep_params)(np.arange(R), N)
+tr = fa.generate_trace(ctx, 0x5EED0005 if C5 else 0x5EED0003, R, T, N, mg, sc)
 out = fa.allocate_outputs(R, T, dev, N=N, energy=False, hist=True)
 torch.cuda.synchronize()
 for stage in os.environ.get("FOGNET_STAGES", "all,replay,stats,all,replay").split(","):
