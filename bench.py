@@ -79,7 +79,10 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this job may use")
     ap.add_argument("--cpu-reps-1t", type=int, default=16, help="replications of the single-thread CPU sample")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--policy", default="REF_V3", choices=("REF_V3", "EXT_LAT"))
+    ap.add_argument("--policy", default=None, choices=("REF_V3", "EXT_LAT", "EXT_HIER"),
+                    help="default REF_V3; c5: EXT_HIER (hierarchical brokers + mobility handoff, BASELINE configs[4])")
+    ap.add_argument("--hier-threshold-s", type=int, default=60)
+    ap.add_argument("--hier-up-ms", type=int, default=20)
     ap.add_argument("--workload", default="c3", choices=("c1", "c3", "c4", "c5"))
     ap.add_argument("--R-total", type=int, default=None,
                     help="c4/c5: replications over all ranks (default 1,000,000 / 1024)")
@@ -87,6 +90,8 @@ def main():
                     help="c4: replications per device block (replay launches queue 4x the resident waves, so "
                          "waves that finish early are refilled)")
     args = ap.parse_args()
+    if args.policy is None:
+        args.policy = "EXT_HIER" if args.workload == "c5" else "REF_V3"
     if args.workload in ("c4", "c5"):
         if args.T == 100_000:
             args.T = 10_000
@@ -140,6 +145,9 @@ def main():
     pb, pi = fa.power_model(trace["mips"].cpu().numpy())
     trace["p_busy"] = torch.from_numpy(pb).to(dev)
     trace["p_idle"] = torch.from_numpy(pi).to(dev)
+    if args.policy == "EXT_HIER":  # each publish's regional broker under the mobility model
+        trace["region"] = fa.mobility_regions(trace["arrive"], N)
+    hier = dict(hier_threshold_s=args.hier_threshold_s, hier_up_tick=args.hier_up_ms * 10**9)
     out = fa.allocate_outputs(R, T, dev, N=N, energy=False, hist=True)
     torch.cuda.synchronize()
     log(f"[rank {rank}] trace generated R={R} T={T} N={N} in {time.time() - t0:.2f}s")
@@ -153,7 +161,7 @@ def main():
         if ev_a is not None:
             ev_a.record()
         # replay kernel with the statistics pass fused as its epilogue
-        fa.run_batch(ctx, trace, out, ring_capacity=args.ring, stage="all", policy=args.policy)
+        fa.run_batch(ctx, trace, out, ring_capacity=args.ring, stage="all", policy=args.policy, **hier)
         if ev_b is not None:
             ev_b.record()
         job_buf = torch.zeros(_abi.JOB_STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
@@ -236,8 +244,11 @@ def main():
             "config": {"workload": "C5 large topology (BASELINE.json configs[4])" if args.workload == "c5"
                        else "C3 policy sweep (BASELINE.json configs[2])", "R_per_gpu": R, "T": T, "N": N,
                        "R_total": args.R_total if args.workload == "c5" else R * world, "ring_capacity": args.ring,
-                       "policy": "REF_V3 (BrokerBaseApp3)" if args.policy == "REF_V3" else
-                       "EXT_LAT (north-star cost; not in the reference)",
+                       "policy": {"REF_V3": "REF_V3 (BrokerBaseApp3)",
+                                  "EXT_LAT": "EXT_LAT (north-star cost; not in the reference)",
+                                  "EXT_HIER": f"EXT_HIER (regional brokers of 1024 nodes + parent, mobility handoff, "
+                                              f"escalation above {args.hier_threshold_s} s, +{args.hier_up_ms} ms hop; "
+                                              f"not in the reference)"}[args.policy],
                        "parallelism": f"replications sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
@@ -500,8 +511,13 @@ def cpu_baseline(trace, args, R, T, N, out=None):
 
     reps = min(args.cpu_reps, R)
     h = {k: trace[k][:reps].cpu().numpy() for k in ("arrive", "req", "mips", "dl", "ul", "init")}
-    # the power model rides along when the device run used it (energy_j is part of the record compared)
+    # the power model rides along when the device run used it (energy_j is part of the record compared),
+    # and so do the policy and its inputs
     pw = {k: trace[k][:reps].cpu().numpy() for k in ("p_busy", "p_idle")} if "p_busy" in trace else {}
+    pw["policy"] = oracle_lib.POLICIES[args.policy]
+    if args.policy == "EXT_HIER":
+        pw.update(region=trace["region"][:reps].cpu().numpy(), hier_threshold_s=args.hier_threshold_s,
+                  hier_up_tick=args.hier_up_ms * 10**9)
     model, nproc, avail, cores = host_cpu_info()
     threads = max(1, min(args.cpu_threads, cores)) if args.cpu_threads > 0 else cores
     log(f"cpu baseline: {reps} replications on {threads} threads (host {nproc} CPUs, {avail} in this job's mask) ...")

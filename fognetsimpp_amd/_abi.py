@@ -27,10 +27,12 @@ TASK_QUEUED, TASK_STARTED, TASK_LOST = 4, 5, 9  # fognet_task_status
 FOGNET_POLICY_REF_V3 = 1
 FOGNET_POLICY_REF_V2 = 2
 FOGNET_POLICY_EXT_LAT = 16
+FOGNET_POLICY_EXT_HIER = 32
+HIER_REGION_NODES = 1024
 TICKS_PER_SECOND = 10**12
 # fognet_v2_action (BrokerBaseApp2 decision outcome)
 V2_LOCAL, V2_FORWARD, V2_DROPPED, V2_NO_NODES = 3, 4, 5, 6
-ABI_VERSION = 7
+ABI_VERSION = 8
 HIST_METRICS = 2  # 0 queueTime, 1 response
 HIST_BINS = 64
 COMM_ID_BYTES = 128  # FOGNET_COMM_ID_BYTES
@@ -112,6 +114,8 @@ class BatchIn(C.Structure):
         ("arrive_tick", C.c_void_p), ("req_mips", C.c_void_p), ("mips", C.c_void_p),
         ("dl_tick", C.c_void_p), ("ul_tick", C.c_void_p), ("init_adv_tick", C.c_void_p),
         ("p_busy_w", C.c_void_p), ("p_idle_w", C.c_void_p), ("down_tick", C.c_void_p),
+        ("region", C.c_void_p), ("hier_up_tick", C.c_int64), ("hier_threshold_s", C.c_int32),
+        ("pad_hier", C.c_int32),
     ]
 
 

@@ -93,8 +93,13 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   if (in->N == 0) return fail(c, FOGNET_ERR_NO_NODES, "N == 0 (BrokerBaseApp3.cc:268 reads brokers[0])");
   if (in->N > fognet::kWideMaxNodes)
     return fail(c, FOGNET_ERR_UNSUPPORTED, "N > 65536 (the wide replay kernel keeps 20 B of group minima per 16 nodes in LDS)");
-  if (in->policy != FOGNET_POLICY_REF_V3 && in->policy != FOGNET_POLICY_EXT_LAT)
+  if (in->policy != FOGNET_POLICY_REF_V3 && in->policy != FOGNET_POLICY_EXT_LAT && in->policy != FOGNET_POLICY_EXT_HIER)
     return fail(c, FOGNET_ERR_UNSUPPORTED, "unknown policy");
+  if (in->policy == FOGNET_POLICY_EXT_HIER) {
+    if (in->R > 0 && in->T > 0 && !in->region) return fail(c, FOGNET_ERR_ARG, "EXT_HIER needs the region array");
+    if (in->hier_threshold_s < 0 || in->hier_up_tick < 0 || in->hier_up_tick >= ((int64_t)1 << 50))
+      return fail(c, FOGNET_ERR_ARG, "EXT_HIER: threshold >= 0 and 0 <= up latency < 2^50 ticks");
+  }
   if ((in->p_busy_w == nullptr) != (in->p_idle_w == nullptr))
     return fail(c, FOGNET_ERR_ARG, "p_busy_w and p_idle_w must both be given or both be null");
   if (in->down_tick && in->p_busy_w)
@@ -131,6 +136,11 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   a->p_busy = in->p_busy_w;
   a->p_idle = in->p_idle_w;
   a->down = in->down_tick;
+  if (in->policy == FOGNET_POLICY_EXT_HIER) {
+    a->region = in->region;
+    a->hier_up = in->hier_up_tick;
+    a->hier_thr = in->hier_threshold_s;
+  }
   return FOGNET_OK;
 }
 
@@ -368,7 +378,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
   a.hist = out->hist;
   if (a.out_energy && !a.p_busy) return fail(c, FOGNET_ERR_ARG, "node_energy_j needs the power model (p_busy_w/p_idle_w)");
   hipError_t e = hipSuccess;
-  if (use_wide(a.N) || a.down) {
+  if (use_wide(a.N) || a.down || a.policy == FOGNET_POLICY_EXT_HIER) {  // (regions: the wide kernel's groups)
     // crashes are only modelled by the wide kernel; it accumulates the statistics while it replays, so the
     // statistics-only stage has nothing left to do
     if (!(which & 1)) return FOGNET_OK;
@@ -445,20 +455,29 @@ int fognet_run_batch(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out*
   const size_t HB = FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(int64_t);
   const bool pw = in->p_busy_w != nullptr;
   const bool dn = in->down_tick != nullptr;
-  // inputs 0..8, outputs 9..15
+  // inputs 0..8, outputs 9..15, region 16
   const void* hsrc[9] = {in->arrive_tick, in->req_mips, in->mips, in->dl_tick, in->ul_tick, in->init_adv_tick,
                          in->p_busy_w, in->p_idle_w, in->down_tick};
   const size_t isz[9] = {R * T * 8, R * T * 4, NR * N * 4, NR * N * 8, NR * N * 8, NR * N * 8,
                          pw ? NR * N * 8 : 0, pw ? NR * N * 8 : 0, dn ? NR * N * 8 : 0};
+  const bool rg = in->policy == FOGNET_POLICY_EXT_HIER && in->region != nullptr;
   void* hdst[7] = {out->node, out->status, out->start_tick, out->done_tick, out->stats, out->node_energy_j,
                    out->hist};
   const size_t osz[7] = {R * T * 4, R * T * 1, R * T * 8, R * T * 8, R * sizeof(fognet_rep_stats),
                          out->node_energy_j ? R * N * 8 : 0, out->hist ? HB : 0};
-  void* d[16] = {};
+  void* d[17] = {};
   auto cleanup = [&]() {
-    for (int i = 0; i < 16; ++i)
+    for (int i = 0; i < 17; ++i)
       if (d[i]) (void)hipFree(d[i]);
   };
+  if (rg) {
+    hipError_t e = hipMalloc(&d[16], R * T * 4 ? R * T * 4 : 8);
+    if (e == hipSuccess && R * T) e = hipMemcpyAsync(d[16], in->region, R * T * 4, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_fail(c, e, "region copy-in");
+    }
+  }
   for (int i = 0; i < 16; ++i) {
     const size_t sz = i < 9 ? isz[i] : osz[i - 9];
     if (i >= 6 && i < 8 && !pw) continue;
@@ -487,6 +506,7 @@ int fognet_run_batch(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out*
   din.p_busy_w = (const double*)d[6];
   din.p_idle_w = (const double*)d[7];
   din.down_tick = (const int64_t*)d[8];
+  din.region = (const int32_t*)d[16];
   fognet_batch_out dout = {(int32_t*)d[9], (uint8_t*)d[10], (int64_t*)d[11], (int64_t*)d[12],
                            (fognet_rep_stats*)d[13], (double*)d[14], (int64_t*)d[15]};
   rc = fognet_run_batch_dev(c, &din, &dout, c->stream);

@@ -186,6 +186,11 @@ struct ReplayArgs {
   // task; the register kernel writes to an internal [R][T] scratch instead
   // (its fused statistics epilogue reads the outputs back).
   int32_t no_task_out;
+  // FOGNET_POLICY_EXT_HIER (wide kernel): [R][T] regional broker per publish, escalation
+  // threshold (advertised busy seconds) and the escalated task's extra latency
+  const int32_t* region;
+  int64_t hier_up;
+  int32_t hier_thr;
 };
 
 // Internal per-replication status between the two replay kernels (never
@@ -209,7 +214,7 @@ struct WideEntry {
   uint32_t S;    // service seconds, requiredMIPS / MIPS (int division)
   int32_t prev;  // previous task on the same node (-1: none)
   int32_t next;  // next task on the same node (valid while this one is pending)
-  int32_t pad;
+  int32_t pad;   // 1: escalated to the parent broker (FOGNET_POLICY_EXT_HIER)
 };
 static_assert(sizeof(WideEntry) == 40, "wide entry is 40 B");
 
@@ -226,7 +231,7 @@ struct WideNode {
   int64_t tl_a;     // tail: arrival tick
   int64_t tl_done;  //       completion tick
   uint64_t tl_C;    //       cumulative service (0: no task yet) = the node's service seconds so far
-  uint32_t hd_S, tl_S;
+  uint32_t hd_S, tl_S;  // (bit 31 of tl_S: the tail was escalated, FOGNET_POLICY_EXT_HIER)
 };
 static_assert(sizeof(WideNode) == 64, "wide node record is one 64-B line");
 

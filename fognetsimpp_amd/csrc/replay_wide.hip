@@ -134,19 +134,22 @@ __device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn
 // are not done yet, a difference of cumulative sums; the head advances.
 // Returns false when the advertised busy time does not fit 32 bits.
 // h: node j's record (loaded from HBM or the lane's cached copy), updated in place.
-__device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, int64_t dl, int64_t ul,
+// up: FOGNET_POLICY_EXT_HIER's extra hop, which an escalated task (entry pad
+// != 0, bit 31 of the record's tl_S for the tail) took before its downlink:
+// the same-tick rule compares the arrival's own insertion tick.
+__device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, int64_t dl, int64_t ul, int64_t up,
                                              int64_t& nxt_j, uint32_t& busy_j) {
   // the entry after the head, loaded first: for the lane's cached node h is in
   // registers, so this load issues together with the group's view loads
   WideEntry nx{};
   if (h.npend >= 2) nx = e[h.hd_next];
   uint64_t c_arrived = h.hd_C;  // only the completing task itself ...
-  if (arrives_before(h.tl_a, h.hd_done, dl, h.hd_S)) {
+  if (arrives_before(h.tl_a, h.hd_done, dl + ((h.tl_S >> 31) ? up : 0), h.hd_S)) {
     c_arrived = h.tl_C;  // ... or everything up to the newest task (the common case)
   } else {
     for (int32_t x = e[h.tl].prev; x != h.hd;) {  // newest first
       const WideEntry ex = e[x];
-      if (arrives_before(ex.a, h.hd_done, dl, h.hd_S)) {
+      if (arrives_before(ex.a, h.hd_done, dl + (ex.pad ? up : 0), h.hd_S)) {
         c_arrived = ex.C;
         break;
       }
@@ -217,6 +220,8 @@ template <int POL>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
                                                 int64_t* VN, uint32_t* VB, unsigned char* w_lds) {
   constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
+  constexpr bool kHier = POL == FOGNET_POLICY_EXT_HIER;
+  constexpr bool kPerPublish = kExt || kHier;  // the decision depends on the publish itself
   const int lane = threadIdx.x;
   const int T = A.T, N = A.N;
   WideLds L;
@@ -288,9 +293,11 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     const bool live = lane < cnt;
     const int64_t ca = live ? A.arrive[tbase + c0 + lane] : kNever;
     const int32_t cr = live ? A.req[tbase + c0 + lane] : 0;
+    int32_t cg = 0;  // EXT_HIER: the publish's regional broker (region = group of the LDS minima)
+    if constexpr (kHier) cg = live ? A.region[tbase + c0 + lane] : 0;
     // trace preconditions: nondecreasing ticks, requirement >= 0, ticks < 2^61
     const int64_t prv = dpp_or_i64<kDppWaveShr1>(prev_t, ca);  // lane 0 gets prev_t
-    if (ballot(live && (ca < prv || cr < 0 || ca > kMaxTick))) {
+    if (ballot(live && (ca < prv || cr < 0 || ca > kMaxTick || (kHier && (cg < 0 || cg >= L.G))))) {
       err = FOGNET_ERR_ARG;
       break;
     }
@@ -315,7 +322,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           uint32_t gb[kWideGroupSlots];
           group_load(V, g, gx, gb);
           WideNode h = hit ? ch : nd[j];
-          lerr |= !apply_advert(h, e, hit ? c_dl : A.dl[nbase + j], hit ? c_ul : A.ul[nbase + j], nxt_j, busy_j);
+          lerr |= !apply_advert(h, e, hit ? c_dl : A.dl[nbase + j], hit ? c_ul : A.ul[nbase + j], kHier ? A.hier_up : 0,
+                                nxt_j, busy_j);
           if (hit) ch = h;
           else nd[j] = h;
           V.nxt[sl] = nxt_j;
@@ -330,6 +338,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       }
 
       // 2) the decision over the advertised view
+      bool escalated = false;
       if constexpr (kExt) {
         // north-star cost (fognet_hip.h FOGNET_POLICY_EXT_LAT), first index on ties; per publish
         const uint32_t rq = readlane_u32((uint32_t)cr, jp);
@@ -345,6 +354,13 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         }
         const uint64_t m = wave_min_u64(mc);
         k = wave_min_u32(mc == m ? mjj : ~0u);
+      } else if constexpr (kHier) {
+        // regional broker: the smallest (busy, index) of its region (the region's LDS group
+        // minima, one per lane); above the threshold the parent takes the global one
+        const int b = __builtin_amdgcn_readlane(cg, jp);
+        const uint64_t kb = wave_min_u64(L.g_key[b * kWave + lane]);
+        escalated = (kb >> 32) > (uint64_t)A.hier_thr;
+        k = escalated ? (uint32_t)wave_min_u64(mk) : (uint32_t)kb;
       } else if (view_changed) {
         // BrokerBaseApp3.cc:267-281: busy_j + req/mips_0 < tempp over exact
         // integer busy values <=> the smallest (busy, j)
@@ -364,12 +380,14 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         c_down = A.down ? A.down[nbase + k] : kNever;
       }
       const int32_t mips_k = (int32_t)readlane_u32((uint32_t)c_mips, kl);
-      const int64_t dl_k = readlane_i64(c_dl, kl), ul_k = readlane_i64(c_ul, kl), down_k = readlane_i64(c_down, kl);
+      // (an escalated task takes the regional -> parent hop before the downlink)
+      const int64_t dl_k = readlane_i64(c_dl, kl) + (escalated ? A.hier_up : 0);
+      const int64_t ul_k = readlane_i64(c_ul, kl), down_k = readlane_i64(c_down, kl);
       const int32_t tl = (int32_t)readlane_u32((uint32_t)ch.tl, kl);
       const int32_t npend0 = (int32_t)readlane_u32((uint32_t)ch.npend, kl);
       const int64_t tl_done = readlane_i64(ch.tl_done, kl);
       const uint64_t tl_C = (uint64_t)readlane_i64((int64_t)ch.tl_C, kl);
-      const uint32_t tl_S = readlane_u32(ch.tl_S, kl);
+      const uint32_t tl_S = readlane_u32(ch.tl_S, kl) & 0x7FFFFFFFu;  // (bit 31: the tail was escalated)
       const int64_t base_done = tl >= 0 ? tl_done : INT64_MIN;  // kNever: the node crashed with work left
 
       // 4) the run: publishes jp .. jq-1 up to the earliest pending advert E
@@ -377,7 +395,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       //    k has nothing pending, the run's first task becomes its head and
       //    that task's advert bounds the run too
       int jq = jp + 1;
-      if constexpr (!kExt) {
+      if constexpr (!kPerPublish) {
         int64_t E = (int64_t)wave_min_u64((uint64_t)mn);
         if (npend0 == 0) {
           const uint32_t S0 = readlane_u32((uint32_t)cr, jp) / (uint32_t)mips_k;
@@ -441,7 +459,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       const int i = c0 + lane;
       if (in_run) {
         const int32_t prev = lane == jp ? tl : i - 1;
-        e[i] = WideEntry{a, done, C, S, prev, lane + 1 < jq ? i + 1 : -1, 0};
+        e[i] = WideEntry{a, done, C, S, prev, lane + 1 < jq ? i + 1 : -1, escalated ? 1 : 0};
         if (!A.no_task_out) {  // (statistics-only replays keep no per-task outputs)
           const size_t o = tbase + (size_t)i;
           A.out_node[o] = (int32_t)k;
@@ -503,7 +521,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         h.tl_a = a_z;
         h.tl_done = done_z;
         h.tl_C = C_z;
-        h.tl_S = S_z;
+        h.tl_S = S_z | (escalated ? 0x80000000u : 0u);
         h.npend += Lr;
         ch = h;
         max_pend = max(max_pend, (uint32_t)h.npend);
@@ -584,6 +602,8 @@ hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slot
   const size_t lds = replay_wide_lds_bytes(a.N);
   if (a.policy == FOGNET_POLICY_EXT_LAT)
     launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, slots, e, nd, vn, vb, lds, s);
+  else if (a.policy == FOGNET_POLICY_EXT_HIER)
+    launch_wide_pol<FOGNET_POLICY_EXT_HIER>(a, slots, e, nd, vn, vb, lds, s);
   else
     launch_wide_pol<FOGNET_POLICY_REF_V3>(a, slots, e, nd, vn, vb, lds, s);
   return hipGetLastError();

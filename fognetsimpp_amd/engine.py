@@ -30,9 +30,11 @@ _TENSOR_DTYPES = {
     "dl": torch.int64, "ul": torch.int64, "init": torch.int64, "first_adv": torch.int64,
     "p_busy": torch.float64, "p_idle": torch.float64,  # optional power model (a11)
     "down": torch.int64,  # optional node crash ticks (node-down extension)
+    "region": torch.int32,  # EXT_HIER: regional broker of each publish [R, T]
 }
 NEVER = np.iinfo(np.int64).max  # down tick of a node that never crashes
-POLICIES = {"REF_V3": _abi.FOGNET_POLICY_REF_V3, "EXT_LAT": _abi.FOGNET_POLICY_EXT_LAT}
+POLICIES = {"REF_V3": _abi.FOGNET_POLICY_REF_V3, "EXT_LAT": _abi.FOGNET_POLICY_EXT_LAT,
+            "EXT_HIER": _abi.FOGNET_POLICY_EXT_HIER}
 
 
 def _ptr(t):
@@ -219,11 +221,14 @@ def as_device_trace(trace: dict, device) -> dict:
     if out["arrive"].dim() == 1:
         out["arrive"] = out["arrive"].unsqueeze(0)
         out["req"] = out["req"].unsqueeze(0)
+        if "region" in out:
+            out["region"] = out["region"].unsqueeze(0)
     return out
 
 
 def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_capacity: int = 0,
-              stream=None, stage: str = "all", policy: str | int = "REF_V3", hist: bool = False) -> BatchResult:
+              stream=None, stage: str = "all", policy: str | int = "REF_V3", hist: bool = False,
+              hier_threshold_s: int = 60, hier_up_tick: int = 20 * 10**9) -> BatchResult:
     """Enqueue R trace replays (fognet_run_batch_dev) on the current stream.
 
     ``trace``: device tensors arrive/req [R, T], node params mips/dl/ul/init
@@ -232,8 +237,12 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
     (same shape as mips, NEVER = no crash; ComputeBrokerApp3::handleNodeCrash,
     ComputeBrokerApp3.cc:423-427: lost tasks get status 9).  ``stage``: "all", "replay"
     (fognet_replay_dev) or "stats" (fognet_rep_stats_dev).  ``policy``:
-    "REF_V3" (BrokerBaseApp3) or "EXT_LAT" (north-star cost, not in the
-    reference).  ``hist``: allocate the job histogram when ``out`` is None.
+    "REF_V3" (BrokerBaseApp3), "EXT_LAT" (north-star cost) or "EXT_HIER"
+    (hierarchical brokers with mobility handoff: needs ``trace["region"]``
+    [R, T], see :func:`mobility_regions`; escalation above
+    ``hier_threshold_s`` busy seconds, extra hop ``hier_up_tick``); the two
+    extensions are not in the reference.  ``hist``: allocate the job
+    histogram when ``out`` is None.
     """
     arrive, req = trace["arrive"], trace["req"]
     R, T = arrive.shape
@@ -254,9 +263,13 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
         raise FognetError(_abi.FOGNET_ERR_ARG, "output buffers too small for the trace")
     if out is None:
         out = allocate_outputs(R, T, arrive.device, N=N, energy=energy, hist=hist)
+    region = trace.get("region")
+    if pol == _abi.FOGNET_POLICY_EXT_HIER and (region is None or tuple(region.shape) != (R, T)):
+        raise FognetError(_abi.FOGNET_ERR_ARG, "EXT_HIER needs trace['region'] of shape [R, T]")
     bi = _abi.BatchIn(R, T, N, pol, stride, ring_capacity,
                       _ptr(arrive), _ptr(req), _ptr(mips), _ptr(trace["dl"]), _ptr(trace["ul"]),
-                      _ptr(trace["init"]), _ptr(trace.get("p_busy")), _ptr(trace.get("p_idle")), _ptr(down))
+                      _ptr(trace["init"]), _ptr(trace.get("p_busy")), _ptr(trace.get("p_idle")), _ptr(down),
+                      _ptr(region), int(hier_up_tick), int(hier_threshold_s), 0)
     bo = _abi.BatchOut(_ptr(out.node), _ptr(out.status), _ptr(out.start_tick), _ptr(out.done_tick),
                        _ptr(out.stats), _ptr(out.node_energy), _ptr(out.hist))
     s = C.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(arrive.device)
@@ -479,6 +492,32 @@ def c5_params(r_global: np.ndarray, N: int, req_lo=1000, req_hi=64000):
     mips = 1000.0 * (1 + (np.arange(N) % 4))
     es = 0.5 * (req_lo + req_hi) * float(np.mean(1.0 / mips))
     return es / (N * rho) * _abi.TICKS_PER_SECOND, sc
+
+
+def mobility_regions(arrive, N: int, users: int = 256, period_s=(30, 45, 60, 75)):
+    """Regional broker of every publish under a builder-defined mobility model
+    (FOGNET_POLICY_EXT_HIER; not in the reference, whose only mobility is the
+    users' radio mobility, simulations/example/wirelessNet.ini:13-29): publish i
+    of a replication comes from user u = i mod ``users``; user u starts in
+    region u mod B (B = ceil(N / 1024) regions of 1024 consecutive nodes) and
+    hands off to the next region (+1 for even u, -1 for odd u, mod B) every
+    period_s[u mod 4] seconds from the replication's first publish.  Integer
+    arithmetic only, so numpy (host) and torch (device) give the same regions.
+    ``arrive``: [R, T] int64 ticks (numpy array or tensor); returns int32 [R, T]."""
+    B = -(-N // _abi.HIER_REGION_NODES)
+    torch_in = isinstance(arrive, torch.Tensor)
+    xp = torch if torch_in else np
+    R, T = arrive.shape
+    i = xp.arange(T, device=arrive.device) if torch_in else np.arange(T)
+    u = (i % users).to(torch.int64) if torch_in else (i % users).astype(np.int64)
+    per = [p * _abi.TICKS_PER_SECOND for p in period_s]
+    period = (torch.tensor(per, device=arrive.device, dtype=torch.int64) if torch_in else np.array(per, np.int64))[u % 4]
+    sign = 1 - 2 * (u % 2)
+    t0 = arrive[:, :1]
+    hops = (arrive - t0) // period
+    reg = (u % B) + sign * hops
+    reg = reg % B  # floor modulo in both numpy and torch
+    return reg.to(torch.int32) if torch_in else reg.astype(np.int32)
 
 
 def power_model(mips) -> tuple[np.ndarray, np.ndarray]:

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define FOGNET_ABI_VERSION 7
+#define FOGNET_ABI_VERSION 8
 #define FOGNET_TICKS_PER_SECOND 1000000000000LL
 
 /* Latency histograms (device-side statistics, summed over replications; the
@@ -75,12 +75,26 @@ typedef enum fognet_policy {
                                    (fognet_decide_v2; needs the broker's own MIPS)                 */
     FOGNET_POLICY_REF_V3 = 1,   /* BrokerBaseApp3: argmin(busy_j + req / mips_0), int division,
                                    strict '<' (ties -> lowest index), stale advertised view      */
-    FOGNET_POLICY_EXT_LAT = 16  /* north-star cost, NOT in the reference (parity vs the oracle's
+    FOGNET_POLICY_EXT_LAT = 16, /* north-star cost, NOT in the reference (parity vs the oracle's
                                    restatement only): argmin over j of
                                    dl_j + adv_busy_j * 1e12 + (req / mips_j) * 1e12 ticks
                                    (int division by the node's OWN MIPS, exact int64 ticks,
                                    ties -> lowest index); same stale view and node model      */
+    FOGNET_POLICY_EXT_HIER = 32 /* hierarchical brokers with mobility handoff (BASELINE.json C5), NOT
+                                   in the reference (one flat broker, BrokerBaseApp3.cc:271-279):
+                                   the nodes form regions of FOGNET_HIER_REGION_NODES consecutive
+                                   indices, each with a regional broker; publish t reaches the
+                                   broker of region[t] (the user's region when it publishes: a
+                                   handoff changes it).  That broker applies BrokerBaseApp3's rule
+                                   inside its region: the smallest (advertised busy, index).  If
+                                   that busy exceeds hier_threshold_s the task is escalated to the
+                                   parent broker, which applies the rule over ALL nodes, and
+                                   reaches its node hier_up_tick later (the extra hop).  Adverts
+                                   reach every broker with the node's uplink latency.         */
 } fognet_policy;
+
+/* Region size of FOGNET_POLICY_EXT_HIER (node r * 1024 .. r * 1024 + 1023 form region r). */
+#define FOGNET_HIER_REGION_NODES 1024
 
 /* Outcome of one BrokerBaseApp2 decision (BrokerBaseApp2.cc:180-192, 235-286). */
 typedef enum fognet_v2_action {
@@ -188,6 +202,13 @@ typedef struct fognet_batch_in {
      * tick.  Replays with crashes run on the wide kernel; not combinable with the power
      * model (ERR_UNSUPPORTED); not stored in trace files (fognet_io.h). */
     const int64_t *down_tick;
+    /* FOGNET_POLICY_EXT_HIER only (ignored otherwise): [R][T] region of each publish's
+     * regional broker (0 <= region < ceil(N / FOGNET_HIER_REGION_NODES)), the busy seconds
+     * above which a regional broker escalates, the extra latency of an escalated task. */
+    const int32_t *region;
+    int64_t hier_up_tick;
+    int32_t hier_threshold_s;
+    int32_t pad_hier;
 } fognet_batch_in;
 
 /* Per-task status (fognet_batch_out.status). */

@@ -414,6 +414,28 @@ int orc_decide_ext_lat(int32_t n, const double *adv_busy, const int32_t *mips, c
     return ORC_OK;
 }
 
+int orc_decide_hier(int32_t n, const double *adv_busy, const int32_t *adv_mips, int32_t region, int32_t threshold_s,
+                    int32_t req, int32_t *out_node, int32_t *escalated) {
+    /* Extension (fognet_hip.h FOGNET_POLICY_EXT_HIER; not in the reference): the regional
+     * broker runs BrokerBaseApp3's rule (BrokerBaseApp3.cc:267-281) over its own node list,
+     * nodes region*1024 .. region*1024+1023, and escalates to the parent, which runs it over
+     * every node, when its choice's advertised busy time exceeds the threshold. */
+    int32_t lo = region * ORC_HIER_REGION_NODES, hi = lo + ORC_HIER_REGION_NODES;
+    if (region < 0 || lo >= n) return ORC_ERR_ARG;
+    if (hi > n) hi = n;
+    int32_t k;
+    int rc = orc_decide_v3(hi - lo, adv_busy + lo, adv_mips + lo, req, &k);
+    if (rc) return rc;
+    k += lo;
+    *escalated = adv_busy[k] > (double)threshold_s;
+    if (*escalated) {
+        rc = orc_decide_v3(n, adv_busy, adv_mips, req, &k);
+        if (rc) return rc;
+    }
+    *out_node = k;
+    return ORC_OK;
+}
+
 int orc_decide_v2(int32_t n, const int32_t *adv_mips, int32_t local_mips, int32_t req, int32_t *out_node,
                   int32_t *out_action) {
     /* BrokerBaseApp2::handleMessageWhenUp, MqttMsgPublish branch (BrokerBaseApp2.cc:180-192) */
@@ -452,8 +474,12 @@ static int broker_publish(sim_t *s, int64_t t) {
         rc = send_ack(s, 1, -1, t, 4);                    /* pubAck status 4 (:145-150) */
         if (rc) return rc;
     }
+    int32_t escalated = 0;
     if (s->in->policy == ORC_POLICY_EXT_LAT)
         rc = orc_decide_ext_lat(s->in->n_nodes, s->adv_busy, s->in->mips, s->in->dl_tick, s->in->req_mips[t], &k);
+    else if (s->in->policy == ORC_POLICY_EXT_HIER)
+        rc = orc_decide_hier(s->in->n_nodes, s->adv_busy, s->adv_mips, s->in->region ? s->in->region[t] : -1,
+                             s->in->hier_threshold_s, s->in->req_mips[t], &k, &escalated);
     else
         rc = orc_decide_v3(s->in->n_nodes, s->adv_busy, s->adv_mips, s->in->req_mips[t], &k);
     if (rc) return rc;
@@ -462,10 +488,11 @@ static int broker_publish(sim_t *s, int64_t t) {
     node_t *nd = &s->nodes[k];
     nd->pending++;
     if (nd->pending > s->st.max_pending) s->st.max_pending = (int32_t)nd->pending;
-    /* socket.sendTo(tsk, brokers[k]) (:302): delivered one downlink latency later */
+    /* socket.sendTo(tsk, brokers[k]) (:302): delivered one downlink latency later (an escalated
+     * task first takes the regional -> parent hop) */
     ev_t e;
     memset(&e, 0, sizeof e);
-    e.tick = s->now + s->in->dl_tick[k];
+    e.tick = s->now + s->in->dl_tick[k] + (escalated ? s->in->hier_up_tick : 0);
     e.type = EV_TASK;
     e.node = k;
     e.task = t;
@@ -686,6 +713,9 @@ typedef struct {
     const int64_t *user_ul, *user_dl;
     int32_t user_per_task;
     const int64_t *down;
+    const int32_t *region;
+    int32_t hier_threshold_s;
+    int64_t hier_up_tick;
     int32_t *node;
     uint8_t *status;
     int64_t *start_tick, *done_tick;
@@ -710,7 +740,8 @@ static void *batch_worker(void *arg) {
                          b->dl + no, b->ul + no, b->init_adv + no,
                          b->p_busy ? b->p_busy + no : 0, b->p_idle ? b->p_idle + no : 0, b->policy,
                          b->user_ul ? b->user_ul + uo : 0, b->user_dl ? b->user_dl + uo : 0, b->user_per_task,
-                         b->down ? b->down + no : 0};
+                         b->down ? b->down + no : 0, b->region ? b->region + to : 0, b->hier_threshold_s,
+                         b->hier_up_tick};
         orc_rep_out out = {b->node ? b->node + to : 0, b->status ? b->status + to : 0,
                            b->start_tick ? b->start_tick + to : 0, b->done_tick ? b->done_tick + to : 0,
                            0, b->stats ? b->stats + r : 0,
@@ -764,9 +795,23 @@ int orc_run_batch4(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t
                    int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
                    orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
                    int threads) {
+    return orc_run_batch5(R, T, N, node_stride, policy, arrive_tick, req_mips, mips, dl, ul, init_adv, p_busy_w,
+                          p_idle_w, user_ul, user_dl, user_per_task, down_tick, 0, 0, 0, node, status, start_tick,
+                          done_tick, stats, node_energy_j, hist, user_stats, threads);
+}
+
+int orc_run_batch5(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
+                   const int64_t *arrive_tick, const int32_t *req_mips,
+                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                   const double *p_busy_w, const double *p_idle_w,
+                   const int64_t *user_ul, const int64_t *user_dl, int32_t user_per_task,
+                   const int64_t *down_tick, const int32_t *region, int32_t hier_threshold_s, int64_t hier_up_tick,
+                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                   orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
+                   int threads) {
     batch_t b = {R, N, node_stride, policy, T, arrive_tick, req_mips, mips, dl, ul, init_adv, p_busy_w, p_idle_w,
-                 user_ul, user_dl, user_per_task, down_tick, node, status, start_tick, done_tick, stats,
-                 node_energy_j, hist, user_stats, 0};
+                 user_ul, user_dl, user_per_task, down_tick, region, hier_threshold_s, hier_up_tick, node, status,
+                 start_tick, done_tick, stats, node_energy_j, hist, user_stats, 0};
     pthread_mutex_init(&b.mu, 0);
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;

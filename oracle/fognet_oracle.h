@@ -36,8 +36,10 @@ enum {
 /* Broker allocation policies (values mirror include/fognet_hip.h). */
 enum {
     ORC_POLICY_REF_V3 = 1,  /* BrokerBaseApp3::sendPubAck, BrokerBaseApp3.cc:265-281            */
-    ORC_POLICY_EXT_LAT = 16 /* north-star cost (not in the reference): dl_j + busy_j + req/mips_j */
+    ORC_POLICY_EXT_LAT = 16, /* north-star cost (not in the reference): dl_j + busy_j + req/mips_j */
+    ORC_POLICY_EXT_HIER = 32 /* hierarchical brokers + mobility handoff (not in the reference; fognet_hip.h) */
 };
+#define ORC_HIER_REGION_NODES 1024
 
 /* Histograms (fognet_hip.h FOGNET_HIST_*): metric 0 queueTime, 1 response. */
 #define ORC_HIST_METRICS 2
@@ -67,6 +69,11 @@ typedef struct {
      * [N] tick at which node j crashes, INT64_MAX = never; nullable.  The
      * crash precedes every model event of its tick; must be >= init_adv_tick. */
     const int64_t *down_tick;
+    /* ORC_POLICY_EXT_HIER: [T] region of each publish's broker, escalation threshold (busy
+     * seconds) and the escalated task's extra latency (ticks) */
+    const int32_t *region;
+    int32_t hier_threshold_s;
+    int64_t hier_up_tick;
 } orc_rep_in;
 
 /* Task status of a task that reached a crashed node (no ack, never served). */
@@ -148,6 +155,13 @@ int orc_decide_v3(int32_t n, const double *adv_busy, const int32_t *adv_mips, in
  * dl_j + adv_busy_j * 1e12 + (req / mips_j) * 1e12 in int64 ticks, ties -> lowest j. */
 int orc_decide_ext_lat(int32_t n, const double *adv_busy, const int32_t *mips, const int64_t *dl, int32_t req,
                        int32_t *out_node);
+
+/* Hierarchical brokers (ORC_POLICY_EXT_HIER): the broker of region r takes the
+ * smallest (advertised busy, index) among nodes r*1024 .. min(n, r*1024+1024)-1;
+ * if that busy exceeds threshold_s the parent takes it over all n nodes
+ * (*escalated = 1). */
+int orc_decide_hier(int32_t n, const double *adv_busy, const int32_t *adv_mips, int32_t region, int32_t threshold_s,
+                    int32_t req, int32_t *out_node, int32_t *escalated);
 
 /* BrokerBaseApp2 (v2 policy) decision, BrokerBaseApp2.cc:180-192 (publish
  * branch) + 235-270 (sendPubAck(status=false)): served by the broker itself if
@@ -252,6 +266,17 @@ int orc_run_batch3(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t
                    int threads);
 
 /* orc_run_batch3 plus the node-down extension: down_tick [R|1][N] (nullable). */
+/* orc_run_batch4 + the EXT_HIER inputs: region [R][T] (nullable), threshold, up latency. */
+int orc_run_batch5(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
+                   const int64_t *arrive_tick, const int32_t *req_mips,
+                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                   const double *p_busy_w, const double *p_idle_w,
+                   const int64_t *user_ul, const int64_t *user_dl, int32_t user_per_task,
+                   const int64_t *down_tick, const int32_t *region, int32_t hier_threshold_s, int64_t hier_up_tick,
+                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                   orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
+                   int threads);
+
 int orc_run_batch4(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
                    const int64_t *arrive_tick, const int32_t *req_mips,
                    const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,

@@ -39,8 +39,8 @@ MOMENTS_DTYPE = np.dtype([("count", np.int64), ("min_raw", np.int64), ("max_raw"
                           ("sq_top", np.uint64), ("overflow", np.int64)])
 USER_SIGNALS = ("delay", "latency", "latencyH1", "taskTime")
 USER_STATS_DTYPE = np.dtype([(n, MOMENTS_DTYPE) for n in USER_SIGNALS])
-POLICY_REF_V3, POLICY_EXT_LAT = 1, 16
-POLICIES = {"REF_V3": POLICY_REF_V3, "EXT_LAT": POLICY_EXT_LAT}
+POLICY_REF_V3, POLICY_EXT_LAT, POLICY_EXT_HIER = 1, 16, 32
+POLICIES = {"REF_V3": POLICY_REF_V3, "EXT_LAT": POLICY_EXT_LAT, "EXT_HIER": POLICY_EXT_HIER}
 
 _lib = None
 
@@ -67,6 +67,12 @@ def lib():
         _lib.orc_run_batch4.argtypes = ([C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [p] * 10 +
                                         [C.c_int32] + [p] * 9 + [C.c_int])
         _lib.orc_run_batch4.restype = C.c_int
+        _lib.orc_run_batch5.argtypes = ([C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [p] * 10 +
+                                        [C.c_int32, p, p, C.c_int32, C.c_int64] + [p] * 8 + [C.c_int])
+        _lib.orc_run_batch5.restype = C.c_int
+        _lib.orc_decide_hier.argtypes = [C.c_int32, p, p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_int32)]
+        _lib.orc_decide_hier.restype = C.c_int
         _lib.orc_decide_ext_lat.argtypes = [C.c_int32, p, p, p, C.c_int32, C.POINTER(C.c_int32)]
         _lib.orc_decide_ext_lat.restype = C.c_int
         _lib.orc_hist_bin.argtypes = [C.c_int64]
@@ -131,14 +137,26 @@ def decide_ext_lat(adv_busy, mips, dl, req):
     return rc, out.value
 
 
+def decide_hier(adv_busy, adv_mips, region, threshold_s, req):
+    """EXT_HIER decision: (rc, node, escalated)."""
+    adv_busy = np.ascontiguousarray(adv_busy, dtype=np.float64)
+    adv_mips = np.ascontiguousarray(adv_mips, dtype=np.int32)
+    k, esc = C.c_int32(-7), C.c_int32(-7)
+    rc = lib().orc_decide_hier(len(adv_busy), _ptr(adv_busy), _ptr(adv_mips), int(region), int(threshold_s), int(req),
+                               C.byref(k), C.byref(esc))
+    return rc, k.value, esc.value
+
+
 def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool = True, policy: int = 1,
-              p_busy=None, p_idle=None, hist: bool = False, user_ul=None, user_dl=None, down=None):
+              p_busy=None, p_idle=None, hist: bool = False, user_ul=None, user_dl=None, down=None, region=None,
+              hier_threshold_s: int = 60, hier_up_tick: int = 20 * 10**9):
     """Replay R replications.  arrive/req: [R,T]; node params [R,N] or [N] (shared).
     ``p_busy``/``p_idle`` (same shape as mips) enable the energy model; ``hist``
     returns per-replication histograms [R, 2, 64]; ``user_ul``/``user_dl``
     ([R] one user per replication, or [R, T] per task) model the publishing
     users' links and return the user-side signals as ``user`` [R] (USER_STATS_DTYPE).
-    ``down`` (same shape as mips, INT64_MAX = never): node crash ticks."""
+    ``down`` (same shape as mips, INT64_MAX = never): node crash ticks.
+    ``region`` ([R, T] int32): the EXT_HIER regional broker of each publish."""
     arrive = np.ascontiguousarray(np.atleast_2d(arrive), dtype=np.int64)
     req = np.ascontiguousarray(np.atleast_2d(req), dtype=np.int32)
     R, T = arrive.shape
@@ -165,8 +183,10 @@ def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool =
         user = np.zeros(R, USER_STATS_DTYPE)
     stats = (OrcRepStats * R)()
     dn = np.ascontiguousarray(down, dtype=np.int64) if down is not None else None
-    lib().orc_run_batch4(R, T, N, stride, policy, _ptr(arrive), _ptr(req), _ptr(mips), _ptr(dl), _ptr(ul),
-                         _ptr(init), _ptr(pb), _ptr(pi), _ptr(uu), _ptr(ud), per_task, _ptr(dn), _ptr(node),
+    rg = np.ascontiguousarray(np.atleast_2d(region), dtype=np.int32) if region is not None else None
+    lib().orc_run_batch5(R, T, N, stride, policy, _ptr(arrive), _ptr(req), _ptr(mips), _ptr(dl), _ptr(ul),
+                         _ptr(init), _ptr(pb), _ptr(pi), _ptr(uu), _ptr(ud), per_task, _ptr(dn), _ptr(rg),
+                         int(hier_threshold_s), int(hier_up_tick), _ptr(node),
                          _ptr(status),
                          _ptr(start), _ptr(done), C.cast(stats, C.c_void_p), _ptr(energy), _ptr(h), _ptr(user),
                          threads)

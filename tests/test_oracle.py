@@ -380,3 +380,59 @@ def test_v2_node_reproduces_general0_recording():
     np.testing.assert_array_equal(o["start"][0], d["task_arrival_ticks"])
     np.testing.assert_array_equal(o["done"][0], d["release_ticks"])
     assert o["stats"]["n_released_node"][0] == 4
+
+
+def hier_kat():
+    """Hand-traced EXT_HIER replay (hierarchical brokers; not in the reference):
+    N = 1025 nodes -> region 0 = nodes 0..1023, region 1 = node 1024; MIPS 1000,
+    dl = ul = 1 ms, escalation above 1 busy second, extra hop 5 ms.
+      t0 1.0 s   r0 req 3000: view all 0 -> node 0, starts 1.001, done 4.001
+      t1 1.5 s   r0 req 2000: view unchanged -> node 0, queued, 4.001 .. 6.001
+      t2 5.0 s   r0 req 1000: node 0's advert (4.002) says busy 2 -> region
+                 minimum node 1 (busy 0) -> 1.001 + ... starts 5.001, done 6.001
+      t3 5.5 s   r1 req 4000: node 1024 (busy 0), starts 5.501, done 9.501
+      t4 7.0 s   r1 req 3000: node 1024 (its view still 0), queued 9.501 .. 12.501
+      t5 9.6 s   r1 req 1000: node 1024's advert (9.502) says busy 3 > 1 ->
+                 escalated: the parent's minimum is node 0 (its 6.002 advert: 0),
+                 arriving 9.6 + 1 ms + 5 ms = 9.606, idle -> starts at once."""
+    ms, sec = 10**9, 10**12
+    N = 1025
+    tr = dict(arrive=np.array([[sec, 1500 * ms, 5 * sec, 5500 * ms, 7 * sec, 9600 * ms]], np.int64),
+              req=np.array([[3000, 2000, 1000, 4000, 3000, 1000]], np.int32), mips=np.full(N, 1000, np.int32),
+              dl=np.full(N, ms, np.int64), ul=np.full(N, ms, np.int64), init=np.full(N, ms, np.int64),
+              region=np.array([[0, 0, 0, 1, 1, 1]], np.int32))
+    exp = dict(node=[0, 0, 1, 1024, 1024, 0], status=[5, 4, 5, 5, 4, 5],
+               start=[1001 * ms, 4001 * ms, 5001 * ms, 5501 * ms, 9501 * ms, 9606 * ms],
+               done=[4001 * ms, 6001 * ms, 6001 * ms, 9501 * ms, 12501 * ms, 10606 * ms])
+    return tr, exp, dict(hier_threshold_s=1, hier_up_tick=5 * ms)
+
+
+def test_hier_decide_known_answers():
+    busy = np.array([5.0] * 1024 + [1.0] + [9.0] * 10)
+    mips = np.full(busy.size, 1000, np.int32)
+    assert ol.decide_hier(busy, mips, 0, 3, 1000) == (0, 1024, 1)  # region 0 all above 3 s: the parent's minimum
+    busy[:1024] = 2.0
+    assert ol.decide_hier(busy, mips, 0, 3, 1000) == (0, 0, 0)  # region 0, lowest index among equal busy
+    assert ol.decide_hier(busy, mips, 1, 3, 1000) == (0, 1024, 0)
+    assert ol.decide_hier(busy, mips, 2, 3, 1000)[0] == 1  # no region 2 (ORC_ERR_ARG)
+
+
+def test_hier_replay_known_answer():
+    tr, exp, kw = hier_kat()
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], policy=ol.POLICY_EXT_HIER,
+                     region=tr["region"], **kw)
+    assert o["stats"]["status"][0] == 0
+    for k in ("node", "status", "start", "done"):
+        np.testing.assert_array_equal(o[k][0], exp[k], err_msg=k)
+
+
+def test_mobility_model_host_equals_device_formula():
+    """fa.mobility_regions: numpy and torch (CPU) give the same regions; every
+    region is valid and users hand off over time."""
+    import torch
+    import fognetsimpp_amd as fa
+    tr = tg.make_batch(3, 2, 3000, 4000, rho=0.01)
+    a = fa.mobility_regions(tr["arrive"], 3000)
+    b = fa.mobility_regions(torch.from_numpy(tr["arrive"]), 3000).numpy()
+    np.testing.assert_array_equal(a, b)
+    assert a.min() >= 0 and a.max() < 3 and len(np.unique(a)) == 3

@@ -9,7 +9,7 @@ import golden_io
 import oracle_lib as ol
 import tracegen as tg
 from fognetsimpp_amd import _abi
-from test_oracle import c1_trace, check_fifo_invariants
+from test_oracle import c1_trace, check_fifo_invariants, hier_kat
 
 pytestmark = pytest.mark.gpu
 TPS = 10**12
@@ -949,3 +949,51 @@ def test_down_errors(ctx):
     with pytest.raises(fa.FognetError) as ei:
         fa.run_batch(ctx, fa.as_device_trace(dict(tr, p_busy=pb, p_idle=pi), dev))
     assert ei.value.code == _abi.FOGNET_ERR_UNSUPPORTED
+
+
+# ------------------------------------------------------------------ hierarchical brokers + mobility (C5 extension)
+# FOGNET_POLICY_EXT_HIER (not in the reference): parity against the oracle's
+# restatement of the same definition (include/fognet_hip.h).
+
+def test_hier_known_answer_gpu(ctx):
+    tr, exp, kw = hier_kat()
+    dev = torch.device("cuda", ctx.device)
+    out = fa.run_batch(ctx, fa.as_device_trace(tr, dev), policy="EXT_HIER", **kw)
+    torch.cuda.synchronize()
+    assert out.rep_stats()["status"][0] == 0
+    for k, g in (("node", out.node), ("status", out.status), ("start", out.start_tick), ("done", out.done_tick)):
+        np.testing.assert_array_equal(g[0].cpu().numpy(), exp[k], err_msg=k)
+
+
+@pytest.mark.parametrize("kind", ["sweep", "tie_heavy", "down", "light"])
+def test_hier_matches_oracle(ctx, kind):
+    """Hierarchical brokers with mobility handoff (fa.mobility_regions) against the
+    oracle: escalations, same-tick arrivals of escalated tasks, node crashes."""
+    thr, up = 5, 20 * 10**9
+    if kind == "tie_heavy":
+        tr = tie_heavy(17, 3, 2100, 1500)
+        up = 10**11  # the tie-heavy tick base: escalated arrivals collide with completions
+        thr = 1
+    elif kind == "light":
+        tr = tg.make_batch(18, 3, 3000, 3000, rho=0.01, lat_scale=10)
+    else:
+        tr = tg.make_batch(19, 3, 2500, 3000, rho=0.8)
+    tr = dict(tr, region=fa.mobility_regions(tr["arrive"], tr["mips"].shape[-1], users=37))
+    if kind == "down":
+        rng = np.random.default_rng(3)
+        dn = np.full(tr["mips"].shape, np.iinfo(np.int64).max, np.int64)
+        pick = rng.random(dn.shape) < 0.02
+        dn[pick] = (tr["init"].max() + rng.integers(1, 3000, size=dn.shape) * 10**11)[pick]
+        tr["down"] = dn
+    dev = torch.device("cuda", ctx.device)
+    out = fa.run_batch(ctx, fa.as_device_trace(tr, dev), policy="EXT_HIER", hist=True, hier_threshold_s=thr,
+                       hier_up_tick=up)
+    torch.cuda.synchronize()
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8, hist=True,
+                     policy=ol.POLICY_EXT_HIER, region=tr["region"], down=tr.get("down"), hier_threshold_s=thr,
+                     hier_up_tick=up)
+    g = dict(node=out.node.cpu().numpy(), status=out.status.cpu().numpy(), start=out.start_tick.cpu().numpy(),
+             done=out.done_tick.cpu().numpy(), stats=out.rep_stats())
+    assert (g["stats"]["status"] == 0).all()
+    assert_parity(tr, g, o)
+    np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
