@@ -25,9 +25,10 @@ scaling).  Traces are generated on the host before timing.
 
 ``--workload c4`` runs config C4 (Monte Carlo what-if, BASELINE.json
 configs[3]): 1M replications x T = 10,000 x N = 256 in total, sharded over the
-ranks (strong scaling), traces generated on the device INSIDE the timed
-region in blocks of ``--block`` replications (the whole trace would be
-~120 GB), only statistics kept.
+ranks (strong scaling), replayed in blocks of ``--block`` replications by
+fognet_run_generated_dev: each 64-publish chunk of a trace is generated inside
+the replay kernel (the whole trace would be ~120 GB) and only statistics are
+kept (no trace and no per-task output in memory).
 
   python bench.py [--gpus N --steps K --warmup W] [--workload c1|c3|c4|c5]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -270,10 +271,13 @@ def main():
 
 
 def bench_c4(args, ctx, dev, dist, world, rank):
-    """Config C4: R_total replications (sharded over ranks) x T x N; per block
-    of ``args.block`` replications the device generates the traces, replays
-    them and reduces statistics; only the job record, the histograms and the
-    energy survive a block.  Generation is inside the timed region."""
+    """Config C4: R_total replications (sharded over ranks) x T x N, replayed
+    in blocks of ``args.block`` replications by fognet_run_generated_dev: each
+    64-publish chunk of a replication's trace is generated inside the replay
+    kernel, no trace and no per-task output reaches
+    memory; only the per-replication records (reduced to one job record per
+    block), the histograms and the energy survive.  Generation is inside the
+    timed region."""
     from fognetsimpp_amd.dist import shard
     T, N, B = args.T, args.N, args.block
     r0, n = shard(args.R_total, world, rank)
@@ -281,47 +285,23 @@ def bench_c4(args, ctx, dev, dist, world, rank):
     mg_all, sc_all = fa.sweep_params(np.arange(r0, r0 + n), N)
     mg_d = torch.from_numpy(np.ascontiguousarray(mg_all)).to(dev)
     sc_d = torch.from_numpy(np.ascontiguousarray(sc_all)).to(dev)
-    # two trace buffers: block i + 1 is generated on a side stream while block
-    # i replays (generation is HBM-bound, the replay issue/latency-bound)
-    bufs = [fa.allocate_trace(B, T, N, dev) for _ in range(2)]
-    pb, pi = fa.power_model(1000 * (1 + np.arange(N) % 4))  # the generator's MIPS pattern
-    for bf in bufs:
-        bf["p_busy"] = torch.from_numpy(np.tile(pb, (B, 1))).to(dev)  # same [R][N] layout as mips
-        bf["p_idle"] = torch.from_numpy(np.tile(pi, (B, 1))).to(dev)
-    out = fa.allocate_outputs(B, T, dev, N=N, energy=False, hist=True)
+    pb, pi = fa.power_model(1000 * (1 + np.arange(N) % 4))  # the generator's MIPS pattern, shared by all
+    power = (torch.from_numpy(pb).to(dev), torch.from_numpy(pi).to(dev))
+    out = fa.allocate_outputs(B, T, dev, N=N, energy=False, hist=True, per_task=False)
     jrec = torch.zeros((max(1, len(blocks)), _abi.JOB_STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
     stream = fa.engine._stream_ptr(dev)
-    main = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(dev)
-    generated = [torch.cuda.Event() for _ in range(2)]
-    consumed = [torch.cuda.Event() for _ in range(2)]
-    log(f"[rank {rank}] c4: {n} replications in {len(blocks)} blocks of <= {B}, T={T} N={N}")
-
-    def generate(i):
-        b0, nb = blocks[i]
-        bf = bufs[i % 2]
-        with torch.cuda.stream(side):
-            side.wait_event(consumed[i % 2])  # block i - 2's replay has read this buffer
-            fa.generate_trace(ctx, args.seed, nb, T, N, mg_d[b0 - r0: b0 - r0 + nb], sc_d[b0 - r0: b0 - r0 + nb],
-                              r0=b0, out=bf)
-            generated[i % 2].record(side)
+    log(f"[rank {rank}] c4: {n} replications in {len(blocks)} blocks of <= {B}, T={T} N={N} (generated in-kernel)")
 
     def step(evs=None):
         out.hist.zero_()
-        generate(0)
         for i, (b0, nb) in enumerate(blocks):
-            if i + 1 < len(blocks):
-                generate(i + 1)
-            tr = {k: v[:nb] for k, v in bufs[i % 2].items() if not k.startswith("_")}
-            o = fa.BatchResult(out.node[:nb], out.status[:nb], out.start_tick[:nb], out.done_tick[:nb],
-                               out.stats[: nb * _abi.REP_STATS_DTYPE.itemsize], None, out.hist)
-            main.wait_event(generated[i % 2])
+            o = fa.BatchResult(None, None, None, None, out.stats[: nb * _abi.REP_STATS_DTYPE.itemsize], None, out.hist)
             if evs is not None:
                 evs[i][0].record()
-            fa.run_batch(ctx, tr, o, ring_capacity=args.ring, stage="all", policy=args.policy)
+            fa.run_generated(ctx, args.seed, nb, T, N, mg_d[b0 - r0: b0 - r0 + nb], sc_d[b0 - r0: b0 - r0 + nb],
+                             r0=b0, out=o, ring_capacity=args.ring, policy=args.policy, power=power)
             if evs is not None:
                 evs[i][1].record()
-            consumed[i % 2].record(main)
             ctx.check(ctx._lib.fognet_reduce_stats_dev(ctx.handle, fa.engine._ptr(o.stats), nb,
                                                        fa.engine._ptr(jrec[i]), stream), "reduce")
         job = fa.merge_job_stats(list(jrec.cpu().numpy().view(_abi.JOB_STATS_DTYPE).reshape(-1)[:len(blocks)]))
@@ -356,30 +336,45 @@ def bench_c4(args, ctx, dev, dist, world, rank):
     summary = fa.summarize(job)
     hist = out.hist.cpu().numpy()
     decisions = args.R_total * T * args.steps
-    bpd = algorithmic_bytes_per_decision(T, N)
-    achieved_gbs = n * T * bpd / (replay_ms / 1e3) / 1e9
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        nb = blocks[0][1]
-        tr = {k: v[:nb] for k, v in bufs[0].items() if k not in ("p_busy", "p_idle", "_keep")}
-        fa.generate_trace(ctx, args.seed, nb, T, N, mg_d[:nb], sc_d[:nb], r0=r0, out=tr)
+        # the CPU baseline replays the first block's first replications from the materialised trace; its
+        # records must equal the generated replay's (parity)
+        nb = min(args.cpu_reps, blocks[0][1])
+        tr = fa.generate_trace(ctx, args.seed, nb, T, N, mg_d[:nb], sc_d[:nb], r0=r0)
+        tr = {k: v for k, v in tr.items() if not k.startswith("_")}
+        tr["p_busy"], tr["p_idle"] = (x.expand(nb, N) for x in power)
+        o = fa.run_generated(ctx, args.seed, nb, T, N, mg_d[:nb], sc_d[:nb], r0=r0, ring_capacity=args.ring,
+                             policy=args.policy, power=power, hist=False)
         torch.cuda.synchronize()
-        cpu = cpu_baseline(tr, args, nb, T, N)
+        cpu = cpu_baseline(tr, args, nb, T, N, out=o)
+    # VALU utilisation (C4 has no per-task HBM traffic, so no HBM roofline) from the PMC pass
+    # committed under profiles/ when it exists for this configuration
+    valu = None
+    prof = os.path.join(ROOT, "profiles", "pmc_valu_c4.json")
+    if os.path.exists(prof):
+        with open(prof) as f:
+            pj = json.load(f)
+        if pj.get("config") == {"T": T, "N": N, "block": B, "ring": args.ring, "policy": args.policy}:
+            valu = pj.get("valu_busy")
     if rank == 0:
         line = {
             "metric": METRIC, "value": decisions / elapsed, "unit": "decisions/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int64",
-            "data": "synthetic (Philox traces generated on the device inside the timed region, C4 recipe)",
+            "data": "synthetic (Philox traces generated inside the replay kernel, C4 recipe)",
             "config": {"workload": "C4 Monte Carlo what-if (BASELINE.json configs[3])", "R_total": args.R_total,
                        "T": T, "N": N, "block": B, "ring_capacity": args.ring, "policy": args.policy,
                        "parallelism": f"replications sharded over {world} GPU(s); RCCL all-reduce of histograms"
                                       f" + energy, all-gather of the job record"},
-            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "replay_kernel (statistics pass fused)",
-                         "kernel_ms_per_step": replay_ms, "bytes_per_decision": bpd,
-                         "note": "per-task outputs go to a reused block scratch buffer"},
+            "roofline": {"bound": "valu", "achieved": valu, "peak": 1.0, "unit": "VALU busy fraction",
+                         "frac": valu, "traffic": None,
+                         "kernel": "replay_gen_kernel (trace generated per 64-publish chunk, statistics in "
+                                   "registers, no per-task stores)",
+                         "kernel_ms_per_step": replay_ms,
+                         "note": "SURVEY.md §8(d): C4 has no per-task HBM traffic, so VALU utilisation "
+                                 "(PMC: SQ_ACTIVE_INST_VALU*4/SIMDs/GRBM_GUI_ACTIVE per XCD, "
+                                 "profiles/pmc_valu_c4.json) replaces the HBM fraction"},
             "cpu_baseline": cpu,
             "failed_replications": summary["failed"],
             "stats": {"decisions": summary["decisions"], "queueTime_ms_mean": summary["queueTime_ms"].get("mean"),
@@ -527,7 +522,9 @@ def cpu_baseline(trace, args, R, T, N, out=None):
     dt = time.perf_counter() - t0
     ok = int((o["stats"]["status"] == 0).sum())
     parity = None
-    if out is not None:
+    if out is not None and out.node is None:  # statistics-only device run: the records
+        parity = o["stats"].tobytes() == out.stats[: reps * _abi.REP_STATS_DTYPE.itemsize].cpu().numpy().tobytes()
+    elif out is not None:
         parity = bool(np.array_equal(o["node"], out.node[:reps].cpu().numpy())
                       and np.array_equal(o["status"], out.status[:reps].cpu().numpy())
                       and np.array_equal(o["start"], out.start_tick[:reps].cpu().numpy())

@@ -32,7 +32,7 @@ HIER_REGION_NODES = 1024
 TICKS_PER_SECOND = 10**12
 # fognet_v2_action (BrokerBaseApp2 decision outcome)
 V2_LOCAL, V2_FORWARD, V2_DROPPED, V2_NO_NODES = 3, 4, 5, 6
-ABI_VERSION = 8
+ABI_VERSION = 9
 HIST_METRICS = 2  # 0 queueTime, 1 response
 HIST_BINS = 64
 COMM_ID_BYTES = 128  # FOGNET_COMM_ID_BYTES
@@ -194,6 +194,8 @@ SIGNATURES = {
     "fognet_job_stats_add_rep": (None, [C.POINTER(JobStats), C.POINTER(RepStats)]),
     "fognet_gen_trace_dev": (C.c_int, [P, C.POINTER(GenParams), C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                        P, P, P, P, P, P, P]),
+    "fognet_run_generated_dev": (C.c_int, [P, C.POINTER(GenParams), C.c_int64, C.POINTER(BatchIn),
+                                           C.POINTER(BatchOut), P]),
     "fognet_sync": (C.c_int, [P]),
     "fognet_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "fognet_comm_create": (C.c_int, [P, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.POINTER(P)]),

@@ -87,7 +87,8 @@ int set_device(fognet_ctx* c) {
 }
 
 // Validates a batch descriptor; fills the kernel argument block except pointers to outputs.
-int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
+// generated: fognet_run_generated_dev (no trace or node-parameter arrays)
+int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a, bool generated = false) {
   if (!in) return fail(c, FOGNET_ERR_ARG, "null batch");
   if (in->R < 0 || in->T < 0 || in->N < 0) return fail(c, FOGNET_ERR_ARG, "negative R/T/N");
   if (in->N == 0) return fail(c, FOGNET_ERR_NO_NODES, "N == 0 (BrokerBaseApp3.cc:268 reads brokers[0])");
@@ -110,9 +111,9 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a) {
   if (q < 2 || (q & (q - 1)) != 0 || q > (1 << 15)) return fail(c, FOGNET_ERR_ARG, "ring_capacity must be a power of two in [2, 2^15]");
   int qlog = 0;
   while ((1 << qlog) < q) ++qlog;
-  if (in->R > 0 && in->T > 0 && (!in->arrive_tick || !in->req_mips))
+  if (!generated && in->R > 0 && in->T > 0 && (!in->arrive_tick || !in->req_mips))
     return fail(c, FOGNET_ERR_ARG, "null trace arrays");
-  if (in->R > 0 && (!in->mips || !in->dl_tick || !in->ul_tick || !in->init_adv_tick))
+  if (!generated && in->R > 0 && (!in->mips || !in->dl_tick || !in->ul_tick || !in->init_adv_tick))
     return fail(c, FOGNET_ERR_ARG, "null node parameter arrays");
   memset(a, 0, sizeof *a);
   a->R = in->R;
@@ -429,6 +430,64 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     if (e != hipSuccess) return hip_fail(c, e, "stats launch");
   }
   return FOGNET_OK;
+}
+
+int fognet_run_generated_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t r0, const fognet_batch_in* in,
+                             fognet_batch_out* out, void* stream) {
+  if (!c || !p || !in || !out) return FOGNET_ERR_ARG;
+  if (in->arrive_tick || in->req_mips || in->mips || in->dl_tick || in->ul_tick || in->init_adv_tick || in->down_tick ||
+      in->region)
+    return fail(c, FOGNET_ERR_ARG, "generated replay: the trace and node-parameter arrays must be NULL (generated)");
+  if (in->policy != FOGNET_POLICY_REF_V3 && in->policy != FOGNET_POLICY_EXT_LAT)
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "generated replay: policy REF_V3 or EXT_LAT");
+  if (out->node || out->status || out->start_tick || out->done_tick)
+    return fail(c, FOGNET_ERR_ARG, "generated replay: statistics only (per-task arrays must be NULL)");
+  if (!out->stats) return fail(c, FOGNET_ERR_ARG, "stats output is required (per-replication status)");
+  if (r0 < 0 || p->req_lo < 0 || p->req_hi < p->req_lo) return fail(c, FOGNET_ERR_ARG, "bad r0 or req range");
+  if (in->R > 0 && (!p->mean_gap_ticks || !p->lat_scale)) return fail(c, FOGNET_ERR_ARG, "null generator parameters");
+  // per-node totals come from the node tails' 32-bit cumulative service (MIPS >= 1000)
+  if (in->T > 0 && (uint64_t)in->T * (uint64_t)(p->req_hi / 1000) >= (1ull << 32))
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "generated replay: T * req_hi / 1000 must stay below 2^32");
+  fognet::ReplayArgs a;
+  int rc = prepare(c, in, &a, true);
+  if (rc) return rc;
+  if (a.R == 0) return FOGNET_OK;
+  rc = set_device(c);
+  if (rc) return rc;
+  a.gen_on = 1;
+  a.gen_r0 = r0;
+  a.gen = *p;
+  a.no_task_out = 1;
+  a.out_stats = out->stats;
+  a.out_energy = out->node_energy_j;
+  a.hist = out->hist;
+  if (a.out_energy && !a.p_busy) return fail(c, FOGNET_ERR_ARG, "node_energy_j needs the power model (p_busy_w/p_idle_w)");
+  hipError_t e;
+  if (use_wide(a.N)) {
+    const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N, true);
+    rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ws, "wide replay workspace");
+    if (rc) return rc;
+    e = fognet::launch_replay_wide(a, c->ring, a.R, (hipStream_t)stream);
+    return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "wide replay launch");
+  }
+  // workspace: [hand-over counter | list [R] | rings, reused by the wide hand-over]
+  const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
+  const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
+  const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N, true);
+  const size_t head = align256(256 + (size_t)a.R * sizeof(int32_t));
+  rc = ensure(c, (void**)&c->ring, &c->ring_bytes, head + (ring_bytes > fb_bytes ? ring_bytes : fb_bytes),
+              "ring workspace");
+  if (rc) return rc;
+  unsigned char* const base = reinterpret_cast<unsigned char*>(c->ring);
+  a.wide_count = reinterpret_cast<int32_t*>(base);
+  a.wide_list = reinterpret_cast<int32_t*>(base + 256);
+  a.ring = reinterpret_cast<fognet::RingEntry*>(base + head);
+  e = hipMemsetAsync(a.wide_count, 0, sizeof(int32_t), (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "hand-over counter");
+  e = fognet::launch_replay(a, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "replay launch");
+  e = fognet::launch_replay_wide(a, base + head, slots, (hipStream_t)stream);
+  return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "wide hand-over launch");
 }
 
 int fognet_replay_dev(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out, void* stream) {

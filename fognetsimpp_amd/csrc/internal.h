@@ -141,6 +141,52 @@ __device__ __forceinline__ double neg_log_unit(double u) {
   return -ln_u;
 }
 
+// ---------------------------------------------------------------- trace recipe
+// The synthetic trace of one replication (tracegen.hip documents the recipe;
+// tests/tracegen.py restates it on the host).  gen_kernel writes it to HBM;
+// the replay kernels' generated mode (fognet_run_generated_dev) computes the
+// same values 64 publishes at a time and never stores the trace.
+struct GenRep {
+  uint32_t k0, k1;  // Philox key (seed, global replication index)
+  int32_t req_lo;
+  uint32_t pad;
+  uint64_t rspan;   // req_hi - req_lo + 1
+  double mean;      // mean inter-arrival gap (ticks)
+  int64_t scale;    // latency multiplier
+};
+
+// rl: local index into the per-replication parameter arrays
+__device__ __forceinline__ GenRep gen_rep(const fognet_gen_params& p, int64_t r_global, int64_t rl) {
+  GenRep g;
+  g.k0 = p.seed;
+  g.k1 = (uint32_t)r_global;
+  g.req_lo = p.req_lo;
+  g.pad = 0u;
+  g.rspan = (uint64_t)(p.req_hi - p.req_lo) + 1ull;
+  g.mean = p.mean_gap_ticks[rl];
+  g.scale = p.lat_scale[rl];
+  return g;
+}
+
+// node j: MIPS, downlink and uplink latency (its first advert arrives at init = ul)
+__device__ __forceinline__ void gen_node(const GenRep& g, int j, int32_t& m, int64_t& d, int64_t& u) {
+  const uint64_t span = 1000000000ull - 1000000ull + 1ull;
+  const U4 x = philox4x32_10(U4{(uint32_t)j, 1u, 0u, 0u}, g.k0, g.k1);
+  d = (int64_t)(1000000ull + (uint64_t)x.x % span) * g.scale;
+  u = (int64_t)(1000000ull + (uint64_t)x.y % span) * g.scale;
+  m = 1000 * (1 + j % 4);
+}
+
+// task i: requirement and the gap before it (arrive[i] = arrive[i-1] + gap,
+// arrive[-1] = max_j ul_j + 1)
+__device__ __forceinline__ void gen_task(const GenRep& g, int i, int64_t& gap, int32_t& rq) {
+  const U4 x = philox4x32_10(U4{(uint32_t)i, 0u, 0u, 0u}, g.k0, g.k1);
+  rq = (int32_t)((uint64_t)g.req_lo + (uint64_t)x.x % g.rspan);
+  const uint64_t k53 = ((uint64_t)x.y << 21) | ((uint64_t)x.z >> 11);
+  const double u = (double)(k53 + 1ull) * 0x1p-53;
+  gap = (int64_t)(g.mean * neg_log_unit(u));
+}
+
 // ---------------------------------------------------------------- replay
 
 // Pending-task ring entry: one per task assigned to a node, kept until the
@@ -191,6 +237,13 @@ struct ReplayArgs {
   const int32_t* region;
   int64_t hier_up;
   int32_t hier_thr;
+  // Generated mode (fognet_run_generated_dev): gen_on != 0 ->
+  // replication r's trace and node parameters are the gen_kernel recipe's for
+  // global index gen_r0 + r, computed in the kernel (arrive/req/mips/dl/ul/init
+  // unused), and only statistics are written (no per-task outputs).
+  int32_t gen_on;
+  int64_t gen_r0;
+  fognet_gen_params gen;
 };
 
 // Internal per-replication status between the two replay kernels (never
@@ -242,7 +295,8 @@ constexpr int kWideGroupSlots = 16;
 constexpr int kWideMaxNodes = 65536;  // LDS: 82 KiB of group minima
 size_t replay_wide_lds_bytes(int32_t N);
 // workspace: R*T WideEntry followed by R*N WideNode
-size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N);
+// (+ R*N generated node parameters in generated mode)
+size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen = false);
 // slots: workspace slots (workgroups).  With a.wide_list unset, slots == R and
 // workgroup r replays replication r; with it set, the workgroups take the
 // listed replications in turn (slots <= R bounds the workspace).

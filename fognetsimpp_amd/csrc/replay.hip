@@ -104,6 +104,11 @@ __device__ __forceinline__ int64_t nh_a(u32x4 v) { return (int64_t)(((uint64_t)v
 constexpr uint32_t kPrefetchOps = 8;
 constexpr int kNhBase = 112;  // v112..v127: 4 slots x {a lo, a hi, C, S}
 static_assert(kNhBase + 4 * kMaxNodesPerLane == 128, "4 waves/SIMD: 128 VGPRs per lane");
+// Generated mode (replay_gen_kernel) keeps the statistics accumulators in
+// registers through the loop: 3 waves/SIMD, allocation capped at 152, the
+// prefetch registers are v152..v167 (register set 1: slot functions 4..7).
+constexpr int kNhBaseGen = 152;
+static_assert(kNhBaseGen + 4 * kMaxNodesPerLane == 168, "3 waves/SIMD: 168 VGPRs per lane");
 
 #define FOGNET_NH_SLOT(S, R0, R1, R2, R3, RR)                                                  \
   __device__ __forceinline__ void nh_prefetch_##S(const RingEntry* p) {                       \
@@ -180,15 +185,24 @@ FOGNET_NH_SLOT(0, "v112", "v113", "v114", "v115", "v[112:115]")
 FOGNET_NH_SLOT(1, "v116", "v117", "v118", "v119", "v[116:119]")
 FOGNET_NH_SLOT(2, "v120", "v121", "v122", "v123", "v[120:123]")
 FOGNET_NH_SLOT(3, "v124", "v125", "v126", "v127", "v[124:127]")
+FOGNET_NH_SLOT(4, "v152", "v153", "v154", "v155", "v[152:155]")
+FOGNET_NH_SLOT(5, "v156", "v157", "v158", "v159", "v[156:159]")
+FOGNET_NH_SLOT(6, "v160", "v161", "v162", "v163", "v[160:163]")
+FOGNET_NH_SLOT(7, "v164", "v165", "v166", "v167", "v[164:167]")
 #undef FOGNET_NH_SLOT
 static_assert(kPrefetchOps == 8, "nh_read waits at most for vmcnt(8)");
 
+// S: slot + 4 * register set
 template <int S>
 __device__ __forceinline__ void nh_prefetch(const RingEntry* p) {
   if constexpr (S == 0) nh_prefetch_0(p);
   else if constexpr (S == 1) nh_prefetch_1(p);
   else if constexpr (S == 2) nh_prefetch_2(p);
-  else nh_prefetch_3(p);
+  else if constexpr (S == 3) nh_prefetch_3(p);
+  else if constexpr (S == 4) nh_prefetch_4(p);
+  else if constexpr (S == 5) nh_prefetch_5(p);
+  else if constexpr (S == 6) nh_prefetch_6(p);
+  else nh_prefetch_7(p);
 }
 
 // Prefetch stamps are kept per slot, not per node: byte s of the wave-uniform
@@ -206,27 +220,42 @@ __device__ __forceinline__ uint64_t lanes_ge(uint32_t x, uint32_t c) {
   return __builtin_amdgcn_uicmp(x, c, 35 /* ICMP_UGE */);
 }
 
-// Wave-level read of slot S's head+1 entry (`need`: wave-uniform, some lane uses it).
-template <int S>
+// Wave-level read of slot S's head+1 entry (`need`: wave-uniform, some lane
+// uses it) from register set SET (0: v112.., 4: v152..).
+template <int S, int SET>
 __device__ __forceinline__ u32x4 read_nh(bool need, uint32_t pf, uint32_t ops) {
   const uint32_t m = need ? ((ops - (pf >> (8 * S))) & 0xFFu) : 0xFFu;
-  if constexpr (S == 0) return nh_read_0(m);
-  else if constexpr (S == 1) return nh_read_1(m);
-  else if constexpr (S == 2) return nh_read_2(m);
-  else return nh_read_3(m);
+  if constexpr (S + SET == 0) return nh_read_0(m);
+  else if constexpr (S + SET == 1) return nh_read_1(m);
+  else if constexpr (S + SET == 2) return nh_read_2(m);
+  else if constexpr (S + SET == 3) return nh_read_3(m);
+  else if constexpr (S + SET == 4) return nh_read_4(m);
+  else if constexpr (S + SET == 5) return nh_read_5(m);
+  else if constexpr (S + SET == 6) return nh_read_6(m);
+  else return nh_read_7(m);
 }
 
 // Reload the head+1 entry of node (slot s, lane): one cache line.  Ring
 // stores issued earlier by this wave (any lane) precede it in the same
 // in-order memory pipeline, so it observes them.
+template <int SET>
 __device__ __forceinline__ void refill_nh(int s, const Slot& st, const RingEntry* ring, uint32_t qmask, int lane) {
   const RingEntry* p = ring + ((n_head(st) + 1u) & qmask);
   const uint64_t only = 1ull << __builtin_amdgcn_readfirstlane(lane);  // lane is wave-uniform
-  switch (__builtin_amdgcn_readfirstlane(s)) {
-    case 0: nh_refill_0(p, only); break;
-    case 1: nh_refill_1(p, only); break;
-    case 2: nh_refill_2(p, only); break;
-    default: nh_refill_3(p, only); break;
+  if constexpr (SET == 0) {
+    switch (__builtin_amdgcn_readfirstlane(s)) {
+      case 0: nh_refill_0(p, only); break;
+      case 1: nh_refill_1(p, only); break;
+      case 2: nh_refill_2(p, only); break;
+      default: nh_refill_3(p, only); break;
+    }
+  } else {
+    switch (__builtin_amdgcn_readfirstlane(s)) {
+      case 0: nh_refill_4(p, only); break;
+      case 1: nh_refill_5(p, only); break;
+      case 2: nh_refill_6(p, only); break;
+      default: nh_refill_7(p, only); break;
+    }
   }
 }
 
@@ -342,7 +371,7 @@ __device__ __forceinline__ uint32_t c_arrived(const Slot& st, const u32x4 nhw, i
 // Apply the advert of the head completion of node k (lane-local): the broker
 // view takes busyTime after releaseResource (:232, :254), the head advances
 // and entry head+2 is prefetched.  nhw: st.nh read after its wait.
-template <int SL>
+template <int SL, int SET>
 __device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, int64_t dl, int64_t ul, uint32_t tl_C,
                                              const RingEntry* ring, uint32_t qmask, uint32_t ops, uint32_t& scan) {
   const int64_t hd_done = st.nxt - ul;
@@ -361,7 +390,7 @@ __device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, i
   st.hd_S = nhw.w;
   st.nxt = done + ul;
   if (pend >= 2u) {  // the ring holds every pending entry, the tail included
-    nh_prefetch<SL>(ring + ((n_head(st) + 1u) & qmask));  // the caller stamps slot SL
+    nh_prefetch<SL + SET>(ring + ((n_head(st) + 1u) & qmask));  // the caller stamps slot SL
   }
 }
 
@@ -561,13 +590,14 @@ __device__ __forceinline__ void stats_finish(const ReplayArgs& A, int r, int64_t
   }
 }
 
-template <int NPL, int POL>
-// 4 waves per SIMD (<= 128 VGPRs) and <= 10 KiB of LDS (160 KiB / 16): 16
-// replications resident per CU, so the 4096-replication sweep runs in a single
-// wave of workgroups on 256 CUs.  (11 KiB of LDS admits only 14 per CU, and
-// the last 512 replications then run as a second, mostly idle round.)
-__global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))) void replay_kernel(ReplayArgs A) {
+// The replay of replication blockIdx.x (replay_kernel, replay_gen_kernel).
+// GEN: generated mode (ReplayArgs::gen_on): the trace chunks and node
+// parameters are computed here, the statistics are accumulated as the runs
+// are pushed (registers), and nothing is stored per task.
+template <int NPL, int POL, bool GEN>
+__device__ __forceinline__ void replay_body(const ReplayArgs& A) {
   constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
+  constexpr int kSet = GEN ? 4 : 0;  // prefetch register set
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
   __shared__ int64_t s_dl[NPL * kWave];
@@ -583,10 +613,16 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)T;
   const uint32_t qmask = (1u << A.q_log2) - 1u;
-  const int64_t arrive0 = T > 0 ? A.arrive[tbase] : kNever;
+  GenRep g{};
+  if constexpr (GEN) g = gen_rep(A.gen, A.gen_r0 + r, r);
+  // (generated: every first advert precedes the first publish by construction)
+  const int64_t arrive0 = GEN ? kNever : (T > 0 ? A.arrive[tbase] : kNever);
   const uint32_t lds_ch = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)s_ch;
   uint32_t ch_stamp = 0u;  // `ops` after the staged chunk's copies were issued
-  if (T > 0) chunk_dma(A.arrive + tbase, A.req + tbase, (uint32_t)min(lane, min(kWave, T) - 1), lds_ch);
+  if constexpr (!GEN) {
+    if (T > 0) chunk_dma(A.arrive + tbase, A.req + tbase, (uint32_t)min(lane, min(kWave, T) - 1), lds_ch);
+  }
+  uint64_t ul_max = 0u;  // generated: the largest ul (the first publish follows it)
 
   // ---- node parameters + preconditions (fognet_hip.h, fognet_batch_in)
   bool bad = false;
@@ -597,10 +633,17 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     int64_t d = 0, u = 0;
     int32_t m = 1;
     if (k < N) {
-      m = A.mips[nbase + k];
-      d = A.dl[nbase + k];
-      u = A.ul[nbase + k];
-      const int64_t ia = A.init[nbase + k];
+      int64_t ia;
+      if constexpr (GEN) {
+        gen_node(g, k, m, d, u);
+        ia = u;
+        ul_max = (uint64_t)u > ul_max ? (uint64_t)u : ul_max;
+      } else {
+        m = A.mips[nbase + k];
+        d = A.dl[nbase + k];
+        u = A.ul[nbase + k];
+        ia = A.init[nbase + k];
+      }
       bad |= (m <= 0) | (d < 0) | (u < 0) | (d > kMaxTick) | (u > kMaxTick) | (ia < u) | (ia >= arrive0);
       if constexpr (kExt) bad |= d >= kExtMaxDl;
     }
@@ -620,7 +663,13 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     s_tlS[k] = 0u;
     st[s].cnt = 0u;
   }
+  // generated: the histogram rows live in the (unused) chunk stage
+  if (GEN && A.hist)
+    for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) s_ch[h] = 0u;
   __syncthreads();
+  int64_t gen_carry = 0;
+  if constexpr (GEN) gen_carry = (int64_t)~wave_min_u64(~ul_max) + 1;
+  Acc gacc = acc_identity();  // generated: this lane's tasks (lane l: tasks l, l + 64, ...)
 
   uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
   if (N <= 0) err = FOGNET_ERR_NO_NODES;
@@ -644,7 +693,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
   bool dirty = false;
   int64_t prev_t = INT64_MIN;
   uint32_t max_pend = 0u;
-  uint32_t ops = T > 0 ? kChunkOps : 0u;  // tally of issued vector-memory instructions (see kPrefetchOps)
+  uint32_t ops = (!GEN && T > 0) ? kChunkOps : 0u;  // tally of issued vector-memory instructions (see kPrefetchOps)
   uint32_t pf = 0u;                       // per-slot stamps of the youngest head+1 loads (set_stamp)
   ch_stamp = ops;
   int64_t n_done = 0;
@@ -669,10 +718,16 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
     const bool live = lane < cnt;
-    wait_vm((ops - ch_stamp) & 0xFFu);  // the staged chunk has landed in LDS
-    const uint32_t l_ch = lane_now();
-    const int64_t ca = live ? (int64_t)(((uint64_t)s_ch[kWave + l_ch] << 32) | s_ch[l_ch]) : kNever;
-    const int32_t cr = live ? (int32_t)s_ch[2 * kWave + l_ch] : 0;
+    int64_t ca;
+    int32_t cr;
+    if constexpr (GEN) {
+      gen_chunk(g, c0, T, lane, gen_carry, ca, cr);
+    } else {
+      wait_vm((ops - ch_stamp) & 0xFFu);  // the staged chunk has landed in LDS
+      const uint32_t l_ch = lane_now();
+      ca = live ? (int64_t)(((uint64_t)s_ch[kWave + l_ch] << 32) | s_ch[l_ch]) : kNever;
+      cr = live ? (int32_t)s_ch[2 * kWave + l_ch] : 0;
+    }
     PROF(p_chunks++;)
     TMARK(0)
     // trace preconditions: nondecreasing ticks, requirement >= 0, ticks < 2^61
@@ -683,7 +738,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
     }
     prev_t = readlane_i64(ca, cnt - 1);
     const int64_t t_last = prev_t;  // only picks which horizons are evaluated exactly
-    if (c0 + kWave < T) {  // stage the next chunk (ca/cr were consumed above: LDS reads are done)
+    if (!GEN && c0 + kWave < T) {  // stage the next chunk (ca/cr were consumed above: LDS reads are done)
       const int cn = min(kWave, T - c0 - kWave);
       chunk_dma(A.arrive + tbase + c0 + kWave, A.req + tbase + c0 + kWave, (uint32_t)min(lane, cn - 1), lds_ch);
       ops += kChunkOps;
@@ -715,7 +770,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
             dirty = true;
             PROF(p_advit++; p_adv += __popcll(ballot(due)); p_rd++; p_w0 += young(s, due && pending(st[s]) >= 2u);)
             TMARK(1)
-            const u32x4 nhw = read_nh<s>((dm & lanes_ge(pd, 2u)) != 0, pf, ops);
+            const u32x4 nhw = read_nh<s, kSet>((dm & lanes_ge(pd, 2u)) != 0, pf, ops);
             TMARK(8)
             // apply_advert prefetches head+2 where >= 3 are pending: tally it
             // first, so the stamp already counts the load itself
@@ -725,7 +780,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
             }
             if (due) {
               const int k = s * kWave + lane;
-              apply_advert<s>(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops, scan);
+              apply_advert<s, kSet>(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops, scan);
             }
           });
           if (!any) break;
@@ -768,7 +823,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
           if (dm) {
             PROF(p_hz++; p_rd++; p_w0 += young(s, deep && pending(st[s]) >= 2u);)
             TMARK(3)
-            const u32x4 nhw = read_nh<s>((dm & lanes_ge(pd, 2u)) != 0, pf, ops);
+            const u32x4 nhw = read_nh<s, kSet>((dm & lanes_ge(pd, 2u)) != 0, pf, ops);
             TMARK(9)
             if (deep) {
               const int64_t h = horizon(st[s], nhw, j, best, s_tlC[j], s_dl[j], s_ul[j], ring_s(s), qmask, scan);
@@ -891,16 +946,32 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
         e.C = tlC_k + Cs;
         e.S = S;
         ring_k[((cnt_k & 0xFFFFu) + (uint32_t)(lane - jp)) & qmask] = e;
-        // chunk bases are wave-uniform (SGPR) and the lane index a 32-bit
-        // offset, so no per-lane 64-bit addresses stay live across the chunk
-        const size_t o = tbase + (size_t)c0;
-        const uint32_t l = lane_now();
-        (A.out_node + o)[l] = k;
-        (A.out_status + o)[l] = (uint8_t)status;
-        (A.out_start + o)[l] = start;
-        (A.out_done + o)[l] = done;
+        if constexpr (GEN) {
+          // the task's statistics (the fused epilogue's, rep_stats_kernel's)
+          const int64_t resp = done - ca;
+          add_moment(gacc.rs_lo, gacc.rs_hi, gacc.rq_lo, gacc.rq_hi, (uint64_t)resp);
+          gacc.rmin = min(gacc.rmin, resp);
+          gacc.rmax = max(gacc.rmax, resp);
+          if (A.hist) atomicAdd(&s_ch[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
+          if (status == 4u) {
+            gacc.n4 += 1u;
+            acc_qtime(gacc.qs_lo, gacc.qs_hi, gacc.qq_lo, gacc.qq_hi, gacc.qq_top, gacc.qmin, gacc.qmax, gacc.nqt,
+                      gacc.nqo, start, a, A.hist ? s_ch : nullptr);
+          } else {
+            gacc.n5 += 1u;
+          }
+        } else {
+          // chunk bases are wave-uniform (SGPR) and the lane index a 32-bit
+          // offset, so no per-lane 64-bit addresses stay live across the chunk
+          const size_t o = tbase + (size_t)c0;
+          const uint32_t l = lane_now();
+          (A.out_node + o)[l] = k;
+          (A.out_status + o)[l] = (uint8_t)status;
+          (A.out_start + o)[l] = start;
+          (A.out_done + o)[l] = done;
+        }
       }
-      ops += 5u;
+      ops += GEN ? 1u : 5u;  // the ring store (+ the four output stores)
       TMARK(5)
 
       // 6) node k's state after the run
@@ -926,7 +997,7 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
           }
           // k's head+1 changed: reload it (uniform control flow, one lane)
           if ((pend_k == 0u && L >= 2) || pend_k == 1u) {
-            refill_nh(s, st[s], ring_s(s), qmask, kl);
+            refill_nh<kSet>(s, st[s], ring_s(s), qmask, kl);
             PROF(p_refill++;)
             ops += 1u;
             pf = set_stamp(pf, s, ops);  // the stamp counts the refill itself
@@ -996,7 +1067,27 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
 #endif
   }
 #if !defined(FOGNET_REPLAY_PROFILE) || FOGNET_REPLAY_PROFILE == 0
-  if (A.fuse_stats && A.out_stats && err != kNeedsWide) {
+  if constexpr (GEN) {
+    if (A.out_stats && err != kNeedsWide) {
+      // busy seconds, per-node service (energy) and `last` from the node
+      // tails (exact: the host admits T * max service < 2^32), the rest from
+      // the loop's accumulators
+      unsigned long long* e_busy = reinterpret_cast<unsigned long long*>(s_tld);  // [NPL*64] u64
+      double* e_e = reinterpret_cast<double*>(s_ul);                              // [NPL*64] f64
+      for (int j = lane; j < NPL * kWave; j += kWave) {
+        const uint32_t B = s_tlC[j];
+        const int64_t ld = s_tld[j];
+        gacc.busy += B;
+        gacc.last = max(gacc.last, ld);
+        if (A.p_busy) e_busy[j] = B;  // aliases s_tld[j]: read above by this lane
+      }
+      gacc = wave_merge(gacc);
+      __syncthreads();
+      fognet_rep_stats* S = A.out_stats + r;
+      if (lane == 0) write_rep_stats(S, gacc);
+      stats_finish(A, r, n_done > 0 ? gacc.last : 0, S, e_busy, e_e, s_ch, lane, kWave);
+    }
+  } else if (A.fuse_stats && A.out_stats && err != kNeedsWide) {
     // ---- statistics epilogue (rep_stats_kernel's pass, fused).  The wave
     // re-reads its own replication's outputs; task c0 + l was stored by lane
     // l, and lane l reads tasks l, l + 64, ... (its own stores).  The loop's
@@ -1039,6 +1130,23 @@ __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))
 #endif
 }
 
+// 4 waves per SIMD (<= 128 VGPRs) and <= 10 KiB of LDS (160 KiB / 16): 16
+// replications resident per CU, so the 4096-replication sweep runs in a single
+// wave of workgroups on 256 CUs.  (11 KiB of LDS admits only 14 per CU, and
+// the last 512 replications then run as a second, mostly idle round.)
+template <int NPL, int POL>
+__global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))) void replay_kernel(ReplayArgs A) {
+  replay_body<NPL, POL, false>(A);
+}
+
+// Generated mode: 3 waves per SIMD (168 VGPRs: the statistics accumulators stay
+// in registers through the loop), prefetch registers v152..v167.
+template <int NPL, int POL>
+__global__ __launch_bounds__(64, 3) __attribute__((amdgpu_num_vgpr(kNhBaseGen / 2))) void replay_gen_kernel(
+    ReplayArgs A) {
+  replay_body<NPL, POL, true>(A);
+}
+
 constexpr int kStatThreads = 256;
 
 // Standalone statistics pass over the replay outputs (fognet_rep_stats_dev);
@@ -1074,6 +1182,15 @@ __global__ __launch_bounds__(kStatThreads) void rep_stats_kernel(ReplayArgs A) {
 template <int POL>
 void launch_replay_pol(const ReplayArgs& a, hipStream_t s) {
   const int npl = (a.N + kWave - 1) / kWave;
+  if (a.gen_on) {
+    if (npl <= 1)
+      hipLaunchKernelGGL((replay_gen_kernel<1, POL>), dim3(a.R), dim3(kWave), 0, s, a);
+    else if (npl == 2)
+      hipLaunchKernelGGL((replay_gen_kernel<2, POL>), dim3(a.R), dim3(kWave), 0, s, a);
+    else
+      hipLaunchKernelGGL((replay_gen_kernel<4, POL>), dim3(a.R), dim3(kWave), 0, s, a);
+    return;
+  }
   if (npl <= 1) {
     hipLaunchKernelGGL((replay_kernel<1, POL>), dim3(a.R), dim3(kWave), 0, s, a);
   } else if (npl == 2) {

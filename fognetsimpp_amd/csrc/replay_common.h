@@ -74,6 +74,35 @@ __device__ __forceinline__ int64_t wave_scan_max_i64(int64_t v) {
   return v;
 }
 
+__device__ __forceinline__ int64_t wave_scan_add_i64(int64_t v) {
+  v += dpp_or_i64<0x111, 0xF>(0, v);  // row_shr:1
+  v += dpp_or_i64<0x112, 0xF>(0, v);  // row_shr:2
+  v += dpp_or_i64<0x114, 0xF>(0, v);  // row_shr:4
+  v += dpp_or_i64<0x118, 0xF>(0, v);  // row_shr:8
+  v += dpp_or_i64<0x142, 0xA>(0, v);  // row_bcast:15
+  v += dpp_or_i64<0x143, 0xC>(0, v);  // row_bcast:31
+  return v;
+}
+
+// ---------------------------------------------------------------- generated mode
+// Publishes c0 .. c0 + 63 of a generated replication, task c0 + lane in each
+// lane (the gen_kernel recipe, internal.h): tick ca (kNever past T) and
+// requirement cr.  carry: the tick before the chunk's first gap (the previous
+// chunk's last tick; max_j ul_j + 1 before the first chunk), advanced past the
+// chunk.  The gaps' prefix sum is exact integer arithmetic, so the ticks equal
+// gen_kernel's block scan.
+__device__ __forceinline__ void gen_chunk(const GenRep& g, int c0, int T, int lane, int64_t& carry, int64_t& ca,
+                                          int32_t& cr) {
+  const int i = c0 + lane;
+  int64_t gap = 0;
+  int32_t rq = 0;
+  if (i < T) gen_task(g, i, gap, rq);
+  const int64_t inc = wave_scan_add_i64(gap);
+  ca = i < T ? carry + inc : kNever;
+  cr = rq;
+  carry += readlane_i64(inc, kWave - 1);
+}
+
 // ---------------------------------------------------------------- OMNeT++ SimTime
 // The reference's signal arithmetic on simtime_t (OMNeT++ 4.6, scale 1e-12;
 // fognet_hip.h "Reference signal values"): dbl() = t * 1e-12, SimTime(double)

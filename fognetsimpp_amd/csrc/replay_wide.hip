@@ -58,6 +58,7 @@ struct WideLds {
   int32_t* g_j;     // [G][64]
   uint64_t* g_key;  // [G][64]
   uint32_t* hist;   // [FOGNET_HIST_METRICS][FOGNET_HIST_BINS]
+  uint64_t* reg_key;  // [G] EXT_HIER: cached regional minimum key (valid per reg_valid)
   int G;
 };
 
@@ -176,25 +177,37 @@ __device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, in
 
 // Workspace layout (launch_replay_wide, replay_wide_workspace_bytes).
 struct WideWs {
-  size_t e_off, nd_off, nxt_off, busy_off, bytes;
+  size_t e_off, nd_off, nxt_off, busy_off, gm_off, gd_off, gu_off, bytes;
 };
 
 __host__ __device__ __forceinline__ size_t align64(size_t x) { return (x + 63) & ~(size_t)63; }
 
-__host__ __device__ __forceinline__ WideWs wide_ws(int32_t R, int32_t T, int32_t N) {
+// gen: + the generated node parameters (MIPS, dl, ul) of each slot
+__host__ __device__ __forceinline__ WideWs wide_ws(int32_t R, int32_t T, int32_t N, bool gen) {
   const size_t SP = (size_t)wide_groups(N) * kWideGroupSlots;  // view slots per lane
   WideWs w;
   w.e_off = 0;
   w.nd_off = align64(w.e_off + (size_t)R * (size_t)T * sizeof(WideEntry));
   w.nxt_off = align64(w.nd_off + (size_t)R * (size_t)N * sizeof(WideNode));
   w.busy_off = align64(w.nxt_off + (size_t)R * kWave * SP * sizeof(int64_t));
-  w.bytes = align64(w.busy_off + (size_t)R * kWave * SP * sizeof(uint32_t));
+  w.gm_off = align64(w.busy_off + (size_t)R * kWave * SP * sizeof(uint32_t));
+  const size_t RN = gen ? (size_t)R * (size_t)N : 0;
+  w.gd_off = align64(w.gm_off + RN * sizeof(int32_t));
+  w.gu_off = align64(w.gd_off + RN * sizeof(int64_t));
+  w.bytes = align64(w.gu_off + RN * sizeof(int64_t));
   return w;
 }
 
+// Generated mode's per-slot node parameters (workspace).
+struct GenNodes {
+  int32_t* m;
+  int64_t* d;
+  int64_t* u;
+};
+
 template <int POL>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
-                                                int64_t* VN, uint32_t* VB, unsigned char* w_lds);
+                                                int64_t* VN, uint32_t* VB, GenNodes GN, unsigned char* w_lds);
 
 // One replication per workgroup (r = blockIdx.x), or, with A.wide_list set,
 // the replications the register kernel handed over, taken in turn by the
@@ -202,15 +215,15 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 // list (complete before this launch, stream order) is exhausted.
 template <int POL>
 __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry* E, WideNode* ND, int64_t* VN,
-                                                         uint32_t* VB) {
+                                                         uint32_t* VB, GenNodes GN) {
   extern __shared__ __align__(16) unsigned char w_lds[];
   if (A.wide_list == nullptr) {
-    replay_wide_rep<POL>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, w_lds);
+    replay_wide_rep<POL>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, GN, w_lds);
     return;
   }
   const int n = *A.wide_count;
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
-    replay_wide_rep<POL>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, w_lds);
+    replay_wide_rep<POL>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, GN, w_lds);
     __syncthreads();  // LDS reuse by the next replication
   }
 }
@@ -218,7 +231,7 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
 // Replication r with workspace slot wr.
 template <int POL>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
-                                                int64_t* VN, uint32_t* VB, unsigned char* w_lds) {
+                                                int64_t* VN, uint32_t* VB, GenNodes GN, unsigned char* w_lds) {
   constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
   constexpr bool kHier = POL == FOGNET_POLICY_EXT_HIER;
   constexpr bool kPerPublish = kExt || kHier;  // the decision depends on the publish itself
@@ -230,6 +243,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   L.g_key = reinterpret_cast<uint64_t*>(L.g_nxt + L.G * kWave);
   L.g_j = reinterpret_cast<int32_t*>(L.g_key + L.G * kWave);
   L.hist = reinterpret_cast<uint32_t*>(L.g_j + L.G * kWave);
+  L.reg_key = reinterpret_cast<uint64_t*>(L.hist + FOGNET_HIST_METRICS * FOGNET_HIST_BINS);
   const int SP = L.G * kWideGroupSlots;
   const WideView V{VN + ((size_t)wr * kWave + lane) * SP, VB + ((size_t)wr * kWave + lane) * SP};
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
@@ -237,14 +251,37 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   WideEntry* const e = E + (size_t)wr * (size_t)T;
   WideNode* const nd = ND + (size_t)wr * (size_t)N;
   const bool hist = A.hist != nullptr;
-  const int64_t arrive0 = T > 0 ? A.arrive[tbase] : kNever;
+  // generated mode (ReplayArgs::gen_on): the node parameters are computed
+  // into this slot's workspace, the trace 64 publishes at a time
+  const bool gen = A.gen_on != 0;
+  GenRep g{};
+  if (gen) g = gen_rep(A.gen, A.gen_r0 + r, r);
+  const size_t sbase = (size_t)wr * (size_t)N;
+  const int32_t* const P_mips = gen ? GN.m + sbase : A.mips + nbase;
+  const int64_t* const P_dl = gen ? GN.d + sbase : A.dl + nbase;
+  const int64_t* const P_ul = gen ? GN.u + sbase : A.ul + nbase;
+  const int64_t arrive0 = gen ? kNever : (T > 0 ? A.arrive[tbase] : kNever);
+  uint64_t ul_max = 0u;
 
   // ---- node parameters + preconditions (fognet_hip.h, fognet_batch_in);
   // every node's first advert {MIPS, busyTime = 0.0} has reached the broker
   bool bad = false;
   for (int j = lane; j < N; j += kWave) {
-    const int32_t m = A.mips[nbase + j];
-    const int64_t d = A.dl[nbase + j], u = A.ul[nbase + j], ia = A.init[nbase + j];
+    int32_t m;
+    int64_t d, u, ia;
+    if (gen) {
+      gen_node(g, j, m, d, u);
+      ia = u;
+      GN.m[sbase + j] = m;  // read back by this lane only (node j's owner)
+      GN.d[sbase + j] = d;
+      GN.u[sbase + j] = u;
+      ul_max = (uint64_t)u > ul_max ? (uint64_t)u : ul_max;
+    } else {
+      m = A.mips[nbase + j];
+      d = A.dl[nbase + j];
+      u = A.ul[nbase + j];
+      ia = A.init[nbase + j];
+    }
     const int64_t dn = A.down ? A.down[nbase + j] : kNever;
     bad |= (m <= 0) | (d < 0) | (u < 0) | (d > kMaxTick) | (u > kMaxTick) | (ia < u) | (ia >= arrive0);
     bad |= dn != kNever && (dn < ia || dn > kMaxTick);
@@ -264,6 +301,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   }
   __syncthreads();
   uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
+  int64_t gen_carry = gen ? (int64_t)~wave_min_u64(~ul_max) + 1 : 0;
 
   int64_t mn;
   int mj;
@@ -287,12 +325,20 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   // (adverts are the only view updates, BrokerBaseApp3.cc:123-130)
   bool view_changed = true;
   uint32_t k = 0u;
+  uint64_t reg_valid = 0ull, glob_key = 0ull;  // EXT_HIER decision cache (regions < 64)
+  bool glob_valid = false;
 
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
     const bool live = lane < cnt;
-    const int64_t ca = live ? A.arrive[tbase + c0 + lane] : kNever;
-    const int32_t cr = live ? A.req[tbase + c0 + lane] : 0;
+    int64_t ca;
+    int32_t cr;
+    if (gen) {
+      gen_chunk(g, c0, T, lane, gen_carry, ca, cr);
+    } else {
+      ca = live ? A.arrive[tbase + c0 + lane] : kNever;
+      cr = live ? A.req[tbase + c0 + lane] : 0;
+    }
     int32_t cg = 0;  // EXT_HIER: the publish's regional broker (region = group of the LDS minima)
     if constexpr (kHier) cg = live ? A.region[tbase + c0 + lane] : 0;
     // trace preconditions: nondecreasing ticks, requirement >= 0, ticks < 2^61
@@ -322,7 +368,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           uint32_t gb[kWideGroupSlots];
           group_load(V, g, gx, gb);
           WideNode h = hit ? ch : nd[j];
-          lerr |= !apply_advert(h, e, hit ? c_dl : A.dl[nbase + j], hit ? c_ul : A.ul[nbase + j], kHier ? A.hier_up : 0,
+          lerr |= !apply_advert(h, e, hit ? c_dl : P_dl[j], hit ? c_ul : P_ul[j], kHier ? A.hier_up : 0,
                                 nxt_j, busy_j);
           if (hit) ch = h;
           else nd[j] = h;
@@ -345,8 +391,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         uint64_t mc = ~0ull;
         uint32_t mjj = ~0u;
         for (int j = lane; j < N; j += kWave) {
-          const uint32_t S = min(rq / (uint32_t)A.mips[nbase + j], kExtSatS);
-          const uint64_t c = (uint64_t)A.dl[nbase + j] + ((uint64_t)V.busy[j / kWave] + S) * (uint64_t)kTicksPerSecond;
+          const uint32_t S = min(rq / (uint32_t)P_mips[j], kExtSatS);
+          const uint64_t c = (uint64_t)P_dl[j] + ((uint64_t)V.busy[j / kWave] + S) * (uint64_t)kTicksPerSecond;
           if (c < mc) {
             mc = c;
             mjj = (uint32_t)j;
@@ -356,11 +402,28 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         k = wave_min_u32(mc == m ? mjj : ~0u);
       } else if constexpr (kHier) {
         // regional broker: the smallest (busy, index) of its region (the region's LDS group
-        // minima, one per lane); above the threshold the parent takes the global one
+        // minima, one per lane); above the threshold the parent takes the global one.  Both
+        // are kept until an advert changes the view (the LDS region cache, bit b of reg_valid).
         const int b = __builtin_amdgcn_readlane(cg, jp);
-        const uint64_t kb = wave_min_u64(L.g_key[b * kWave + lane]);
+        if (view_changed) {
+          reg_valid = 0ull;
+          glob_valid = false;
+          view_changed = false;
+        }
+        uint64_t kb;
+        if ((reg_valid >> b) & 1ull) {
+          kb = L.reg_key[b];
+        } else {
+          kb = wave_min_u64(L.g_key[b * kWave + lane]);
+          if (lane == 0) L.reg_key[b] = kb;
+          reg_valid |= 1ull << b;
+        }
         escalated = (kb >> 32) > (uint64_t)A.hier_thr;
-        k = escalated ? (uint32_t)wave_min_u64(mk) : (uint32_t)kb;
+        if (escalated && !glob_valid) {
+          glob_key = wave_min_u64(mk);
+          glob_valid = true;
+        }
+        k = escalated ? (uint32_t)glob_key : (uint32_t)kb;
       } else if (view_changed) {
         // BrokerBaseApp3.cc:267-281: busy_j + req/mips_0 < tempp over exact
         // integer busy values <=> the smallest (busy, j)
@@ -374,9 +437,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         if (cj >= 0) nd[cj] = ch;  // write back the previous node's record
         cj = (int)k;
         ch = nd[k];
-        c_mips = A.mips[nbase + k];
-        c_dl = A.dl[nbase + k];
-        c_ul = A.ul[nbase + k];
+        c_mips = P_mips[k];
+        c_dl = P_dl[k];
+        c_ul = P_ul[k];
         c_down = A.down ? A.down[nbase + k] : kNever;
       }
       const int32_t mips_k = (int32_t)readlane_u32((uint32_t)c_mips, kl);
@@ -425,20 +488,28 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         a = ca + dl_k;
       }
       const uint32_t Sd = min(S, kWideMaxS);  // (a larger service time is an error unless the task is lost)
-      const uint32_t Cs = wave_scan_add_u32(in_run ? Sd : 0u);  // service seconds of the run up to this task
-      const uint64_t C = tl_C + (uint64_t)Cs;                    // cumulative assigned service
+      const bool one = Lr == 1;                // a single publish needs no wave scans
+      // service seconds of the run up to this task
+      const uint32_t Cs = one ? (in_run ? Sd : 0u) : wave_scan_add_u32(in_run ? Sd : 0u);
+      const uint64_t C = tl_C + (uint64_t)Cs;  // cumulative assigned service
       int64_t start = kNever, done = kNever;
       uint32_t status = FOGNET_TASK_LOST;
       if (base_done != kNever) {
         int64_t X = in_run ? (int64_t)((uint64_t)a - (uint64_t)ticks_of(Cs - Sd)) : INT64_MIN;
-        X = wave_scan_max_i64(X);
+        if (!one) X = wave_scan_max_i64(X);
         const int64_t dmax = base_done > X ? base_done : X;
         const int64_t dn = (int64_t)((uint64_t)dmax + (uint64_t)ticks_of(Cs));  // unclamped
         const int64_t st = dn - ticks_of(Sd);
-        const int64_t dn_up = dpp_or_i64<kDppWaveShr1>(0, dn);
-        const uint32_t S_up = dpp_or_u32<kDppWaveShr1>(0u, Sd);
-        const int64_t prev_done = lane == jp ? base_done : dn_up;
-        const uint32_t prev_S = lane == jp ? tl_S : S_up;
+        int64_t prev_done = base_done;
+        uint32_t prev_S = tl_S;
+        if (!one) {
+          const int64_t dn_up = dpp_or_i64<kDppWaveShr1>(0, dn);
+          const uint32_t S_up = dpp_or_u32<kDppWaveShr1>(0u, Sd);
+          if (lane != jp) {
+            prev_done = dn_up;
+            prev_S = S_up;
+          }
+        }
         if (in_run && a < down_k) {
           if (prev_done < a) status = 5u;       // idle: "task assigned" (:282-301)
           else if (prev_done > a) status = 4u;  // busy: "task queued" (:304-313)
@@ -578,8 +649,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 
 template <int POL>
 void launch_wide_pol(const ReplayArgs& a, int32_t slots, WideEntry* e, WideNode* nd, int64_t* vn, uint32_t* vb,
-                     size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb);
+                     GenNodes gn, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb, gn);
 }
 
 }  // namespace
@@ -587,25 +658,27 @@ void launch_wide_pol(const ReplayArgs& a, int32_t slots, WideEntry* e, WideNode*
 size_t replay_wide_lds_bytes(int32_t N) {
   const size_t G = (size_t)wide_groups(N);
   return G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int32_t)) +
-         FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t);
+         FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t) + G * sizeof(uint64_t);
 }
 
-size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N) { return wide_ws(R, T, N).bytes; }
+size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen) { return wide_ws(R, T, N, gen).bytes; }
 
 hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slots, hipStream_t s) {
-  const WideWs w = wide_ws(slots, a.T, a.N);
+  const WideWs w = wide_ws(slots, a.T, a.N, a.gen_on != 0);
   unsigned char* const base = static_cast<unsigned char*>(workspace);
   WideEntry* const e = reinterpret_cast<WideEntry*>(base + w.e_off);
   WideNode* const nd = reinterpret_cast<WideNode*>(base + w.nd_off);
   int64_t* const vn = reinterpret_cast<int64_t*>(base + w.nxt_off);
   uint32_t* const vb = reinterpret_cast<uint32_t*>(base + w.busy_off);
+  const GenNodes gn{reinterpret_cast<int32_t*>(base + w.gm_off), reinterpret_cast<int64_t*>(base + w.gd_off),
+                    reinterpret_cast<int64_t*>(base + w.gu_off)};
   const size_t lds = replay_wide_lds_bytes(a.N);
   if (a.policy == FOGNET_POLICY_EXT_LAT)
-    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, slots, e, nd, vn, vb, lds, s);
+    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, slots, e, nd, vn, vb, gn, lds, s);
   else if (a.policy == FOGNET_POLICY_EXT_HIER)
-    launch_wide_pol<FOGNET_POLICY_EXT_HIER>(a, slots, e, nd, vn, vb, lds, s);
+    launch_wide_pol<FOGNET_POLICY_EXT_HIER>(a, slots, e, nd, vn, vb, gn, lds, s);
   else
-    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, slots, e, nd, vn, vb, lds, s);
+    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, slots, e, nd, vn, vb, gn, lds, s);
   return hipGetLastError();
 }
 

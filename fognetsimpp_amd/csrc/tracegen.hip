@@ -49,36 +49,26 @@ __global__ __launch_bounds__(kGenThreads) void gen_kernel(fognet_gen_params p, i
   __shared__ int64_t sh[kGenThreads / kWave];
   const int rl = blockIdx.x;  // local replication index
   const int64_t r = r0 + rl;
-  const uint32_t k0 = p.seed, k1 = (uint32_t)r;
-  const int64_t scale = p.lat_scale[rl];
-  const uint64_t span = 1000000000ull - 1000000ull + 1ull;
+  const GenRep g = gen_rep(p, r, rl);
   int64_t my_max = INT64_MIN;
   for (int j = threadIdx.x; j < N; j += kGenThreads) {
-    const U4 x = philox4x32_10(U4{(uint32_t)j, 1u, 0u, 0u}, k0, k1);
-    const int64_t d = (int64_t)(1000000ull + (uint64_t)x.x % span) * scale;
-    const int64_t u = (int64_t)(1000000ull + (uint64_t)x.y % span) * scale;
+    int32_t m;
+    int64_t d, u;
+    gen_node(g, j, m, d, u);
     const size_t o = (size_t)rl * N + j;
     dl[o] = d;
     ul[o] = u;
     init[o] = u;
-    mips[o] = 1000 * (1 + j % 4);
+    mips[o] = m;
     my_max = u > my_max ? u : my_max;
   }
   const int64_t start = block_max_i64(my_max, sh) + 1;
-  const double mean = p.mean_gap_ticks[rl];
-  const uint64_t rspan = (uint64_t)(p.req_hi - p.req_lo) + 1ull;
   int64_t carry = start;
   for (int base = 0; base < T; base += kGenThreads) {
     const int i = base + threadIdx.x;
     int64_t gap = 0;
     int32_t rq = 0;
-    if (i < T) {
-      const U4 x = philox4x32_10(U4{(uint32_t)i, 0u, 0u, 0u}, k0, k1);
-      rq = (int32_t)((uint64_t)p.req_lo + (uint64_t)x.x % rspan);
-      const uint64_t k53 = ((uint64_t)x.y << 21) | ((uint64_t)x.z >> 11);
-      const double u = (double)(k53 + 1ull) * 0x1p-53;
-      gap = (int64_t)(mean * neg_log_unit(u));
-    }
+    if (i < T) gen_task(g, i, gap, rq);
     const int64_t inc = block_scan_i64(gap, sh);
     if (i < T) {
       const size_t o = (size_t)rl * T + i;

@@ -279,6 +279,44 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
     return out
 
 
+def run_generated(ctx: Context, seed: int, R: int, T: int, N: int, mean_gap_ticks, lat_scale, r0: int = 0,
+                  req_lo: int = 1000, req_hi: int = 64000, out: BatchResult | None = None, ring_capacity: int = 0,
+                  policy: str | int = "REF_V3", power=None, hist: bool = True, energy: bool = False,
+                  device=None, stream=None) -> BatchResult:
+    """Statistics-only replay of generated replications r0 .. r0+R-1
+    (fognet_run_generated_dev): the trace recipe of
+    :func:`generate_trace` is computed inside the replay kernel 64 publishes at
+    a time, so neither the trace nor per-task outputs exist in memory.  The
+    records equal ``generate_trace`` + ``run_batch`` on the same replications.
+    ``power``: optional (p_busy, p_idle) device tensors [R, N] or [N]."""
+    device = device if device is not None else torch.device("cuda", ctx.device)
+    if isinstance(mean_gap_ticks, torch.Tensor):
+        mg, ls = mean_gap_ticks.reshape(R).contiguous(), lat_scale.reshape(R).contiguous()
+    else:
+        mg = torch.as_tensor(np.asarray(mean_gap_ticks, dtype=np.float64).reshape(R), device=device)
+        ls = torch.as_tensor(np.asarray(lat_scale, dtype=np.int64).reshape(R), device=device)
+    pb, pi = power if power is not None else (None, None)
+    stride = 0
+    if pb is not None:
+        if tuple(pb.shape) != tuple(pi.shape) or pb.shape[-1] != N or (pb.dim() == 2 and pb.shape[0] != R):
+            raise FognetError(_abi.FOGNET_ERR_ARG, "power model arrays must be [R, N] or [N]")
+        stride = N if pb.dim() == 2 else 0
+    if out is None:
+        out = allocate_outputs(R, T, device, N=N, energy=energy and pb is not None, hist=hist, per_task=False)
+    elif out.stats.numel() < R * _abi.REP_STATS_DTYPE.itemsize:
+        raise FognetError(_abi.FOGNET_ERR_ARG, "stats buffer too small")
+    pol = POLICIES[policy] if isinstance(policy, str) else int(policy)
+    gp = _abi.GenParams(seed & 0xFFFFFFFF, req_lo, req_hi, 0, _ptr(mg), _ptr(ls))
+    bi = _abi.BatchIn(R, T, N, pol, stride, ring_capacity, None, None, None, None, None, None,
+                      _ptr(pb), _ptr(pi), None, None, 0, 0, 0)
+    bo = _abi.BatchOut(None, None, None, None, _ptr(out.stats), _ptr(out.node_energy), _ptr(out.hist))
+    s = C.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(device)
+    ctx.check(ctx._lib.fognet_run_generated_dev(ctx.handle, C.byref(gp), r0, C.byref(bi), C.byref(bo), s),
+              "run_generated")
+    out._keep = (mg, ls)
+    return out
+
+
 def user_stats(ctx: Context, trace: dict, out: BatchResult, user_ul, user_dl) -> np.ndarray:
     """User-side signals (fognet_user_stats_dev) of a finished replay: broker
     ``delay`` and mqttApp2's ``latency`` / ``latencyH1`` / ``taskTime`` as exact

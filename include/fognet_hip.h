@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define FOGNET_ABI_VERSION 8
+#define FOGNET_ABI_VERSION 9
 #define FOGNET_TICKS_PER_SECOND 1000000000000LL
 
 /* Latency histograms (device-side statistics, summed over replications; the
@@ -422,6 +422,21 @@ int fognet_gen_trace_dev(fognet_ctx *ctx, const fognet_gen_params *p, int64_t r0
                          int32_t T, int32_t N, int64_t *arrive_tick, int32_t *req_mips,
                          int32_t *mips, int64_t *dl_tick, int64_t *ul_tick, int64_t *init_adv_tick,
                          void *hip_stream);
+
+/* Generated replay ("traces are generated in-kernel ...
+ * only stats and histograms are written"): replications r0 .. r0 + R - 1 of
+ * the fognet_gen_trace_dev recipe (p; mean_gap_ticks / lat_scale indexed by the
+ * local replication 0 .. R-1) are replayed with each 64-publish chunk of the
+ * trace and the node parameters computed inside the replay kernel; no trace
+ * and no per-task output ever reaches memory.  Results equal
+ * fognet_gen_trace_dev + fognet_run_batch_dev on the same replications.
+ *   in:  R, T, N, policy (REF_V3 or EXT_LAT), ring_capacity, p_busy_w/p_idle_w,
+ *        node_stride; every trace/node-parameter pointer, down_tick and region
+ *        must be NULL.  T * (req_hi / 1000) < 2^32 (node totals are 32-bit).
+ *   out: stats [R] (required), hist (added to), node_energy_j (nullable);
+ *        node/status/start_tick/done_tick must be NULL. */
+int fognet_run_generated_dev(fognet_ctx *ctx, const fognet_gen_params *p, int64_t r0,
+                             const fognet_batch_in *in, fognet_batch_out *out, void *hip_stream);
 
 /* Synchronise the context's device. */
 int fognet_sync(fognet_ctx *ctx);

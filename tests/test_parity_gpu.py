@@ -490,6 +490,63 @@ def test_stats_only_equals_full_outputs(ctx, monkeypatch, kind):
     assert torch.equal(so.hist, full.hist)
 
 
+@pytest.mark.parametrize("kind", ["c4_first", "c4_last", "n64", "n100", "ext_lat", "handover", "wide", "energy"])
+def test_generated_equals_materialized(ctx, monkeypatch, kind):
+    """Generated replays (fognet_run_generated_dev: trace chunks and node
+    parameters computed inside the replay kernel, statistics only: C4's mode,
+    SURVEY.md §8(d)) give the records, histograms and energy of
+    fognet_gen_trace_dev + fognet_run_batch_dev on the same replications
+    (which test_c4_workload_shape_matches_oracle checks against the oracle)."""
+    seed, R, T, N, r0, ring, policy = 0x5EED0004, 64, 10_000, 256, 0, 0, "REF_V3"
+    if kind == "c4_last":  # the last block of the 1,000,000-replication job
+        r0 = 1_000_000 - R
+    if kind == "n64":
+        N, T = 64, 3000
+    if kind == "n100":
+        R, N, T = 16, 100, 4001
+    if kind == "ext_lat":
+        policy, T = "EXT_LAT", 3000
+    if kind == "handover":  # every replication overflows a 4-entry ring: the wide kernel generates too
+        ring, T = 4, 3000
+    if kind == "wide":
+        monkeypatch.setenv("FOGNET_REPLAY_KERNEL", "wide")
+        T = 3000
+    dev = torch.device("cuda", ctx.device)
+    mg, sc = fa.sweep_params(np.arange(r0, r0 + R), N)
+    d = {k: v for k, v in fa.generate_trace(ctx, seed, R, T, N, mg, sc, r0=r0).items() if not k.startswith("_")}
+    power = None
+    if kind == "energy":
+        pb, pi = fa.power_model(1000 * (1 + np.arange(N) % 4))
+        power = tuple(torch.from_numpy(np.tile(x, (R, 1))).to(dev) for x in (pb, pi))
+        d = dict(d, p_busy=power[0], p_idle=power[1])
+    full = fa.run_batch(ctx, d, ring_capacity=ring, policy=policy, hist=True)
+    gen = fa.run_generated(ctx, seed, R, T, N, mg, sc, r0=r0, ring_capacity=ring, policy=policy, power=power,
+                           hist=True, energy=power is not None)
+    torch.cuda.synchronize()
+    st = full.rep_stats()
+    assert (st["status"] == 0).all() and (st["n_tasks"] == T).all()
+    if kind == "handover":
+        assert (st["max_pending"] > 4).all()
+    assert gen.rep_stats().tobytes() == st.tobytes()
+    assert torch.equal(gen.hist, full.hist)
+    if power is not None:
+        assert torch.equal(gen.node_energy, full.node_energy)
+
+
+def test_generated_preconditions(ctx):
+    """fognet_run_generated_dev refuses what it cannot replay exactly."""
+    mg, sc = fa.sweep_params(np.arange(2), 8)
+    with pytest.raises(fa.FognetError) as e:
+        fa.run_generated(ctx, 1, 2, 100, 8, mg, sc, policy="EXT_HIER")
+    assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED
+    with pytest.raises(fa.FognetError) as e:  # T * req_hi / 1000 >= 2^32: node totals would wrap
+        fa.run_generated(ctx, 1, 2, 2_000_000, 8, mg, sc, req_hi=4_000_000)
+    assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED
+    out = fa.run_generated(ctx, 1, 2, 0, 8, mg, sc)  # empty traces
+    torch.cuda.synchronize()
+    assert (out.rep_stats()["status"] == 0).all() and (out.rep_stats()["n_tasks"] == 0).all()
+
+
 # ------------------------------------------------------------------ a10/a11 statistics and the EXT_LAT policy
 # Builder-defined rows (include/fognet_hip.h): parity against the oracle's
 # restatement of the same definitions (not pinned by the reference).

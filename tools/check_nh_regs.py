@@ -1,6 +1,6 @@
 """Audit the replay kernel ISA: the reserved registers that receive the
-inline-asm prefetch loads (v112..v127, kNhBase in replay.hip) must be
-referenced only by inline asm (the prefetch loads and the wait+copy reads),
+inline-asm prefetch loads (v112..v127, kNhBase in replay.hip; v152..v167,
+kNhBaseGen, in the generated-mode replay_gen_kernel) must be referenced only by inline asm (the prefetch loads and the wait+copy reads),
 anywhere in the kernel.  Usage: python tools/check_nh_regs.py build/asm/replay-...-gfx950.s"""
 import re
 import sys
@@ -15,7 +15,12 @@ def regs_of(s):
     return out
 
 
-def audit(path, kernel_prefix="_ZN6fognet12_GLOBAL__N_113replay_kernelILi"):
+def audit(path):
+    return (audit_one(path, "_ZN6fognet12_GLOBAL__N_113replay_kernelILi", 112)
+            + audit_one(path, "_ZN6fognet12_GLOBAL__N_117replay_gen_kernelILi", 152))
+
+
+def audit_one(path, kernel_prefix, base):
     text = open(path).read().split("\n")
     bad_total = 0
     found = 0
@@ -40,7 +45,7 @@ def audit(path, kernel_prefix="_ZN6fognet12_GLOBAL__N_113replay_kernelILi"):
                 in_asm = False
             elif in_asm and ln.startswith("global_load_dwordx4"):
                 nh |= regs_of(ln.split(",")[0])
-        assert nh and min(nh) >= 112, f"prefetch destinations outside the reserved range: {sorted(nh)}"
+        assert nh and min(nh) >= base and max(nh) < base + 16, f"prefetch destinations outside the reserved range: {sorted(nh)}"
         bad = []
         in_asm = False
         for ln in body:
@@ -54,11 +59,11 @@ def audit(path, kernel_prefix="_ZN6fognet12_GLOBAL__N_113replay_kernelILi"):
                 continue
             if not in_asm and regs_of(ln) & nh:
                 bad.append(ln)
-        print(f"NPL={npl} policy={pol}: prefetch registers {sorted(nh)}; compiler references outside asm: {len(bad)}")
+        print(f"{'replay_gen_kernel' if 'gen' in kernel_prefix else 'replay_kernel'} NPL={npl} policy={pol}: prefetch registers {sorted(nh)}; compiler references outside asm: {len(bad)}")
         for b in bad[:20]:
             print("   ", b)
         bad_total += len(bad)
-    assert found == 6, f"expected 6 replay_kernel instantiations in the ISA, found {found}"
+    assert found == 6, f"expected 6 {kernel_prefix} instantiations in the ISA, found {found}"
     return bad_total
 
 

@@ -40,6 +40,11 @@ def main():
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
             if k in per:
                 out[k + "_frac_of_wave_cycles"] = per[k] / per["SQ_WAVE_CYCLES"]
+    # VALU busy (rocprof's VALUBusy, gfx94x formula): active VALU cycles (x4: a wave64 VALU op
+    # occupies a SIMD for 4 cycles) per SIMD (1024 on MI355X) over the GPU-active cycles of one XCD
+    # (GRBM_GUI_ACTIVE is summed over the 8 XCDs)
+    if "SQ_ACTIVE_INST_VALU" in per and "GRBM_GUI_ACTIVE" in per:
+        out["valu_busy"] = per["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (per["GRBM_GUI_ACTIVE"] / 8)
     # the record bench.py reads (profiles/pmc_traffic[_c5].json): argv[5] = "R,T,N" (default C3)
     if "hbm_bytes_per_launch" in out:
         R, T, N = (int(x) for x in sys.argv[5].split(",")) if len(sys.argv) > 5 else (4096, 100000, 256)
