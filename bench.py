@@ -87,9 +87,9 @@ def main():
     ap.add_argument("--workload", default="c3", choices=("c1", "c3", "c4", "c5"))
     ap.add_argument("--R-total", type=int, default=None,
                     help="c4/c5: replications over all ranks (default 1,000,000 / 1024)")
-    ap.add_argument("--block", type=int, default=16384,
-                    help="c4: replications per device block (replay launches queue 4x the resident waves, so "
-                         "waves that finish early are refilled)")
+    ap.add_argument("--block", type=int, default=0,
+                    help="c4: replications per fognet_run_generated_dev call (0: the rank's whole shard in one "
+                         "launch; its resident workgroups take replications from a work counter)")
     args = ap.parse_args()
     if args.policy is None:
         args.policy = "EXT_HIER" if args.workload == "c5" else "REF_V3"
@@ -279,8 +279,9 @@ def bench_c4(args, ctx, dev, dist, world, rank):
     block), the histograms and the energy survive.  Generation is inside the
     timed region."""
     from fognetsimpp_amd.dist import shard
-    T, N, B = args.T, args.N, args.block
+    T, N = args.T, args.N
     r0, n = shard(args.R_total, world, rank)
+    B = args.block if args.block > 0 else n
     blocks = [(r0 + b, min(B, n - b)) for b in range(0, n, B)]
     mg_all, sc_all = fa.sweep_params(np.arange(r0, r0 + n), N)
     mg_d = torch.from_numpy(np.ascontiguousarray(mg_all)).to(dev)
@@ -355,7 +356,7 @@ def bench_c4(args, ctx, dev, dist, world, rank):
     if os.path.exists(prof):
         with open(prof) as f:
             pj = json.load(f)
-        if pj.get("config") == {"T": T, "N": N, "block": B, "ring": args.ring, "policy": args.policy}:
+        if pj.get("config") == {"T": T, "N": N, "block": args.block, "ring": args.ring, "policy": args.policy}:
             valu = pj.get("valu_busy")
     if rank == 0:
         line = {

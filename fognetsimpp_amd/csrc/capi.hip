@@ -13,9 +13,13 @@
 
 struct fognet_ctx {
   int device = -1;
+  int cus = 256;  // compute units (generated-mode launch size)
   hipStream_t stream = nullptr;  // private stream for the host-buffer entry points
   fognet::RingEntry* ring = nullptr;
   size_t ring_bytes = 0;
+  // partial job records of a multi-block reduction (fognet_reduce_stats_dev)
+  void* red = nullptr;
+  size_t red_bytes = 0;
   // scratch for the v2 scalar decision
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -147,6 +151,17 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a, boo
 
 // N > 256 takes the wide replay kernel (replay_wide.hip); FOGNET_REPLAY_KERNEL=wide
 // forces it for any N (used by the parity tests to check both kernels).
+// FOGNET_REPLAY_STATS=inloop: the statistics of a fused replay come from
+// in-loop accumulators (replay_inl_kernel, 3 waves/SIMD) instead of the
+// epilogue's re-read of the outputs (replay_kernel, 4 waves/SIMD); the records
+// are identical (the parity tests run both).  Not the default: at C3 (4,096
+// replications, all resident at 4 waves/SIMD) it measured 20.9 ms/launch
+// against 14.1 ms, the fourth wave per SIMD being worth more than the re-read.
+bool use_inloop() {
+  const char* f = getenv("FOGNET_REPLAY_STATS");
+  return f != nullptr && strcmp(f, "inloop") == 0;
+}
+
 bool use_wide(int32_t N) {
   if (N > fognet::kWave * fognet::kMaxNodesPerLane) return true;
   const char* f = getenv("FOGNET_REPLAY_KERNEL");
@@ -187,6 +202,7 @@ int fognet_create(fognet_ctx** out, int hip_device) {
   fognet_ctx* c = new (std::nothrow) fognet_ctx();
   if (!c) return FOGNET_ERR_OOM;
   c->device = hip_device;
+  if (prop.multiProcessorCount > 0) c->cus = prop.multiProcessorCount;
   if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return FOGNET_ERR_DEVICE;
@@ -200,6 +216,7 @@ void fognet_destroy(fognet_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->ring) (void)hipFree(c->ring);
   if (c->scratch) (void)hipFree(c->scratch);
+  if (c->red) (void)hipFree(c->red);
   if (c->host_stage) (void)hipHostFree(c->host_stage);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -393,6 +410,9 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
   // both stages: the replay kernel runs the statistics pass as its epilogue
   a.fuse_stats = which == 3 ? 1 : 0;
   if (a.fuse_stats) which = 1;
+  // statistics accumulated in the loop (replay_inl_kernel) where the node tails hold exact totals
+  a.inloop = a.fuse_stats && (uint64_t)a.T * (uint64_t)a.max_s < (1ull << 32) && use_inloop() ? 1 : 0;
+  if (a.inloop) a.no_task_out = stats_only ? 1 : 0;
   if (which & 1) {
     // workspace: [hand-over counter | hand-over list [R] | pending-task rings, reused by the wide kernel's
     // replay of the handed-over replications once the register kernel is done (stream order)]
@@ -402,7 +422,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
     const size_t head = align256(256 + (size_t)a.R * sizeof(int32_t));
     const size_t body = ring_bytes > fb_bytes ? ring_bytes : fb_bytes;
-    const size_t RT = stats_only ? (size_t)a.R * (size_t)a.T : 0;
+    const size_t RT = stats_only && !a.inloop ? (size_t)a.R * (size_t)a.T : 0;
     const size_t o_node = head + align256(body), o_st = o_node + align256(RT * 4), o_start = o_st + align256(RT),
                  o_done = o_start + align256(RT * 8), total = o_done + align256(RT * 8);
     rc = ensure(c, (void**)&c->ring, &c->ring_bytes, total, "ring workspace");
@@ -411,7 +431,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     a.wide_count = reinterpret_cast<int32_t*>(base);
     a.wide_list = reinterpret_cast<int32_t*>(base + 256);
     a.ring = reinterpret_cast<fognet::RingEntry*>(base + head);
-    if (stats_only) {
+    if (stats_only && !a.inloop) {
       a.out_node = reinterpret_cast<int32_t*>(base + o_node);
       a.out_status = reinterpret_cast<uint8_t*>(base + o_st);
       a.out_start = reinterpret_cast<int64_t*>(base + o_start);
@@ -470,8 +490,11 @@ int fognet_run_generated_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t 
     e = fognet::launch_replay_wide(a, c->ring, a.R, (hipStream_t)stream);
     return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "wide replay launch");
   }
-  // workspace: [hand-over counter | list [R] | rings, reused by the wide hand-over]
-  const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
+  // workspace: [hand-over counter, work counter | list [R] | rings of the resident workgroups, reused by
+  // the wide hand-over]
+  const int64_t resident = (int64_t)c->cus * fognet::kGenWavesPerCu;
+  a.gen_slots = (int32_t)(a.R < resident ? a.R : resident);
+  const size_t ring_bytes = (size_t)a.gen_slots * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
   const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
   const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N, true);
   const size_t head = align256(256 + (size_t)a.R * sizeof(int32_t));
@@ -482,8 +505,9 @@ int fognet_run_generated_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t 
   a.wide_count = reinterpret_cast<int32_t*>(base);
   a.wide_list = reinterpret_cast<int32_t*>(base + 256);
   a.ring = reinterpret_cast<fognet::RingEntry*>(base + head);
-  e = hipMemsetAsync(a.wide_count, 0, sizeof(int32_t), (hipStream_t)stream);
-  if (e != hipSuccess) return hip_fail(c, e, "hand-over counter");
+  a.queue = reinterpret_cast<int32_t*>(base + sizeof(int32_t));
+  e = hipMemsetAsync(base, 0, 2 * sizeof(int32_t), (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "hand-over and work counters");
   e = fognet::launch_replay(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(c, e, "replay launch");
   e = fognet::launch_replay_wide(a, base + head, slots, (hipStream_t)stream);
@@ -646,7 +670,13 @@ int fognet_reduce_stats_dev(fognet_ctx* c, const fognet_rep_stats* stats, int32_
   if (!c || !out || (R > 0 && !stats) || R < 0) return FOGNET_ERR_ARG;
   int rc = set_device(c);
   if (rc) return rc;
-  hipError_t e = fognet::launch_reduce_stats(stats, R, out, (hipStream_t)stream);
+  const int32_t np = fognet::reduce_stats_parts(R);
+  if (np > 0) {
+    rc = ensure(c, &c->red, &c->red_bytes, (size_t)np * sizeof(fognet_job_stats), "reduction partials");
+    if (rc) return rc;
+  }
+  hipError_t e = fognet::launch_reduce_stats(stats, R, out, static_cast<fognet_job_stats*>(c->red),
+                                             (hipStream_t)stream);
   return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "reduce launch");
 }
 

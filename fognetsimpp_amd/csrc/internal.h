@@ -241,10 +241,18 @@ struct ReplayArgs {
   // replication r's trace and node parameters are the gen_kernel recipe's for
   // global index gen_r0 + r, computed in the kernel (arrive/req/mips/dl/ul/init
   // unused), and only statistics are written (no per-task outputs).
+  // 1: replay_inl_kernel (statistics accumulated in the loop, no epilogue
+  // re-read; fused-statistics replays while T * max_s < 2^32)
+  int32_t inloop;
   int32_t gen_on;
+  int32_t gen_slots;  // generated mode: workgroups (and ring slots) of the work-counter launch
   int64_t gen_r0;
   fognet_gen_params gen;
+  int32_t* queue;     // generated mode: work counter (zeroed before the launch)
 };
+
+// Generated-mode launch: 3 waves per SIMD, 4 SIMDs per CU (replay_gen_kernel)
+constexpr int kGenWavesPerCu = 12;
 
 // Internal per-replication status between the two replay kernels (never
 // returned: the wide kernel overwrites the record of every listed replication).
@@ -304,7 +312,12 @@ hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slot
 
 hipError_t launch_replay(const ReplayArgs& a, hipStream_t s);
 hipError_t launch_rep_stats(const ReplayArgs& a, hipStream_t s);
-hipError_t launch_reduce_stats(const fognet_rep_stats* st, int32_t R, fognet_job_stats* out,
+// Job reduction: one block up to kReduceChunk records, else blocks of
+// kReduceChunk into reduce_stats_parts(R) partial records (workspace `parts`)
+// and a merge.
+constexpr int32_t kReduceChunk = 4096;
+int32_t reduce_stats_parts(int32_t R);
+hipError_t launch_reduce_stats(const fognet_rep_stats* st, int32_t R, fognet_job_stats* out, fognet_job_stats* parts,
                                hipStream_t s);
 hipError_t launch_decide(int64_t m, int32_t n, int64_t view_stride, const double* busy, const int32_t* mips,
                          const int32_t* req, int32_t* node, int32_t* status, hipStream_t s);

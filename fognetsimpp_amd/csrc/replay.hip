@@ -591,14 +591,17 @@ __device__ __forceinline__ void stats_finish(const ReplayArgs& A, int r, int64_t
 }
 
 // The replay of replication blockIdx.x (replay_kernel, replay_gen_kernel).
-// GEN: generated mode (ReplayArgs::gen_on): the trace chunks and node
-// parameters are computed here, the statistics are accumulated as the runs
-// are pushed (registers), and nothing is stored per task.
-template <int NPL, int POL, bool GEN>
-__device__ __forceinline__ void replay_body(const ReplayArgs& A) {
+// INL: the statistics are accumulated as the runs are pushed (registers,
+// 3 waves/SIMD) instead of by the fused epilogue's re-read of the outputs;
+// per-task outputs are still stored unless A.no_task_out.
+// GEN (implies INL): generated mode (ReplayArgs::gen_on): the trace chunks
+// and node parameters are computed here, and nothing is stored per task.
+// r: the replication; slot: its pending-task rings in the workspace.
+template <int NPL, int POL, bool GEN, bool INL>
+__device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, const int slot) {
+  static_assert(INL || !GEN, "generated mode accumulates in the loop");
   constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
-  constexpr int kSet = GEN ? 4 : 0;  // prefetch register set
-  const int r = blockIdx.x;
+  constexpr int kSet = INL ? 4 : 0;  // prefetch register set
   const int lane = threadIdx.x;
   __shared__ int64_t s_dl[NPL * kWave];
   __shared__ int64_t s_ul[NPL * kWave];
@@ -608,6 +611,9 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A) {
   __shared__ uint32_t s_tlC[NPL * kWave];  // tail cumulative service (mod 2^32)
   __shared__ uint32_t s_tlS[NPL * kWave];  // tail service seconds
   __shared__ uint32_t s_ch[3 * kWave];     // staged trace chunk: arrive lo | arrive hi | req
+  // in-loop statistics: the histogram rows (generated mode: in the unused chunk stage)
+  __shared__ uint32_t s_hl[(INL && !GEN) ? FOGNET_HIST_METRICS * FOGNET_HIST_BINS : 1];
+  uint32_t* const s_hs = GEN ? s_ch : s_hl;
 
   const int T = A.T, N = A.N;
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
@@ -663,18 +669,17 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A) {
     s_tlS[k] = 0u;
     st[s].cnt = 0u;
   }
-  // generated: the histogram rows live in the (unused) chunk stage
-  if (GEN && A.hist)
-    for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) s_ch[h] = 0u;
+  if (INL && A.hist)
+    for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) s_hs[h] = 0u;
   __syncthreads();
   int64_t gen_carry = 0;
   if constexpr (GEN) gen_carry = (int64_t)~wave_min_u64(~ul_max) + 1;
-  Acc gacc = acc_identity();  // generated: this lane's tasks (lane l: tasks l, l + 64, ...)
+  Acc gacc = acc_identity();  // in-loop statistics: this lane's tasks (lane l: tasks l, l + 64, ...)
 
   uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
   if (N <= 0) err = FOGNET_ERR_NO_NODES;
 
-  RingEntry* const ring_r = A.ring + (size_t)r * (size_t)N * ((size_t)qmask + 1u);
+  RingEntry* const ring_r = A.ring + (size_t)slot * (size_t)N * ((size_t)qmask + 1u);
   const int q_log2 = A.q_log2;
   // ring of this lane's node in slot s (lanes past N alias node 0: in bounds, never used)
   // Per-lane addresses are rebuilt at each use from wave-uniform bases and an
@@ -946,21 +951,22 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A) {
         e.C = tlC_k + Cs;
         e.S = S;
         ring_k[((cnt_k & 0xFFFFu) + (uint32_t)(lane - jp)) & qmask] = e;
-        if constexpr (GEN) {
+        if constexpr (INL) {
           // the task's statistics (the fused epilogue's, rep_stats_kernel's)
           const int64_t resp = done - ca;
           add_moment(gacc.rs_lo, gacc.rs_hi, gacc.rq_lo, gacc.rq_hi, (uint64_t)resp);
           gacc.rmin = min(gacc.rmin, resp);
           gacc.rmax = max(gacc.rmax, resp);
-          if (A.hist) atomicAdd(&s_ch[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
+          if (A.hist) atomicAdd(&s_hs[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
           if (status == 4u) {
             gacc.n4 += 1u;
             acc_qtime(gacc.qs_lo, gacc.qs_hi, gacc.qq_lo, gacc.qq_hi, gacc.qq_top, gacc.qmin, gacc.qmax, gacc.nqt,
-                      gacc.nqo, start, a, A.hist ? s_ch : nullptr);
+                      gacc.nqo, start, a, A.hist ? s_hs : nullptr);
           } else {
             gacc.n5 += 1u;
           }
-        } else {
+        }
+        if (!GEN && !(INL && A.no_task_out)) {
           // chunk bases are wave-uniform (SGPR) and the lane index a 32-bit
           // offset, so no per-lane 64-bit addresses stay live across the chunk
           const size_t o = tbase + (size_t)c0;
@@ -971,7 +977,7 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A) {
           (A.out_done + o)[l] = done;
         }
       }
-      ops += GEN ? 1u : 5u;  // the ring store (+ the four output stores)
+      ops += (GEN || (INL && A.no_task_out)) ? 1u : 5u;  // the ring store (+ the four output stores)
       TMARK(5)
 
       // 6) node k's state after the run
@@ -1067,10 +1073,10 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A) {
 #endif
   }
 #if !defined(FOGNET_REPLAY_PROFILE) || FOGNET_REPLAY_PROFILE == 0
-  if constexpr (GEN) {
+  if constexpr (INL) {
     if (A.out_stats && err != kNeedsWide) {
       // busy seconds, per-node service (energy) and `last` from the node
-      // tails (exact: the host admits T * max service < 2^32), the rest from
+      // tails (exact: the host takes this path only while T * max service < 2^32), the rest from
       // the loop's accumulators
       unsigned long long* e_busy = reinterpret_cast<unsigned long long*>(s_tld);  // [NPL*64] u64
       double* e_e = reinterpret_cast<double*>(s_ul);                              // [NPL*64] f64
@@ -1085,7 +1091,7 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A) {
       __syncthreads();
       fognet_rep_stats* S = A.out_stats + r;
       if (lane == 0) write_rep_stats(S, gacc);
-      stats_finish(A, r, n_done > 0 ? gacc.last : 0, S, e_busy, e_e, s_ch, lane, kWave);
+      stats_finish(A, r, n_done > 0 ? gacc.last : 0, S, e_busy, e_e, s_hs, lane, kWave);
     }
   } else if (A.fuse_stats && A.out_stats && err != kNeedsWide) {
     // ---- statistics epilogue (rep_stats_kernel's pass, fused).  The wave
@@ -1136,15 +1142,34 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A) {
 // the last 512 replications then run as a second, mostly idle round.)
 template <int NPL, int POL>
 __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))) void replay_kernel(ReplayArgs A) {
-  replay_body<NPL, POL, false>(A);
+  replay_body<NPL, POL, false, false>(A, blockIdx.x, blockIdx.x);
+}
+
+// Statistics in the loop (ReplayArgs::inloop): 3 waves per SIMD like the
+// generated mode, the trace and outputs as replay_kernel's.
+template <int NPL, int POL>
+__global__ __launch_bounds__(64, 3) __attribute__((amdgpu_num_vgpr(kNhBaseGen / 2))) void replay_inl_kernel(
+    ReplayArgs A) {
+  replay_body<NPL, POL, false, true>(A, blockIdx.x, blockIdx.x);
 }
 
 // Generated mode: 3 waves per SIMD (168 VGPRs: the statistics accumulators stay
-// in registers through the loop), prefetch registers v152..v167.
+// in registers through the loop), prefetch registers v152..v167.  A grid of
+// at most the resident workgroups takes the replications from a work
+// counter (A.queue, zeroed before the launch), so the rings are per workgroup
+// and a million-replication job is one launch without a tail per block; every
+// workgroup leaves once the counter has passed R.
 template <int NPL, int POL>
 __global__ __launch_bounds__(64, 3) __attribute__((amdgpu_num_vgpr(kNhBaseGen / 2))) void replay_gen_kernel(
     ReplayArgs A) {
-  replay_body<NPL, POL, true>(A);
+  for (;;) {
+    int next = 0;
+    if (threadIdx.x == 0) next = atomicAdd(A.queue, 1);
+    const int r = __builtin_amdgcn_readlane(next, 0);
+    if (r >= A.R) break;
+    replay_body<NPL, POL, true, true>(A, r, blockIdx.x);
+    __syncthreads();  // LDS reuse by the next replication
+  }
 }
 
 constexpr int kStatThreads = 256;
@@ -1183,12 +1208,22 @@ template <int POL>
 void launch_replay_pol(const ReplayArgs& a, hipStream_t s) {
   const int npl = (a.N + kWave - 1) / kWave;
   if (a.gen_on) {
+    const dim3 grid(a.R < a.gen_slots ? a.R : a.gen_slots);
     if (npl <= 1)
-      hipLaunchKernelGGL((replay_gen_kernel<1, POL>), dim3(a.R), dim3(kWave), 0, s, a);
+      hipLaunchKernelGGL((replay_gen_kernel<1, POL>), grid, dim3(kWave), 0, s, a);
     else if (npl == 2)
-      hipLaunchKernelGGL((replay_gen_kernel<2, POL>), dim3(a.R), dim3(kWave), 0, s, a);
+      hipLaunchKernelGGL((replay_gen_kernel<2, POL>), grid, dim3(kWave), 0, s, a);
     else
-      hipLaunchKernelGGL((replay_gen_kernel<4, POL>), dim3(a.R), dim3(kWave), 0, s, a);
+      hipLaunchKernelGGL((replay_gen_kernel<4, POL>), grid, dim3(kWave), 0, s, a);
+    return;
+  }
+  if (a.inloop) {
+    if (npl <= 1)
+      hipLaunchKernelGGL((replay_inl_kernel<1, POL>), dim3(a.R), dim3(kWave), 0, s, a);
+    else if (npl == 2)
+      hipLaunchKernelGGL((replay_inl_kernel<2, POL>), dim3(a.R), dim3(kWave), 0, s, a);
+    else
+      hipLaunchKernelGGL((replay_inl_kernel<4, POL>), dim3(a.R), dim3(kWave), 0, s, a);
     return;
   }
   if (npl <= 1) {

@@ -129,12 +129,14 @@ __device__ __forceinline__ void job_merge(fognet_job_stats& a, const fognet_job_
   add192(a.resp_sq, b.resp_sq[0], b.resp_sq[1], b.resp_sq[2]);
 }
 
-__global__ __launch_bounds__(kRedThreads) void reduce_kernel(const fognet_rep_stats* st, int32_t R,
+// Block b reduces records [b * chunk, min(R, (b + 1) * chunk)) into out[b].
+__global__ __launch_bounds__(kRedThreads) void reduce_kernel(const fognet_rep_stats* st, int32_t R, int32_t chunk,
                                                              fognet_job_stats* out) {
   __shared__ fognet_job_stats sh[kRedThreads];
   fognet_job_stats a;
   job_init(a);
-  for (int r = threadIdx.x; r < R; r += kRedThreads) {
+  const int r0 = blockIdx.x * chunk, r1 = min(R, r0 + chunk);
+  for (int r = r0 + threadIdx.x; r < r1; r += kRedThreads) {
     const fognet_rep_stats& s = st[r];
     a.n_reps += 1;
     if (s.status != FOGNET_OK) {
@@ -166,6 +168,22 @@ __global__ __launch_bounds__(kRedThreads) void reduce_kernel(const fognet_rep_st
     if ((int)threadIdx.x < w) job_merge(sh[threadIdx.x], sh[threadIdx.x + w]);
     __syncthreads();
   }
+  if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
+}
+
+// Merge of n partial job records (the blocks of reduce_kernel), in the same tree shape.
+__global__ __launch_bounds__(kRedThreads) void merge_jobs_kernel(const fognet_job_stats* parts, int32_t n,
+                                                                 fognet_job_stats* out) {
+  __shared__ fognet_job_stats sh[kRedThreads];
+  fognet_job_stats a;
+  job_init(a);
+  for (int i = threadIdx.x; i < n; i += kRedThreads) job_merge(a, parts[i]);
+  sh[threadIdx.x] = a;
+  __syncthreads();
+  for (int w = kRedThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) job_merge(sh[threadIdx.x], sh[threadIdx.x + w]);
+    __syncthreads();
+  }
   if (threadIdx.x == 0) *out = sh[0];
 }
 
@@ -179,8 +197,17 @@ hipError_t launch_gen_trace(const fognet_gen_params& p, int64_t r0, int32_t R, i
   return hipGetLastError();
 }
 
-hipError_t launch_reduce_stats(const fognet_rep_stats* st, int32_t R, fognet_job_stats* out, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kRedThreads), 0, s, st, R, out);
+int32_t reduce_stats_parts(int32_t R) { return R <= kReduceChunk ? 0 : (R + kReduceChunk - 1) / kReduceChunk; }
+
+hipError_t launch_reduce_stats(const fognet_rep_stats* st, int32_t R, fognet_job_stats* out, fognet_job_stats* parts,
+                               hipStream_t s) {
+  const int32_t np = reduce_stats_parts(R);
+  if (np == 0) {  // one block (up to kReduceChunk records)
+    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kRedThreads), 0, s, st, R, R, out);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(reduce_kernel, dim3(np), dim3(kRedThreads), 0, s, st, R, kReduceChunk, parts);
+  hipLaunchKernelGGL(merge_jobs_kernel, dim3(1), dim3(kRedThreads), 0, s, parts, np, out);
   return hipGetLastError();
 }
 

@@ -349,6 +349,25 @@ def test_reduce_stats_exact(ctx):
     assert fa.merge_job_stats(halves).tobytes() == job.tobytes()
 
 
+def test_reduce_stats_multi_block(ctx):
+    """Above 4,096 records the job reduction runs in blocks plus a merge
+    (generated replays: C4's million-replication launches); the integer
+    fields equal the exact host reduction."""
+    R, T, N = 9000, 64, 8
+    mg, sc = fa.sweep_params(np.arange(R), N)
+    out = fa.run_generated(ctx, 7, R, T, N, mg, sc, hist=False)
+    job = fa.reduce_stats(ctx, out.stats, R)
+    st = out.rep_stats()
+    ref = job_from_reps(st)
+    u192 = lambda a: int(a[0]) | (int(a[1]) << 64) | (int(a[2]) << 128)
+    assert int(job["n_reps"]) == R and int(job["n_failed"]) == 0 == ref["n_failed"]
+    assert int(job["n_tasks"]) == ref["n_tasks"] == R * T and int(job["n_queued"]) == ref["n_queued"]
+    assert u192(job["queue_sum"]) == ref["queue_sum"] and u192(job["queue_sq"]) == ref["queue_sq"]
+    assert u192(job["resp_sq"]) == ref["resp_sq"]
+    assert int(job["resp_max_ticks"]) == ref["resp_max"] and int(job["max_pending"]) == ref["max_pending"]
+    assert int(job["n_qtime"]) == int(st["n_qtime"].sum())
+
+
 def test_full_size_sweep_properties(ctx):
     """C3 shape at reduced R: R=256 x T=100k x N=256, checked through
     size-independent properties on the device (FIFO recurrence per node,

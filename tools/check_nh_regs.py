@@ -1,6 +1,6 @@
 """Audit the replay kernel ISA: the reserved registers that receive the
 inline-asm prefetch loads (v112..v127, kNhBase in replay.hip; v152..v167,
-kNhBaseGen, in the generated-mode replay_gen_kernel) must be referenced only by inline asm (the prefetch loads and the wait+copy reads),
+kNhBaseGen, in replay_gen_kernel and replay_inl_kernel) must be referenced only by inline asm (the prefetch loads and the wait+copy reads),
 anywhere in the kernel.  Usage: python tools/check_nh_regs.py build/asm/replay-...-gfx950.s"""
 import re
 import sys
@@ -17,7 +17,8 @@ def regs_of(s):
 
 def audit(path):
     return (audit_one(path, "_ZN6fognet12_GLOBAL__N_113replay_kernelILi", 112)
-            + audit_one(path, "_ZN6fognet12_GLOBAL__N_117replay_gen_kernelILi", 152))
+            + audit_one(path, "_ZN6fognet12_GLOBAL__N_117replay_gen_kernelILi", 152)
+            + audit_one(path, "_ZN6fognet12_GLOBAL__N_117replay_inl_kernelILi", 152))
 
 
 def audit_one(path, kernel_prefix, base):
@@ -59,7 +60,7 @@ def audit_one(path, kernel_prefix, base):
                 continue
             if not in_asm and regs_of(ln) & nh:
                 bad.append(ln)
-        print(f"{'replay_gen_kernel' if 'gen' in kernel_prefix else 'replay_kernel'} NPL={npl} policy={pol}: prefetch registers {sorted(nh)}; compiler references outside asm: {len(bad)}")
+        print(f"{kernel_prefix[26:-3]} NPL={npl} policy={pol}: prefetch registers {sorted(nh)}; compiler references outside asm: {len(bad)}")
         for b in bad[:20]:
             print("   ", b)
         bad_total += len(bad)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # C4 (generated replay) counters: one PMC pass over one step of
-# `bench.py --workload c4` (8 blocks of 16,384 replications), summarised into
+# `bench.py --workload c4` (1,000,000 replications, one launch), summarised into
 # gpurun_out/pmc_c4/pmc_valu_c4.json (VALU busy, instructions per decision),
 # the record bench.py's C4 line reads from profiles/.
 set -o pipefail
@@ -9,19 +9,19 @@ rm -rf gpurun_out/pmc_c4; mkdir -p gpurun_out/pmc_c4
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
   --output-format csv -d gpurun_out/pmc_c4/p1 -o p1 -- \
-  python3 bench.py --workload c4 --R-total 131072 --steps 1 --warmup 0 --no-cpu > gpurun_out/pmc_c4/p1.log 2>&1 || exit 1
+  python3 bench.py --workload c4 --steps 1 --warmup 0 --no-cpu > gpurun_out/pmc_c4/p1.log 2>&1 || exit 1
 python3 - <<'PY'
 import json, sys
 sys.path.insert(0, "tools")
 import pmc_summary
 d = pmc_summary.load("gpurun_out/pmc_c4", kernel="replay_gen_kernel")
 per = {k: v / n for k, (v, n) in d.items()}
-dec = 16384 * 10000
+dec = 1000000 * 10000
 out = {"kernel": "replay_gen_kernel", "per_dispatch": per,
        "valu_busy": per["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (per["GRBM_GUI_ACTIVE"] / 8),
        "SQ_INSTS_VALU_per_decision": per["SQ_INSTS_VALU"] / dec, "SQ_INSTS_SALU_per_decision": per["SQ_INSTS_SALU"] / dec,
        "dispatches": d["SQ_INSTS_VALU"][1],
-       "config": {"T": 10000, "N": 256, "block": 16384, "ring": 2048, "policy": "REF_V3"},
+       "config": {"T": 10000, "N": 256, "block": 0, "ring": 2048, "policy": "REF_V3"},
        "note": "valu_busy = SQ_ACTIVE_INST_VALU*4/1024 SIMDs/(GRBM_GUI_ACTIVE/8 XCDs), rocprof's VALUBusy (gfx94x formula)"}
 json.dump(out, open("gpurun_out/pmc_c4/pmc_valu_c4.json", "w"), indent=1)
 print(json.dumps({k: out[k] for k in ("valu_busy", "SQ_INSTS_VALU_per_decision", "dispatches")}))
