@@ -552,6 +552,31 @@ def test_generated_equals_materialized(ctx, monkeypatch, kind):
         assert torch.equal(gen.node_energy, full.node_energy)
 
 
+@pytest.mark.parametrize("N,T,ring", [(7, 1500, 0), (64, 3000, 0), (130, 2111, 0), (256, 3000, 0), (64, 3000, 4)])
+def test_inloop_statistics_equal_epilogue(ctx, monkeypatch, N, T, ring):
+    """FOGNET_REPLAY_STATS=inloop (replay_inl_kernel: statistics accumulated
+    while the runs are pushed) writes the outputs, records, histograms and
+    energy of the default fused epilogue, with per-task outputs and without."""
+    tr = tg.make_batch(51 + N, 5, N, T, sweep=True)
+    pb, pi = fa.power_model(tr["mips"])
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(dict(tr, p_busy=pb, p_idle=pi), dev)
+    R = tr["arrive"].shape[0]
+    ref = fa.run_batch(ctx, d, ring_capacity=ring, hist=True)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("FOGNET_REPLAY_STATS", "inloop")
+    inl = fa.run_batch(ctx, d, ring_capacity=ring, hist=True)
+    so = fa.allocate_outputs(R, T, dev, N=N, energy=True, hist=True, per_task=False)
+    fa.run_batch(ctx, d, out=so, ring_capacity=ring)
+    torch.cuda.synchronize()
+    assert (ref.rep_stats()["status"] == 0).all()
+    for k in ("node", "status", "start_tick", "done_tick"):
+        assert torch.equal(getattr(inl, k), getattr(ref, k)), k
+    for o in (inl, so):
+        assert o.rep_stats().tobytes() == ref.rep_stats().tobytes()
+        assert torch.equal(o.hist, ref.hist) and torch.equal(o.node_energy, ref.node_energy)
+
+
 def test_generated_preconditions(ctx):
     """fognet_run_generated_dev refuses what it cannot replay exactly."""
     mg, sc = fa.sweep_params(np.arange(2), 8)
