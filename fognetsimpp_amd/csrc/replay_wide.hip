@@ -650,6 +650,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 template <int POL>
 void launch_wide_pol(const ReplayArgs& a, int32_t slots, WideEntry* e, WideNode* nd, int64_t* vn, uint32_t* vb,
                      GenNodes gn, size_t lds, hipStream_t s) {
+  if (lds > 65536)  // above the default dynamic-LDS limit (N > ~51,000 nodes; gfx950 has 160 KiB per CU)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&replay_wide_kernel<POL>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb, gn);
 }
 

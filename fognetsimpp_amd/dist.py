@@ -5,8 +5,11 @@ the global replication index; each rank generates and replays its own block
 (trace keys depend on the global index only, so results do not depend on the
 number of GPUs).  The only collective is one all-gather of the per-rank
 ``fognet_job_stats`` record, merged with exact integer arithmetic
-(``fognet_job_stats_merge``), so the job statistics are bit-identical for any
-sharding.  Works with the ``nccl`` (RCCL) backend on device tensors and with
+(``fognet_job_stats_merge``), so the integer job statistics (counts, 192-bit
+moments, minima/maxima, histograms) are bit-identical for any sharding.  The
+builder-defined energy ``energy_j`` is an fp64 sum whose rounding depends on
+the sharding and the merge order: equal within 1e-9 relative, not bitwise
+(include/fognet_hip.h).  Works with the ``nccl`` (RCCL) backend on device tensors and with
 ``gloo`` on CPU tensors.
 """
 from __future__ import annotations
@@ -36,8 +39,9 @@ def job_record_tensor(job, device) -> torch.Tensor:
 
 def allgather_job_stats(job_bytes: torch.Tensor, group=None) -> np.ndarray:
     """All-gather each rank's job record (uint8 tensor of one JOB_STATS_DTYPE)
-    and return the exact merge over ranks (rank order; the merge is
-    associative, so any order gives the same record)."""
+    and return the merge over ranks in rank order (the integer fields' merge
+    is associative, so any order gives the same values; energy_j is an fp64
+    sum taken in rank order)."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)

@@ -699,7 +699,8 @@ def test_ext_lat_latency_bound(ctx):
 # completion advert lands, so the C3 loads (rho 0.5..0.95) keep 10^3-10^4 nodes
 # on node 0 for the whole trace; light loads spread decisions over many nodes.
 @pytest.mark.parametrize("N,T,R,rho", [(257, 2000, 3, 0.8), (700, 3000, 3, 0.01), (4096, 4000, 2, 0.01),
-                                       (12288, 3000, 1, 0.002), (20000, 1500, 1, 0.001)])
+                                       (12288, 3000, 1, 0.002), (20000, 1500, 1, 0.001),
+                                       (65536, 1200, 1, 0.0005)])  # the advertised limit (82 KiB of LDS)
 def test_wide_matches_oracle(ctx, N, T, R, rho):
     tr = tg.make_batch(0x5EED0005 + N, R, N, T, rho=rho, lat_scale=10)
     pb, pi = fa.power_model(tr["mips"])

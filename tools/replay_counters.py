@@ -62,6 +62,13 @@ def main():
             row["decisions_per_iteration"] = float(dec / st["n_queued"][m].sum())
         key = "all" if c < 0 else f"rho={(0.5, 0.8, 0.95)[c % 3]} lat_x{(1, 10, 100)[c // 3]}"
         res[key] = row
+    if MODE == "time":  # per-replication wall cycles: the spread that sets the launch's tail
+        tot = st["queue_sum_hi"].astype(np.float64)
+        res["per_rep_total_cycles"] = {
+            "min": float(tot.min()), "p50": float(np.median(tot)), "p90": float(np.percentile(tot, 90)),
+            "max": float(tot.max()), "mean": float(tot.mean()),
+            "by_class_mean": [float(tot[cls == c].mean()) for c in range(9)],
+            "by_class_max": [float(tot[cls == c].max()) for c in range(9)]}
     txt = json.dumps(res, indent=1)
     print(txt)
     if a.out:
