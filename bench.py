@@ -213,12 +213,14 @@ def main():
     achieved_gbs = R * T * bpd / replay_avg_s / 1e9
 
     traffic = None
-    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json" if args.workload == "c3" else
-                        f"pmc_traffic_{args.workload}.json")
+    default_policy = "EXT_HIER" if args.workload == "c5" else "REF_V3"
+    prof = os.path.join(ROOT, "profiles", ("pmc_traffic" if args.workload == "c3" else f"pmc_traffic_{args.workload}")
+                        + ("" if args.policy == default_policy else f"_{args.policy}") + ".json")
     if os.path.exists(prof):
         try:
             pj = json.load(open(prof))
-            if pj.get("config") == {"R": R, "T": T, "N": N, "ring": args.ring}:
+            if pj.get("config") == {"R": R, "T": T, "N": N, "ring": args.ring} and \
+                    pj.get("policy", "REF_V3" if args.workload == "c3" else "EXT_HIER") == args.policy:
                 traffic = pj.get("replay_hbm_bytes_per_launch")
         except Exception:
             traffic = None

@@ -72,61 +72,80 @@ __host__ __device__ __forceinline__ int wide_groups(int N) {
   return ((N + kWave - 1) / kWave + kWideGroupSlots - 1) / kWideGroupSlots;
 }
 
-// Load group g of this lane's view (issued before the advert that changes
-// one of its slots, so these loads overlap the node-record load instead of
-// queueing behind the advert's stores: gfx9's vmcnt counts both).
-__device__ __forceinline__ void group_load(const WideView& V, int g, int64_t (&x)[kWideGroupSlots],
-                                           uint32_t (&b)[kWideGroupSlots]) {
+// Load the next-advert ticks of group g of this lane's view (issued before
+// the advert that changes one of its slots, so these loads overlap the
+// node-record load instead of queueing behind the advert's stores: gfx9's
+// vmcnt counts both).
+__device__ __forceinline__ void group_load(const WideView& V, int g, int64_t (&x)[kWideGroupSlots]) {
 #pragma unroll
-  for (int i = 0; i < kWideGroupSlots; ++i) {
-    x[i] = V.nxt[g * kWideGroupSlots + i];
-    b[i] = V.busy[g * kWideGroupSlots + i];
-  }
+  for (int i = 0; i < kWideGroupSlots; ++i) x[i] = V.nxt[g * kWideGroupSlots + i];
 }
 
-// Rescan group g of this lane from its loaded view (slot `sl` replaced by the
-// values just computed: its load was issued before their store).
-__device__ __forceinline__ void group_scan(const WideLds& L, int N, int lane, int g, int sl, int64_t sl_nxt,
-                                           uint32_t sl_busy, const int64_t (&x)[kWideGroupSlots],
-                                           const uint32_t (&b)[kWideGroupSlots]) {
+// Earliest advert of group g of this lane from its loaded ticks (slot `sl`
+// replaced by the value just computed: its load was issued before the store).
+// Slots past N hold kNever, so they need no test.
+__device__ __forceinline__ void group_scan_nxt(const WideLds& L, int lane, int g, int sl, int64_t sl_nxt,
+                                               const int64_t (&x)[kWideGroupSlots]) {
   int64_t mn = kNever;
   int mj = lane;
-  uint64_t mk = ~0ull;
 #pragma unroll
   for (int i = 0; i < kWideGroupSlots; ++i) {
     const int s = g * kWideGroupSlots + i;
-    const int j = s * kWave + lane;
-    if (j < N) {
-      const int64_t xi = s == sl ? sl_nxt : x[i];
-      if (xi < mn) {
-        mn = xi;
-        mj = j;
-      }
-      const uint64_t key = ((uint64_t)(s == sl ? sl_busy : b[i]) << 32) | (uint32_t)j;
-      mk = key < mk ? key : mk;
+    const int64_t xi = s == sl ? sl_nxt : x[i];
+    if (xi < mn) {
+      mn = xi;
+      mj = s * kWave + lane;
     }
   }
   L.g_nxt[g * kWave + lane] = mn;
   L.g_j[g * kWave + lane] = mj;
-  L.g_key[g * kWave + lane] = mk;
 }
 
-// The lane's minima over its groups (earliest advert: first group on ties).
-__device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn, int& mj, uint64_t& mk) {
+// Smallest view key (busy << 32 | node) of group g of this lane, from HBM
+// (slot sl's busy just stored by this lane).  Slots past N hold busy
+// 0xFFFFFFFF, above every admissible advertised busy time.
+__device__ __forceinline__ uint64_t group_key(const WideView& V, int lane, int g) {
+  uint32_t b[kWideGroupSlots];
+#pragma unroll
+  for (int i = 0; i < kWideGroupSlots; ++i) b[i] = V.busy[g * kWideGroupSlots + i];
+  uint64_t mk = ~0ull;
+#pragma unroll
+  for (int i = 0; i < kWideGroupSlots; ++i) {
+    const uint64_t key = ((uint64_t)b[i] << 32) | (uint32_t)((g * kWideGroupSlots + i) * kWave + lane);
+    mk = key < mk ? key : mk;
+  }
+  return mk;
+}
+
+// The lane's earliest advert over its groups (first group on ties).
+__device__ __forceinline__ void lane_min_nxt(const WideLds& L, int lane, int64_t& mn, int& mj) {
   mn = kNever;
   mj = lane;
-  mk = ~0ull;
 #pragma unroll 4
   for (int g = 0; g < L.G; ++g) {
     const int64_t x = L.g_nxt[g * kWave + lane];
     const int jj = L.g_j[g * kWave + lane];
-    const uint64_t key = L.g_key[g * kWave + lane];
     if (x < mn) {
       mn = x;
       mj = jj;
     }
+  }
+}
+
+// The lane's smallest view key over its groups.
+__device__ __forceinline__ uint64_t lane_min_key(const WideLds& L, int lane) {
+  uint64_t mk = ~0ull;
+#pragma unroll 4
+  for (int g = 0; g < L.G; ++g) {
+    const uint64_t key = L.g_key[g * kWave + lane];
     mk = key < mk ? key : mk;
   }
+  return mk;
+}
+
+__device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn, int& mj, uint64_t& mk) {
+  lane_min_nxt(L, lane, mn, mj);
+  mk = lane_min_key(L, lane);
 }
 
 // The advert of node j's head completion reaches the broker (owner lane):
@@ -288,9 +307,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     if constexpr (kExt) bad |= d >= kExtMaxDl;
     nd[j] = WideNode{-1, -1, 0, -1, 0, 0u, 0, 0, 0u, 0u, 0u};
   }
-  for (int s = 0; s < SP; ++s) {  // slots past N too (group rescans read them)
+  for (int s = 0; s < SP; ++s) {  // slots past N too (group rescans read them): never due, never chosen
     V.nxt[s] = kNever;
-    V.busy[s] = 0u;
+    V.busy[s] = s * kWave + lane < N ? 0u : 0xFFFFFFFFu;
   }
   for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) L.hist[h] = 0u;
   for (int g = 0; g < L.G; ++g) {  // the initial view: nothing pending, every busy 0
@@ -365,8 +384,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           const bool hit = j == cj;
           const int g = sl / kWideGroupSlots;
           int64_t gx[kWideGroupSlots];
-          uint32_t gb[kWideGroupSlots];
-          group_load(V, g, gx, gb);
+          group_load(V, g, gx);
           WideNode h = hit ? ch : nd[j];
           lerr |= !apply_advert(h, e, hit ? c_dl : P_dl[j], hit ? c_ul : P_ul[j], kHier ? A.hier_up : 0,
                                 nxt_j, busy_j);
@@ -374,8 +392,18 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           else nd[j] = h;
           V.nxt[sl] = nxt_j;
           V.busy[sl] = busy_j;
-          group_scan(L, N, lane, g, sl, nxt_j, busy_j, gx, gb);
-          lane_min(L, lane, mn, mj, mk);
+          // the earliest advert: j's was the lane's (so its group's), rescan both levels
+          group_scan_nxt(L, lane, g, sl, nxt_j, gx);
+          lane_min_nxt(L, lane, mn, mj);
+          // the view key: only j's changed; the group (and lane) minimum needs a rescan only
+          // when j held it and its busy time grew
+          const uint64_t gk_old = L.g_key[g * kWave + lane];
+          const uint64_t nk = ((uint64_t)busy_j << 32) | (uint32_t)j;
+          const uint64_t gk_new = ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? group_key(V, lane, g)
+                                                                                 : (nk < gk_old ? nk : gk_old);
+          L.g_key[g * kWave + lane] = gk_new;
+          if (gk_new < mk) mk = gk_new;
+          else if (mk == gk_old && gk_new > gk_old) mk = lane_min_key(L, lane);
         }
       }
       if (ballot(lerr)) {

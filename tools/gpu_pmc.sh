@@ -6,9 +6,11 @@
 # outputs + trace) with the element widths the replay's own loads use.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/pmc
+rm -rf gpurun_out/pmc; mkdir -p gpurun_out/pmc
 if [ "${WORKLOAD:-c3}" = c5 ]; then
-  BARGS="--workload c5"; KERNEL=replay_wide_kernel; DEC=10240000; OUT=pmc_traffic_c5.json; CFG=1024,10000,10000
+  # POLICY=REF_V3: the flat broker (pmc_traffic_c5_REF_V3.json); default EXT_HIER (pmc_traffic_c5.json)
+  BARGS="--workload c5 --policy ${POLICY:-EXT_HIER}"; KERNEL=replay_wide_kernel; DEC=10240000; CFG=1024,10000,10000
+  OUT=pmc_traffic_c5$([ "${POLICY:-EXT_HIER}" = EXT_HIER ] || echo _${POLICY}).json
 else
   BARGS=""; KERNEL=replay_kernel; DEC=409600000; OUT=pmc_traffic.json; CFG=4096,100000,256
 fi
@@ -23,7 +25,7 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_W
   echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/p$i.log; exit $rc; fi
 done
-python3 tools/pmc_summary.py $KERNEL $DEC gpurun_out/pmc/$OUT 2048 $CFG > /dev/null || exit 1
+python3 tools/pmc_summary.py $KERNEL $DEC gpurun_out/pmc/$OUT 2048 $CFG ${POLICY:-$([ "${WORKLOAD:-c3}" = c5 ] && echo EXT_HIER || echo REF_V3)} > /dev/null || exit 1
 if [ "${WORKLOAD:-c3}" = c3 ]; then
   for grp in "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))

@@ -49,6 +49,7 @@ def main():
     if "hbm_bytes_per_launch" in out:
         R, T, N = (int(x) for x in sys.argv[5].split(",")) if len(sys.argv) > 5 else (4096, 100000, 256)
         out["config"] = {"R": R, "T": T, "N": N, "ring": int(sys.argv[4]) if len(sys.argv) > 4 else 2048}
+        out["policy"] = sys.argv[6] if len(sys.argv) > 6 else "REF_V3"
         out["replay_hbm_bytes_per_launch"] = out["hbm_bytes_per_launch"]
     txt = json.dumps(out, indent=1)
     print(txt)
