@@ -196,7 +196,7 @@ __device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, in
 
 // Workspace layout (launch_replay_wide, replay_wide_workspace_bytes).
 struct WideWs {
-  size_t e_off, nd_off, nxt_off, busy_off, gm_off, gd_off, gu_off, bytes;
+  size_t e_off, nd_off, nxt_off, busy_off, dv_off, gm_off, gd_off, gu_off, bytes;
 };
 
 __host__ __device__ __forceinline__ size_t align64(size_t x) { return (x + 63) & ~(size_t)63; }
@@ -209,7 +209,8 @@ __host__ __device__ __forceinline__ WideWs wide_ws(int32_t R, int32_t T, int32_t
   w.nd_off = align64(w.e_off + (size_t)R * (size_t)T * sizeof(WideEntry));
   w.nxt_off = align64(w.nd_off + (size_t)R * (size_t)N * sizeof(WideNode));
   w.busy_off = align64(w.nxt_off + (size_t)R * kWave * SP * sizeof(int64_t));
-  w.gm_off = align64(w.busy_off + (size_t)R * kWave * SP * sizeof(uint32_t));
+  w.dv_off = align64(w.busy_off + (size_t)R * kWave * SP * sizeof(uint32_t));
+  w.gm_off = align64(w.dv_off + (size_t)R * (size_t)N * sizeof(uint64_t));
   const size_t RN = gen ? (size_t)R * (size_t)N : 0;
   w.gd_off = align64(w.gm_off + RN * sizeof(int32_t));
   w.gu_off = align64(w.gd_off + RN * sizeof(int64_t));
@@ -222,6 +223,7 @@ struct GenNodes {
   int32_t* m;
   int64_t* d;
   int64_t* u;
+  uint64_t* dv;
 };
 
 template <int POL>
@@ -306,6 +308,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     bad |= dn != kNever && (dn < ia || dn > kMaxTick);
     if constexpr (kExt) bad |= d >= kExtMaxDl;
     nd[j] = WideNode{-1, -1, 0, -1, 0, 0u, 0, 0, 0u, 0u, 0u};
+    const UDiv dv = udiv_magic((uint32_t)(m > 0 ? m : 1));
+    GN.dv[sbase + j] = (uint64_t)dv.m | ((uint64_t)dv.sh << 32);
   }
   for (int s = 0; s < SP; ++s) {  // slots past N too (group rescans read them): never due, never chosen
     V.nxt[s] = kNever;
@@ -338,6 +342,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   int cj = -1;
   WideNode ch{};
   int32_t c_mips = 1;
+  uint64_t c_dv = 1ull;
   int64_t c_dl = 0, c_ul = 0, c_down = kNever;
 
   // the decision is recomputed only after an advert changed the view
@@ -466,11 +471,13 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         cj = (int)k;
         ch = nd[k];
         c_mips = P_mips[k];
+        c_dv = GN.dv[sbase + k];
         c_dl = P_dl[k];
         c_ul = P_ul[k];
         c_down = A.down ? A.down[nbase + k] : kNever;
       }
       const int32_t mips_k = (int32_t)readlane_u32((uint32_t)c_mips, kl);
+      const UDiv div_k{readlane_u32((uint32_t)c_dv, kl), readlane_u32((uint32_t)(c_dv >> 32), kl)};
       // (an escalated task takes the regional -> parent hop before the downlink)
       const int64_t dl_k = readlane_i64(c_dl, kl) + (escalated ? A.hier_up : 0);
       const int64_t ul_k = readlane_i64(c_ul, kl), down_k = readlane_i64(c_down, kl);
@@ -512,7 +519,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       int64_t a = 0;
       bool lerr2 = false;
       if (in_run) {
-        S = (uint32_t)cr / (uint32_t)mips_k;  // double tskTime = requiredMIPS / MIPS (:276)
+        S = udiv((uint32_t)cr, div_k);  // double tskTime = requiredMIPS / MIPS (:276)
         a = ca + dl_k;
       }
       const uint32_t Sd = min(S, kWideMaxS);  // (a larger service time is an error unless the task is lost)
@@ -702,7 +709,7 @@ hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slot
   int64_t* const vn = reinterpret_cast<int64_t*>(base + w.nxt_off);
   uint32_t* const vb = reinterpret_cast<uint32_t*>(base + w.busy_off);
   const GenNodes gn{reinterpret_cast<int32_t*>(base + w.gm_off), reinterpret_cast<int64_t*>(base + w.gd_off),
-                    reinterpret_cast<int64_t*>(base + w.gu_off)};
+                    reinterpret_cast<int64_t*>(base + w.gu_off), reinterpret_cast<uint64_t*>(base + w.dv_off)};
   const size_t lds = replay_wide_lds_bytes(a.N);
   if (a.policy == FOGNET_POLICY_EXT_LAT)
     launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, slots, e, nd, vn, vb, gn, lds, s);
