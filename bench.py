@@ -536,8 +536,9 @@ def cpu_baseline(trace, args, R, T, N, out=None):
     del o
     s1 = min(max(16, args.cpu_reps_1t), reps)
     t1 = time.perf_counter()
+    pw1 = {k: (v[:s1] if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == reps else v) for k, v in pw.items()}
     oracle_lib.run_batch(h["arrive"][:s1], h["req"][:s1], h["mips"][:s1], h["dl"][:s1], h["ul"][:s1], h["init"][:s1],
-                         threads=1, outputs=False)
+                         threads=1, outputs=False, **pw1)  # the same policy, power model and regions
     dt1 = time.perf_counter() - t1
     return {"value": reps * T / dt, "unit": "decisions/s", "cores": threads, "kind": "port",
             "sample": f"{reps} replications x {T} tasks x {N} nodes (rank 0's first replications of the same "
