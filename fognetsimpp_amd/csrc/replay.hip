@@ -905,29 +905,38 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
       Cs = scan_add_level<0x118, 0xF>(Cs);  // row_shr:8
       Cs = scan_add_level<0x142, 0xA>(Cs);  // row_bcast:15
       Cs = scan_add_level<0x143, 0xC>(Cs);  // row_bcast:31
-      int64_t X = in_run ? (int64_t)((uint64_t)a - (uint64_t)ticks_of(Cs - S)) : INT64_MIN;
-      int64_t xt = INT64_MIN;
-      X = scan_max_level<0x111, 0xF>(X, xt);
-      X = scan_max_level<0x112, 0xF>(X, xt);
-      X = scan_max_level<0x114, 0xF>(X, xt);
-      X = scan_max_level<0x118, 0xF>(X, xt);
-      X = scan_max_level<0x142, 0xA>(X, xt);
-      X = scan_max_level<0x143, 0xC>(X, xt);
       const int64_t base_done = tld_k;  // INT64_MIN when k never ran a task
-      const int64_t dmax = base_done > X ? base_done : X;
-      const int64_t done = (int64_t)((uint64_t)dmax + (uint64_t)ticks_of(Cs));
-      // previous task on node k: the run's previous lane, or k's tail
-      const int64_t done_up = dpp_or_i64<kDppWaveShr1>(0, done);
-      const uint32_t S_up = dpp_or_u32<kDppWaveShr1>(0u, S);
-      const int64_t prev_done = lane == jp ? base_done : done_up;
-      const uint32_t prev_S = lane == jp ? tlS_k : S_up;
+      int64_t done;
       uint32_t status;
-      if (prev_done < a) {
-        status = 5u;  // idle: "task assigned" (:282-301)
-      } else if (prev_done > a) {
+      // Queued run (the common case under the stale view's herding): k is busy
+      // past the run's last arrival, so every task queues behind it and
+      // done_m = base_done + P_m; no prefix maximum, no status tests.
+      if (base_done > (int64_t)((uint64_t)readlane_i64(ca, jq - 1) + (uint64_t)dl_k)) {
+        done = (int64_t)((uint64_t)base_done + (uint64_t)ticks_of(Cs));
         status = 4u;  // busy: "task queued" (:304-313)
-      } else {        // completion of the previous task at the same tick
-        status = (dl_k < (int64_t)prev_S * kTicksPerSecond) ? 5u : 4u;
+      } else {
+        int64_t X = in_run ? (int64_t)((uint64_t)a - (uint64_t)ticks_of(Cs - S)) : INT64_MIN;
+        int64_t xt = INT64_MIN;
+        X = scan_max_level<0x111, 0xF>(X, xt);
+        X = scan_max_level<0x112, 0xF>(X, xt);
+        X = scan_max_level<0x114, 0xF>(X, xt);
+        X = scan_max_level<0x118, 0xF>(X, xt);
+        X = scan_max_level<0x142, 0xA>(X, xt);
+        X = scan_max_level<0x143, 0xC>(X, xt);
+        const int64_t dmax = base_done > X ? base_done : X;
+        done = (int64_t)((uint64_t)dmax + (uint64_t)ticks_of(Cs));
+        // previous task on node k: the run's previous lane, or k's tail
+        const int64_t done_up = dpp_or_i64<kDppWaveShr1>(0, done);
+        const uint32_t S_up = dpp_or_u32<kDppWaveShr1>(0u, S);
+        const int64_t prev_done = lane == jp ? base_done : done_up;
+        const uint32_t prev_S = lane == jp ? tlS_k : S_up;
+        if (prev_done < a) {
+          status = 5u;  // idle: "task assigned" (:282-301)
+        } else if (prev_done > a) {
+          status = 4u;  // busy: "task queued" (:304-313)
+        } else {        // completion of the previous task at the same tick
+          status = (dl_k < (int64_t)prev_S * kTicksPerSecond) ? 5u : 4u;
+        }
       }
       const int64_t start = done - dd;
       lerr = lerr || (in_run && done > kMaxTick);
