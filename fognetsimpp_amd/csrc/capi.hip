@@ -420,7 +420,8 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
     const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
     const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
-    const size_t head = align256(256 + (size_t)a.R * sizeof(int32_t));
+    const size_t o_board = align256(256 + (size_t)a.R * sizeof(int32_t));
+    const size_t head = o_board + fognet::kBoardWords * sizeof(uint32_t);
     const size_t body = ring_bytes > fb_bytes ? ring_bytes : fb_bytes;
     const size_t RT = stats_only && !a.inloop ? (size_t)a.R * (size_t)a.T : 0;
     const size_t o_node = head + align256(body), o_st = o_node + align256(RT * 4), o_start = o_st + align256(RT),
@@ -439,6 +440,11 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     }
     e = hipMemsetAsync(a.wide_count, 0, sizeof(int32_t), (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "hand-over counter");
+    if (!a.inloop) {  // replay_kernel's progress board: every slot empty
+      a.board = reinterpret_cast<uint32_t*>(base + o_board);
+      e = hipMemsetAsync(a.board, 0xFF, fognet::kBoardWords * sizeof(uint32_t), (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(c, e, "progress board");
+    }
     e = fognet::launch_replay(a, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "replay launch");
     // the handed-over replications (usually none: every workgroup leaves at once)

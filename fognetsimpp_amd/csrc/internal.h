@@ -249,7 +249,13 @@ struct ReplayArgs {
   int64_t gen_r0;
   fognet_gen_params gen;
   int32_t* queue;     // generated mode: work counter (zeroed before the launch)
+  // replay_kernel's progress board (kBoardWords u32, 0xFF-filled before the
+  // launch): one word per hardware wave slot (XCC, SE, SH, CU, SIMD, wave),
+  // the wave's replay progress, read by the other waves of its SIMD to set
+  // their issue priority (least progress first).  Nullable.
+  uint32_t* board;
 };
+constexpr size_t kBoardWords = (size_t)1 << 17;  // 8 XCC x 8 SE x 2 SH x 16 CU x 4 SIMD x 16 slots
 
 // Generated-mode launch: 3 waves per SIMD, 4 SIMDs per CU (replay_gen_kernel)
 constexpr int kGenWavesPerCu = 12;

@@ -259,6 +259,54 @@ __device__ __forceinline__ void refill_nh(int s, const Slot& st, const RingEntry
   }
 }
 
+// ---- issue priority: least replay progress first
+//
+// The four waves on a SIMD share its VALU, which issues by priority, then age
+// (MI355X_MICROARCH.md, "VALU issue is arbitrated ... by priority, then age").
+// At equal priority the oldest wave runs nearly unimpeded and the youngest
+// gets the leftover slots, so the SIMD's replications finish one after the
+// other and the last runs alone, latency-bound (the C3 tail: per-replication
+// time min/median/max 14.6/22.5/32.2 M cycles).  Each wave posts its progress
+// (fraction of the trace replayed, 2^20 = done) into its hardware slot of a
+// board in HBM every kPrioEvery chunks, reads its SIMD's 16 slots and takes
+// priority 3 - (number of co-resident waves with less progress), capped at 0:
+// the waves advance together and the SIMD stays busy to the end.  Only the
+// schedule changes, never a result.
+#ifndef FOGNET_PRIO
+#define FOGNET_PRIO 2
+#endif
+#ifndef FOGNET_PRIO_EVERY
+#define FOGNET_PRIO_EVERY 32
+#endif
+constexpr int kPrioEvery = FOGNET_PRIO_EVERY;  // chunks between board updates
+
+__device__ __forceinline__ void set_prio(uint32_t p) {
+  switch (p) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+  }
+}
+
+// This wave's board word: XCC (3 bits) | HW_ID CU/SH/SE (bits 8-15) | SIMD | wave slot.
+__device__ __forceinline__ uint32_t board_slot() {
+  uint32_t hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  return ((xcc & 7u) << 14) | (((hw >> 8) & 0xFFu) << 6) | (((hw >> 4) & 3u) << 4) | (hw & 15u);
+}
+
+// Post progress `my` (wave-uniform) and set the priority from the SIMD's slots.
+__device__ __forceinline__ void board_update(uint32_t* board, uint32_t slot, uint32_t my, int lane) {
+  if (lane == 0) __hip_atomic_store(board + slot, my, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t l = (uint32_t)lane & 15u;
+  const uint32_t v = __hip_atomic_load(board + (slot & ~15u) + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t behind = ballot(lane < 16 && l != (slot & 15u) && v < my);  // empty / finished slots hold ~0
+  const uint32_t n = (uint32_t)__popcll(behind);
+  set_prio(n >= 3u ? 0u : 3u - n);
+}
+
 // ---- trace chunk staging (LDS-DMA)
 //
 // The next 64 publishes {arrive lo, arrive hi, req} are copied global -> LDS
@@ -719,6 +767,14 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   // while the publishes stay within its horizon E_carry (argmin unchanged).
   bool carry = false;
   int64_t E_carry = 0;
+  // issue priority (replay_kernel only; see board_update)
+  constexpr bool kPrio = FOGNET_PRIO != 0 && !GEN && !INL;
+  uint32_t b_slot = 0u;
+  float b_scale = 0.0f;
+  if constexpr (kPrio) {
+    b_slot = board_slot();
+    b_scale = 1048576.0f / (float)(T > 0 ? T : 1);
+  }
 
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
@@ -734,6 +790,16 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
       cr = live ? (int32_t)s_ch[2 * kWave + l_ch] : 0;
     }
     PROF(p_chunks++;)
+    if constexpr (kPrio) {
+      if (((c0 >> 6) & (kPrioEvery - 1)) == 0) {
+        const uint32_t my = __builtin_amdgcn_readfirstlane((uint32_t)((float)c0 * b_scale));
+#if FOGNET_PRIO == 2
+        if (A.board) board_update(A.board, b_slot, my, lane);
+#else
+        set_prio(3u - min(my >> 18, 3u));  // quartile of the trace
+#endif
+      }
+    }
     TMARK(0)
     // trace preconditions: nondecreasing ticks, requirement >= 0, ticks < 2^61
     const int64_t prv = dpp_or_i64<kDppWaveShr1>(prev_t, ca);  // lane 0 gets prev_t
@@ -1034,6 +1100,9 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   }
   // drain the inline-asm prefetches before the wave retires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (kPrio && FOGNET_PRIO == 2) {  // this slot is free again
+    if (A.board && lane == 0) __hip_atomic_store(A.board + b_slot, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 
 #if FOGNET_REPLAY_PROFILE == 2
   TMARK(7)
