@@ -318,6 +318,11 @@ __device__ __forceinline__ void board_update(uint32_t* board, uint32_t slot, uin
 // instruction offset is added to the LDS address as well as to the global one
 // (LDS = M0 + inst_offset + 4*lane), so the high-dword copy sets
 // M0 = base + 0x100 - 4 and lands at base + 0x100 + 4*lane.
+#ifdef FOGNET_NT_TRACE
+#define FOGNET_TRACE_NT " nt"
+#else
+#define FOGNET_TRACE_NT ""
+#endif
 __device__ __forceinline__ void chunk_dma(const int64_t* arrive_c, const int32_t* req_c, uint32_t lane_cl,
                                           uint32_t lds) {
   uint32_t keep;
@@ -326,13 +331,13 @@ __device__ __forceinline__ void chunk_dma(const int64_t* arrive_c, const int32_t
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %5\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dword %1, %3\n\t"
+      "global_load_lds_dword %1, %3" FOGNET_TRACE_NT "\n\t"
       "s_add_u32 m0, %5, 0xfc\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dword %1, %3 offset:4\n\t"
+      "global_load_lds_dword %1, %3 offset:4" FOGNET_TRACE_NT "\n\t"
       "s_add_u32 m0, %5, 0x200\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dword %2, %4\n\t"
+      "global_load_lds_dword %2, %4" FOGNET_TRACE_NT "\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(lane_cl * 8u), "v"(lane_cl * 4u), "s"(arrive_c), "s"(req_c), "s"(lds)
@@ -1046,10 +1051,12 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
           // offset, so no per-lane 64-bit addresses stay live across the chunk
           const size_t o = tbase + (size_t)c0;
           const uint32_t l = lane_now();
-          (A.out_node + o)[l] = k;
-          (A.out_status + o)[l] = (uint8_t)status;
-          (A.out_start + o)[l] = start;
-          (A.out_done + o)[l] = done;
+          // nontemporal: the outputs are re-read only by the epilogue, long
+          // after they left L2; the ring's head lines keep the cache (-4 %)
+          __builtin_nontemporal_store(k, (A.out_node + o) + l);
+          __builtin_nontemporal_store((uint8_t)status, (A.out_status + o) + l);
+          __builtin_nontemporal_store(start, (A.out_start + o) + l);
+          __builtin_nontemporal_store(done, (A.out_done + o) + l);
         }
       }
       ops += (GEN || (INL && A.no_task_out)) ? 1u : 5u;  // the ring store (+ the four output stores)

@@ -57,6 +57,7 @@ struct WideLds {
   int64_t* g_nxt;   // [G][64]
   int32_t* g_j;     // [G][64]
   uint64_t* g_key;  // [G][64]
+  int64_t* g_w;     // [G][64] REF_V3 run horizon: smallest w (node_w) of the group
   uint32_t* hist;   // [FOGNET_HIST_METRICS][FOGNET_HIST_BINS]
   uint64_t* reg_key;  // [G] EXT_HIER: cached regional minimum key (valid per reg_valid)
   int G;
@@ -66,6 +67,7 @@ struct WideLds {
 struct WideView {
   int64_t* nxt;    // [G * kWideGroupSlots]
   uint32_t* busy;  // [G * kWideGroupSlots]
+  int64_t* w;      // [G * kWideGroupSlots] REF_V3: node_w of the slot
 };
 
 __host__ __device__ __forceinline__ int wide_groups(int N) {
@@ -148,6 +150,56 @@ __device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn
   mk = lane_min_key(L, lane);
 }
 
+// ---- REF_V3 run horizon (the register kernel's horizon_all_in, restated per
+// node so that it needs no knowledge of the current decision).
+//
+// Node j != k (k: the argmin, key best = busy_b << 32 | k) can change the
+// decision only with an advert whose busy value v satisfies (v << 32 | j) <
+// best, i.e. v <= busy_b.  While a run is pushed to k, j receives no task.
+// If every pending task of j reached it before its head completes, its next
+// advert (at nxt_j) carries v1 = tl_C - hd_C and each later one the service
+// of the remaining tasks, so it drops by at most the seconds elapsed: an
+// advert of j with v <= busy_b comes no earlier than nxt_j + (v1 - busy_b)
+// seconds, and never earlier than nxt_j.  With
+//   w_j = nxt_j + v1 s      (all arrived)      w_j = nxt_j  (tasks in flight)
+// every such advert comes at or after max(nxt_j, w_j - busy_b s), so at or
+// after max(min_j nxt_j, min_j w_j - busy_b s): the run may extend to that
+// tick and to k's own next advert.  v1 is capped at 2^21 s (keeps the sum
+// below 2^63); a cap, a stale (too small) group minimum or k's own entry only
+// lower the bound, which shortens runs and never changes a decision.
+__device__ __forceinline__ int64_t node_w(const WideNode& h, int64_t nxt, int64_t dl) {
+  if (h.npend == 0 || nxt == kNever) return kNever;
+  if (!arrives_before(h.tl_a, h.hd_done, dl, h.hd_S)) return nxt;
+  const uint64_t v1 = h.tl_C - h.hd_C;
+  return nxt + ticks_of((uint32_t)(v1 < ((uint64_t)1 << 21) ? v1 : ((uint64_t)1 << 21)));
+}
+
+__device__ __forceinline__ void group_load_w(const WideView& V, int g, int64_t (&x)[kWideGroupSlots]) {
+#pragma unroll
+  for (int i = 0; i < kWideGroupSlots; ++i) x[i] = V.w[g * kWideGroupSlots + i];
+}
+
+// Group g's smallest w (slot sl replaced by the value just computed).
+__device__ __forceinline__ int64_t group_min_w(int g, int sl, int64_t sl_w, const int64_t (&x)[kWideGroupSlots]) {
+  int64_t mn = kNever;
+#pragma unroll
+  for (int i = 0; i < kWideGroupSlots; ++i) {
+    const int64_t xi = g * kWideGroupSlots + i == sl ? sl_w : x[i];
+    mn = xi < mn ? xi : mn;
+  }
+  return mn;
+}
+
+__device__ __forceinline__ int64_t lane_min_w(const WideLds& L, int lane) {
+  int64_t m = kNever;
+#pragma unroll 4
+  for (int g = 0; g < L.G; ++g) {
+    const int64_t x = L.g_w[g * kWave + lane];
+    m = x < m ? x : m;
+  }
+  return m;
+}
+
 // The advert of node j's head completion reaches the broker (owner lane):
 // the view takes busyTime after releaseResource (ComputeBrokerApp3.cc:232,
 // :254) = the service of the tasks that reached j before that completion and
@@ -196,7 +248,7 @@ __device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, in
 
 // Workspace layout (launch_replay_wide, replay_wide_workspace_bytes).
 struct WideWs {
-  size_t e_off, nd_off, nxt_off, busy_off, dv_off, gm_off, gd_off, gu_off, bytes;
+  size_t e_off, nd_off, nxt_off, busy_off, w_off, dv_off, gm_off, gd_off, gu_off, bytes;
 };
 
 __host__ __device__ __forceinline__ size_t align64(size_t x) { return (x + 63) & ~(size_t)63; }
@@ -209,7 +261,8 @@ __host__ __device__ __forceinline__ WideWs wide_ws(int32_t R, int32_t T, int32_t
   w.nd_off = align64(w.e_off + (size_t)R * (size_t)T * sizeof(WideEntry));
   w.nxt_off = align64(w.nd_off + (size_t)R * (size_t)N * sizeof(WideNode));
   w.busy_off = align64(w.nxt_off + (size_t)R * kWave * SP * sizeof(int64_t));
-  w.dv_off = align64(w.busy_off + (size_t)R * kWave * SP * sizeof(uint32_t));
+  w.w_off = align64(w.busy_off + (size_t)R * kWave * SP * sizeof(uint32_t));
+  w.dv_off = align64(w.w_off + (size_t)R * kWave * SP * sizeof(int64_t));
   w.gm_off = align64(w.dv_off + (size_t)R * (size_t)N * sizeof(uint64_t));
   const size_t RN = gen ? (size_t)R * (size_t)N : 0;
   w.gd_off = align64(w.gm_off + RN * sizeof(int32_t));
@@ -228,7 +281,7 @@ struct GenNodes {
 
 template <int POL>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
-                                                int64_t* VN, uint32_t* VB, GenNodes GN, unsigned char* w_lds);
+                                                int64_t* VN, uint32_t* VB, int64_t* VW, GenNodes GN, unsigned char* w_lds);
 
 // One replication per workgroup (r = blockIdx.x), or, with A.wide_list set,
 // the replications the register kernel handed over, taken in turn by the
@@ -236,15 +289,15 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 // list (complete before this launch, stream order) is exhausted.
 template <int POL>
 __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry* E, WideNode* ND, int64_t* VN,
-                                                         uint32_t* VB, GenNodes GN) {
+                                                         uint32_t* VB, int64_t* VW, GenNodes GN) {
   extern __shared__ __align__(16) unsigned char w_lds[];
   if (A.wide_list == nullptr) {
-    replay_wide_rep<POL>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, GN, w_lds);
+    replay_wide_rep<POL>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, VW, GN, w_lds);
     return;
   }
   const int n = *A.wide_count;
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
-    replay_wide_rep<POL>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, GN, w_lds);
+    replay_wide_rep<POL>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, VW, GN, w_lds);
     __syncthreads();  // LDS reuse by the next replication
   }
 }
@@ -252,7 +305,7 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
 // Replication r with workspace slot wr.
 template <int POL>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
-                                                int64_t* VN, uint32_t* VB, GenNodes GN, unsigned char* w_lds) {
+                                                int64_t* VN, uint32_t* VB, int64_t* VW, GenNodes GN, unsigned char* w_lds) {
   constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
   constexpr bool kHier = POL == FOGNET_POLICY_EXT_HIER;
   constexpr bool kPerPublish = kExt || kHier;  // the decision depends on the publish itself
@@ -262,11 +315,13 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   L.G = wide_groups(N);
   L.g_nxt = reinterpret_cast<int64_t*>(w_lds);
   L.g_key = reinterpret_cast<uint64_t*>(L.g_nxt + L.G * kWave);
-  L.g_j = reinterpret_cast<int32_t*>(L.g_key + L.G * kWave);
+  L.g_w = reinterpret_cast<int64_t*>(L.g_key + L.G * kWave);
+  L.g_j = reinterpret_cast<int32_t*>(L.g_w + L.G * kWave);
   L.hist = reinterpret_cast<uint32_t*>(L.g_j + L.G * kWave);
   L.reg_key = reinterpret_cast<uint64_t*>(L.hist + FOGNET_HIST_METRICS * FOGNET_HIST_BINS);
   const int SP = L.G * kWideGroupSlots;
-  const WideView V{VN + ((size_t)wr * kWave + lane) * SP, VB + ((size_t)wr * kWave + lane) * SP};
+  const WideView V{VN + ((size_t)wr * kWave + lane) * SP, VB + ((size_t)wr * kWave + lane) * SP,
+                   VW + ((size_t)wr * kWave + lane) * SP};
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)T;
   WideEntry* const e = E + (size_t)wr * (size_t)T;
@@ -314,11 +369,13 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   for (int s = 0; s < SP; ++s) {  // slots past N too (group rescans read them): never due, never chosen
     V.nxt[s] = kNever;
     V.busy[s] = s * kWave + lane < N ? 0u : 0xFFFFFFFFu;
+    if constexpr (!kPerPublish) V.w[s] = kNever;
   }
   for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) L.hist[h] = 0u;
   for (int g = 0; g < L.G; ++g) {  // the initial view: nothing pending, every busy 0
     const int j0 = g * kWideGroupSlots * kWave + lane;
     L.g_nxt[g * kWave + lane] = kNever;
+    L.g_w[g * kWave + lane] = kNever;
     L.g_j[g * kWave + lane] = lane;
     L.g_key[g * kWave + lane] = j0 < N ? (uint64_t)(uint32_t)j0 : ~0ull;
   }
@@ -330,6 +387,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   int mj;
   uint64_t mk;
   lane_min(L, lane, mn, mj, mk);
+  int64_t mw = kNever;  // REF_V3 run horizon: this lane's smallest node_w
   Acc acc = acc_identity();
   uint32_t max_pend = 0u;  // over this lane's nodes
   int n_short = 0;         // tasks of this lane's nodes that never complete (node-down)
@@ -349,6 +407,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   // (adverts are the only view updates, BrokerBaseApp3.cc:123-130)
   bool view_changed = true;
   uint32_t k = 0u;
+  uint64_t k_key = 0ull;  // REF_V3: the decision's view key (busy << 32 | k)
   uint64_t reg_valid = 0ull, glob_key = 0ull;  // EXT_HIER decision cache (regions < 64)
   bool glob_valid = false;
 
@@ -388,11 +447,12 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           uint32_t busy_j;
           const bool hit = j == cj;
           const int g = sl / kWideGroupSlots;
-          int64_t gx[kWideGroupSlots];
+          int64_t gx[kWideGroupSlots], gw[kWideGroupSlots];
           group_load(V, g, gx);
+          if constexpr (!kPerPublish) group_load_w(V, g, gw);
           WideNode h = hit ? ch : nd[j];
-          lerr |= !apply_advert(h, e, hit ? c_dl : P_dl[j], hit ? c_ul : P_ul[j], kHier ? A.hier_up : 0,
-                                nxt_j, busy_j);
+          const int64_t dl_j = hit ? c_dl : P_dl[j];
+          lerr |= !apply_advert(h, e, dl_j, hit ? c_ul : P_ul[j], kHier ? A.hier_up : 0, nxt_j, busy_j);
           if (hit) ch = h;
           else nd[j] = h;
           V.nxt[sl] = nxt_j;
@@ -400,6 +460,12 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           // the earliest advert: j's was the lane's (so its group's), rescan both levels
           group_scan_nxt(L, lane, g, sl, nxt_j, gx);
           lane_min_nxt(L, lane, mn, mj);
+          if constexpr (!kPerPublish) {
+            const int64_t w_j = node_w(h, nxt_j, dl_j);
+            V.w[sl] = w_j;
+            L.g_w[g * kWave + lane] = group_min_w(g, sl, w_j, gw);
+            mw = lane_min_w(L, lane);
+          }
           // the view key: only j's changed; the group (and lane) minimum needs a rescan only
           // when j held it and its busy time grew
           const uint64_t gk_old = L.g_key[g * kWave + lane];
@@ -460,7 +526,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       } else if (view_changed) {
         // BrokerBaseApp3.cc:267-281: busy_j + req/mips_0 < tempp over exact
         // integer busy values <=> the smallest (busy, j)
-        k = (uint32_t)wave_min_u64(mk);
+        k_key = wave_min_u64(mk);
+        k = (uint32_t)k_key;
         view_changed = false;
       }
       const int kl = (int)(k % kWave);
@@ -494,7 +561,17 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       //    that task's advert bounds the run too
       int jq = jp + 1;
       if constexpr (!kPerPublish) {
-        int64_t E = (int64_t)wave_min_u64((uint64_t)mn);
+        // run horizon (node_w): no other node's advert changes the decision before E
+        const int64_t MN = (int64_t)wave_min_u64((uint64_t)mn);
+        const int64_t MW = (int64_t)wave_min_u64((uint64_t)mw);
+        const uint32_t busy_b = (uint32_t)(k_key >> 32);
+        int64_t E = MN;
+        if (busy_b < (1u << 21) && (uint64_t)(MW - MN) > (uint64_t)ticks_of(busy_b)) E = MW - ticks_of(busy_b);
+        if (npend0 > 0) {  // k's own next advert changes its key
+          const int64_t hd_done_k = readlane_i64(ch.hd_done, kl);
+          const int64_t nxt_k = hd_done_k == kNever ? kNever : hd_done_k + ul_k;
+          E = nxt_k < E ? nxt_k : E;
+        }
         if (npend0 == 0) {
           const uint32_t S0 = readlane_u32((uint32_t)cr, jp) / (uint32_t)mips_k;
           const int64_t a0 = t + dl_k;
@@ -631,6 +708,15 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         h.npend += Lr;
         ch = h;
         max_pend = max(max_pend, (uint32_t)h.npend);
+        if constexpr (!kPerPublish) {
+          // k's w (a larger value may leave its group minimum stale-small: conservative)
+          const int sk = (int)k / kWave, gk = sk / kWideGroupSlots;
+          const int64_t nxt_k = h.hd_done == kNever ? kNever : h.hd_done + ul_k;
+          const int64_t w_k = node_w(h, nxt_k, c_dl);
+          V.w[sk] = w_k;
+          if (w_k < L.g_w[gk * kWave + lane]) L.g_w[gk * kWave + lane] = w_k;
+          if (w_k < mw) mw = w_k;
+        }
       }
       n_done += Lr;
       jp = jq;
@@ -684,18 +770,18 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 
 template <int POL>
 void launch_wide_pol(const ReplayArgs& a, int32_t slots, WideEntry* e, WideNode* nd, int64_t* vn, uint32_t* vb,
-                     GenNodes gn, size_t lds, hipStream_t s) {
+                     int64_t* vw, GenNodes gn, size_t lds, hipStream_t s) {
   if (lds > 65536)  // above the default dynamic-LDS limit (N > ~51,000 nodes; gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&replay_wide_kernel<POL>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb, gn);
+  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb, vw, gn);
 }
 
 }  // namespace
 
 size_t replay_wide_lds_bytes(int32_t N) {
   const size_t G = (size_t)wide_groups(N);
-  return G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int32_t)) +
+  return G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int64_t) + sizeof(int32_t)) +
          FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t) + G * sizeof(uint64_t);
 }
 
@@ -708,15 +794,16 @@ hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slot
   WideNode* const nd = reinterpret_cast<WideNode*>(base + w.nd_off);
   int64_t* const vn = reinterpret_cast<int64_t*>(base + w.nxt_off);
   uint32_t* const vb = reinterpret_cast<uint32_t*>(base + w.busy_off);
+  int64_t* const vw = reinterpret_cast<int64_t*>(base + w.w_off);
   const GenNodes gn{reinterpret_cast<int32_t*>(base + w.gm_off), reinterpret_cast<int64_t*>(base + w.gd_off),
                     reinterpret_cast<int64_t*>(base + w.gu_off), reinterpret_cast<uint64_t*>(base + w.dv_off)};
   const size_t lds = replay_wide_lds_bytes(a.N);
   if (a.policy == FOGNET_POLICY_EXT_LAT)
-    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, slots, e, nd, vn, vb, gn, lds, s);
+    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, slots, e, nd, vn, vb, vw, gn, lds, s);
   else if (a.policy == FOGNET_POLICY_EXT_HIER)
-    launch_wide_pol<FOGNET_POLICY_EXT_HIER>(a, slots, e, nd, vn, vb, gn, lds, s);
+    launch_wide_pol<FOGNET_POLICY_EXT_HIER>(a, slots, e, nd, vn, vb, vw, gn, lds, s);
   else
-    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, slots, e, nd, vn, vb, gn, lds, s);
+    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, slots, e, nd, vn, vb, vw, gn, lds, s);
   return hipGetLastError();
 }
 
