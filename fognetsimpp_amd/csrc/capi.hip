@@ -97,7 +97,7 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a, boo
   if (in->R < 0 || in->T < 0 || in->N < 0) return fail(c, FOGNET_ERR_ARG, "negative R/T/N");
   if (in->N == 0) return fail(c, FOGNET_ERR_NO_NODES, "N == 0 (BrokerBaseApp3.cc:268 reads brokers[0])");
   if (in->N > fognet::kWideMaxNodes)
-    return fail(c, FOGNET_ERR_UNSUPPORTED, "N > 65536 (the wide replay kernel keeps 20 B of group minima per 16 nodes in LDS)");
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "N > 65536 (the wide replay kernel keeps 28 B of group minima per 16 nodes in LDS)");
   if (in->policy != FOGNET_POLICY_REF_V3 && in->policy != FOGNET_POLICY_EXT_LAT && in->policy != FOGNET_POLICY_EXT_HIER)
     return fail(c, FOGNET_ERR_UNSUPPORTED, "unknown policy");
   if (in->policy == FOGNET_POLICY_EXT_HIER) {

@@ -303,10 +303,10 @@ struct WideNode {
 static_assert(sizeof(WideNode) == 64, "wide node record is one 64-B line");
 
 // LDS of the wide kernel: per lane and group of 16 of its nodes the earliest
-// advert, its node and the smallest view key (20 B) + the histogram; the
+// advert, its node, the smallest view key and run-horizon bound (28 B) + the histogram; the
 // per-node view (next advert tick, advertised busy) is in HBM.
 constexpr int kWideGroupSlots = 16;
-constexpr int kWideMaxNodes = 65536;  // LDS: 82 KiB of group minima
+constexpr int kWideMaxNodes = 65536;  // LDS: 115 KiB of group minima
 size_t replay_wide_lds_bytes(int32_t N);
 // workspace: R*T WideEntry followed by R*N WideNode
 // (+ R*N generated node parameters in generated mode)

@@ -20,7 +20,7 @@
 //          WideNode [R][N]: chain ends + copies of head and tail fields (64 B).
 //   LDS    per lane and group of 16 of its slots: earliest advert, its node,
 //          smallest view key (busy << 32 | j); the lane's minima in VGPRs.
-//          13 KiB at N = 10,000, so four replications share a CU (the loop is
+//          18 KiB at N = 10,000, so four replications share a CU (the loop is
 //          latency-bound: every applied advert waits on HBM).
 //   VGPRs  the record and parameters of the node the lane pushed to last
 //          (the stale view keeps choosing it), written back when the lane
