@@ -638,6 +638,15 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         err = FOGNET_ERR_ARG;
         break;
       }
+      if constexpr (kHier) {
+        // the node serves in arrival order; the chain is in decision order.  A task
+        // that reaches k before an escalated task decided earlier (which took the
+        // extra hop) would overtake it: not modelled, the replication fails loudly
+        if (ballot(lane == jp && in_run && a < readlane_i64(ch.tl_a, kl))) {
+          err = FOGNET_ERR_UNSUPPORTED;
+          break;
+        }
+      }
       // task entries: chained in publish order (consecutive task indices)
       const int i = c0 + lane;
       if (in_run) {

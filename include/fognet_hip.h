@@ -90,7 +90,10 @@ typedef enum fognet_policy {
                                    that busy exceeds hier_threshold_s the task is escalated to the
                                    parent broker, which applies the rule over ALL nodes, and
                                    reaches its node hier_up_tick later (the extra hop).  Adverts
-                                   reach every broker with the node's uplink latency.         */
+                                   reach every broker with the node's uplink latency.  A task
+                                   that would reach its node before an escalated task decided
+                                   earlier (overtaking it inside the hop) is not modelled: that
+                                   replication's status is FOGNET_ERR_UNSUPPORTED.            */
 } fognet_policy;
 
 /* Region size of FOGNET_POLICY_EXT_HIER (node r * 1024 .. r * 1024 + 1023 form region r). */
