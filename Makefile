@@ -27,6 +27,15 @@ $(OBJDIR)/io.o: $(SRC_DIR)/io.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HOSTCXX) -O2 -std=c++17 -fPIC -Wall -ffp-contract=off -Iinclude -c $< -o $@
 
+# replay.o keeps its gfx950 assembly: the inline-asm prefetch of replay.hip is
+# correct only while no compiler-generated instruction of the replay loops
+# touches the reserved registers, so the library is not linked
+# unless tools/check_nh_regs.py passes on exactly the code that ships.
+$(OBJDIR)/replay.o: $(SRC_DIR)/replay.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o $@ -save-temps=obj
+	python3 tools/check_nh_regs.py $(OBJDIR)/replay-hip-amdgcn-amd-amdhsa-$(ARCH).s
+
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 

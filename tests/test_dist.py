@@ -162,3 +162,81 @@ def test_comm_allreduce_world1_is_identity(ctx):
         comm.close()
     assert merged.tobytes() == job.tobytes()
     assert torch.equal(out.hist, hist0)
+
+
+# ------------------------------------------------------------------ HIP engine in every rank (world 2, one GPU)
+
+def _gpu_worker(rank, world, port, R_total, T, N, q):
+    """One rank: replay its contiguous block of the global replications on the
+    GPU (device Philox traces keyed by the global index), reduce on the device,
+    all-gather the job record and all-reduce the histogram + energy over gloo
+    (both ranks share cuda:0 on a one-GPU box, which RCCL does not allow)."""
+    import fognetsimpp_amd as fa
+    from fognetsimpp_amd import engine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        ctx = fa.Context(0)
+        r0, n = shard(R_total, world, rank)
+        mg, sc = fa.sweep_params(np.arange(r0, r0 + n), N)
+        tr = fa.generate_trace(ctx, 0x5EED0003, n, T, N, mg, sc, r0=r0)
+        pb, pi = fa.power_model(tr["mips"].cpu().numpy())
+        tr["p_busy"], tr["p_idle"] = torch.from_numpy(pb).to(dev), torch.from_numpy(pi).to(dev)
+        out = fa.run_batch(ctx, tr, hist=True)
+        job = fa.reduce_stats(ctx, out.stats, n)
+        torch.cuda.synchronize()
+        hist = out.hist.cpu()
+        energy = torch.tensor([float(job["energy_j"])], dtype=torch.float64)
+        merged = allgather_job_stats(job_record_tensor(job, torch.device("cpu")))
+        allreduce_hist_energy(hist, energy)
+        if rank == 0:
+            q.put((merged.tobytes(), hist.numpy().copy(), float(energy[0])))
+        del out, tr
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+def test_gloo_world2_hip_engine_matches_single_rank(ctx):
+    """two ranks each replay their block of C3-recipe
+    replications through libfognet_hip; the merged job record and histogram
+    equal one rank replaying all of them (integer fields bit-exact, the fp64
+    energy sum within 1e-12 relative), and the histogram counts every task."""
+    import fognetsimpp_amd as fa
+    R_total, T, N = 6, 3000, 256
+    dev = torch.device("cuda", 0)
+    mg, sc = fa.sweep_params(np.arange(R_total), N)
+    tr = fa.generate_trace(ctx, 0x5EED0003, R_total, T, N, mg, sc)
+    pb, pi = fa.power_model(tr["mips"].cpu().numpy())
+    tr["p_busy"], tr["p_idle"] = torch.from_numpy(pb).to(dev), torch.from_numpy(pi).to(dev)
+    out = fa.run_batch(ctx, tr, hist=True)
+    single = fa.reduce_stats(ctx, out.stats, R_total)
+    torch.cuda.synchronize()
+    single_hist = out.hist.cpu().numpy()
+
+    mpx = mp.get_context("spawn")
+    q = mpx.Queue()
+    port = free_port()
+    procs = [mpx.Process(target=_gpu_worker, args=(r, 2, port, R_total, T, N, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got, got_hist, got_energy = q.get(timeout=200)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    got_rec = np.frombuffer(got, dtype=_abi.JOB_STATS_DTYPE)[0]
+    assert int(got_rec["n_reps"]) == R_total and int(got_rec["n_failed"]) == 0
+    assert int(got_rec["n_tasks"]) == R_total * T
+    np.testing.assert_array_equal(got_hist, single_hist)
+    assert got_hist[1].sum() == R_total * T
+    np.testing.assert_allclose(got_energy, float(single["energy_j"]), rtol=1e-12)
+    a, b = got_rec.copy(), np.array(single).copy().reshape(-1)[0]
+    a["energy_j"] = b["energy_j"] = 0.0
+    assert a.tobytes() == b.tobytes()
