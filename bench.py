@@ -76,7 +76,8 @@ def main():
     ap.add_argument("--N", type=int, default=256)
     ap.add_argument("--ring", type=int, default=2048)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0003)
-    ap.add_argument("--cpu-reps", type=int, default=1024, help="replications in the CPU-baseline sample")
+    ap.add_argument("--cpu-reps", type=int, default=None,
+                    help="replications in the CPU-baseline sample (default 1024; 256 for c5)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this job may use")
     ap.add_argument("--cpu-reps-1t", type=int, default=16, help="replications of the single-thread CPU sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -105,8 +106,10 @@ def main():
     if args.workload == "c5":
         if args.N == 256:
             args.N = 10_000
-        if args.cpu_reps == 1024:
+        if args.cpu_reps is None:
             args.cpu_reps = 256  # ~1 s on 16 threads (~17 CPU-seconds)
+    if args.cpu_reps is None:
+        args.cpu_reps = 1024
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
