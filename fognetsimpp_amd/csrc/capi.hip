@@ -15,7 +15,7 @@ struct fognet_ctx {
   int device = -1;
   int cus = 256;  // compute units (generated-mode launch size)
   hipStream_t stream = nullptr;  // private stream for the host-buffer entry points
-  fognet::RingEntry* ring = nullptr;
+  fognet::RingWord* ring = nullptr;
   size_t ring_bytes = 0;
   // partial job records of a multi-block reduction (fognet_reduce_stats_dev)
   void* red = nullptr;
@@ -417,7 +417,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     // workspace: [hand-over counter | hand-over list [R] | pending-task rings, reused by the wide kernel's
     // replay of the handed-over replications once the register kernel is done (stream order)]
     // + for a statistics-only replay the per-task outputs the fused statistics epilogue reads back
-    const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
+    const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingWord);
     const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
     const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
     const size_t o_board = align256(256 + (size_t)a.R * sizeof(int32_t));
@@ -431,7 +431,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     unsigned char* const base = reinterpret_cast<unsigned char*>(c->ring);
     a.wide_count = reinterpret_cast<int32_t*>(base);
     a.wide_list = reinterpret_cast<int32_t*>(base + 256);
-    a.ring = reinterpret_cast<fognet::RingEntry*>(base + head);
+    a.ring = reinterpret_cast<fognet::RingWord*>(base + head);
     if (stats_only && !a.inloop) {
       a.out_node = reinterpret_cast<int32_t*>(base + o_node);
       a.out_status = reinterpret_cast<uint8_t*>(base + o_st);
@@ -500,7 +500,7 @@ int fognet_run_generated_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t 
   // the wide hand-over]
   const int64_t resident = (int64_t)c->cus * fognet::kGenWavesPerCu;
   a.gen_slots = (int32_t)(a.R < resident ? a.R : resident);
-  const size_t ring_bytes = (size_t)a.gen_slots * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingEntry);
+  const size_t ring_bytes = (size_t)a.gen_slots * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingWord);
   const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
   const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N, true);
   const size_t head = align256(256 + (size_t)a.R * sizeof(int32_t));
@@ -510,7 +510,7 @@ int fognet_run_generated_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t 
   unsigned char* const base = reinterpret_cast<unsigned char*>(c->ring);
   a.wide_count = reinterpret_cast<int32_t*>(base);
   a.wide_list = reinterpret_cast<int32_t*>(base + 256);
-  a.ring = reinterpret_cast<fognet::RingEntry*>(base + head);
+  a.ring = reinterpret_cast<fognet::RingWord*>(base + head);
   a.queue = reinterpret_cast<int32_t*>(base + sizeof(int32_t));
   e = hipMemsetAsync(base, 0, 2 * sizeof(int32_t), (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(c, e, "hand-over and work counters");

@@ -189,14 +189,21 @@ __device__ __forceinline__ void gen_task(const GenRep& g, int i, int64_t& gap, i
 
 // ---------------------------------------------------------------- replay
 
-// Pending-task ring entry: one per task assigned to a node, kept until the
-// advertisement of its completion has been applied to the broker's view.
-struct RingEntry {
-  int64_t a;   // arrival tick at the node (broker decision tick + dl)
-  uint32_t C;  // cumulative service seconds assigned to the node, this task included (mod 2^32)
-  uint32_t S;  // service seconds, requiredMIPS / MIPS (int division)
-};
-static_assert(sizeof(RingEntry) == 16, "ring entry is 16 B");
+// Pending-task ring entry of the register kernel (replay.hip): one 8-B word
+// per task assigned to a node, kept until the advertisement of its
+// completion has been applied to the broker's view:
+//   bits 8..63  arrival tick at the node (broker decision tick + dl), < 2^56
+//   bits 0..7   service seconds, requiredMIPS / MIPS (int division), < 2^8
+// The cumulative service of an entry is not stored: it follows from the
+// head's (+ S) or the tail's (- the later entries' S).  Two consecutive
+// entries share a 16-B aligned pair, which the head+1 prefetch loads at once,
+// so one cache-line fetch serves two completions.  A task outside these
+// ranges (a simulated time past 2^56 ticks = 20 h, or a service time above
+// 255 s) hands its replication to the wide kernel (exact, unbounded).
+typedef uint64_t RingWord;
+constexpr int kRingSBits = 8;
+constexpr uint32_t kRingSMask = (1u << kRingSBits) - 1u;
+constexpr int64_t kRingAMax = (int64_t)((1ull << (64 - kRingSBits)) - 1ull);
 
 struct ReplayArgs {
   int32_t R, T, N, node_stride;
@@ -215,7 +222,7 @@ struct ReplayArgs {
   int64_t* out_start;
   int64_t* out_done;
   fognet_rep_stats* out_stats;
-  RingEntry* ring;  // [R][N][Q]
+  RingWord* ring;  // [R][N][Q]
   const double* p_busy;   // [R|1][N] power model (nullable)
   const double* p_idle;
   double* out_energy;     // [R][N] (nullable)

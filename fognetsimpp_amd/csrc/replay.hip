@@ -42,7 +42,8 @@ struct Slot {
   // (head completion tick = nxt - ul: the advert leaves the node at completion)
   uint32_t hd_C;     // cumulative service up to and including the head
   uint32_t hd_S;     // head service seconds (< 2^24)
-  // (entry head+1 {a lo, a hi, C, S} lives in reserved VGPRs, see nh_prefetch)
+  // (the 16-B ring pair holding entry head+1 lives in reserved VGPRs, see
+  //  nh_prefetch; RingWord layout in internal.h)
   int64_t tl_a;      // tail (newest) task: arrival tick at the node
   // (tail completion tick, cumulative service and service time live in LDS:
   //  s_tld / s_tlC / s_tlS, read at a uniform address when the node is chosen)
@@ -75,7 +76,15 @@ __device__ __forceinline__ uint32_t n_push(const Slot& st) { return st.cnt & 0xF
 __device__ __forceinline__ uint32_t n_head(const Slot& st) { return st.cnt >> 16; }
 __device__ __forceinline__ uint32_t pending(const Slot& st) { return (n_push(st) - n_head(st)) & 0xFFFFu; }
 __device__ __forceinline__ uint32_t head_S(const Slot& st) { return st.hd_S; }
-__device__ __forceinline__ int64_t nh_a(u32x4 v) { return (int64_t)(((uint64_t)v.y << 32) | v.x); }
+// Ring pairs: entries 2p and 2p + 1 of a node's ring share one 16-B aligned
+// pair; the reserved registers of a slot hold the pair of its head+1 entry.
+// Entry head+1 is its odd half when head+1 is odd.
+__device__ __forceinline__ uint32_t nh_odd(const Slot& st) { return (n_head(st) + 1u) & 1u; }
+__device__ __forceinline__ RingWord nh_word(u32x4 v, uint32_t odd) {
+  return odd ? (((uint64_t)v.w << 32) | v.z) : (((uint64_t)v.y << 32) | v.x);
+}
+__device__ __forceinline__ int64_t rw_a(RingWord w) { return (int64_t)(w >> kRingSBits); }
+__device__ __forceinline__ uint32_t rw_S(RingWord w) { return (uint32_t)w & kRingSMask; }
 
 // ---- head+1 prefetch, outside the compiler's register allocation
 //
@@ -111,11 +120,11 @@ constexpr int kNhBaseGen = 152;
 static_assert(kNhBaseGen + 4 * kMaxNodesPerLane == 168, "3 waves/SIMD: 168 VGPRs per lane");
 
 #define FOGNET_NH_SLOT(S, R0, R1, R2, R3, RR)                                                  \
-  __device__ __forceinline__ void nh_prefetch_##S(const RingEntry* p) {                       \
+  __device__ __forceinline__ void nh_prefetch_##S(const RingWord* p) {                       \
     asm volatile("global_load_dwordx4 " RR ", %0, off" : : "v"(p) : "memory", R0, R1, R2, R3); \
   }                                                                                           \
   /* one lane's load: EXEC narrowed inside the statement (uniform control flow) */           \
-  __device__ __forceinline__ void nh_refill_##S(const RingEntry* p, uint64_t only) {          \
+  __device__ __forceinline__ void nh_refill_##S(const RingWord* p, uint64_t only) {          \
     uint64_t saved;                                                                           \
     asm volatile("s_mov_b64 %0, exec\n\t"                                                     \
                  "s_mov_b64 exec, %2\n\t"                                                     \
@@ -194,7 +203,7 @@ static_assert(kPrefetchOps == 8, "nh_read waits at most for vmcnt(8)");
 
 // S: slot + 4 * register set
 template <int S>
-__device__ __forceinline__ void nh_prefetch(const RingEntry* p) {
+__device__ __forceinline__ void nh_prefetch(const RingWord* p) {
   if constexpr (S == 0) nh_prefetch_0(p);
   else if constexpr (S == 1) nh_prefetch_1(p);
   else if constexpr (S == 2) nh_prefetch_2(p);
@@ -235,12 +244,12 @@ __device__ __forceinline__ u32x4 read_nh(bool need, uint32_t pf, uint32_t ops) {
   else return nh_read_7(m);
 }
 
-// Reload the head+1 entry of node (slot s, lane): one cache line.  Ring
-// stores issued earlier by this wave (any lane) precede it in the same
-// in-order memory pipeline, so it observes them.
+// Reload the pair holding the head+1 entry of node (slot s, lane): one cache
+// line.  Ring stores issued earlier by this wave (any lane) precede it in the
+// same in-order memory pipeline, so it observes them.
 template <int SET>
-__device__ __forceinline__ void refill_nh(int s, const Slot& st, const RingEntry* ring, uint32_t qmask, int lane) {
-  const RingEntry* p = ring + ((n_head(st) + 1u) & qmask);
+__device__ __forceinline__ void refill_nh(int s, const Slot& st, const RingWord* ring, uint32_t qmask, int lane) {
+  const RingWord* p = ring + (((n_head(st) + 1u) & qmask) & ~1u);
   const uint64_t only = 1ull << __builtin_amdgcn_readfirstlane(lane);  // lane is wave-uniform
   if constexpr (SET == 0) {
     switch (__builtin_amdgcn_readfirstlane(s)) {
@@ -397,38 +406,45 @@ __device__ __forceinline__ void wait_vm(uint32_t m) {
 
 // Cumulative service of the tasks that reached the node before the
 // completion (tick `done`, service S) of pending entry head+d0; scans back
-// from the newest assignment.  c_self: cumulative service of that entry.
+// from the newest assignment (tail: cumulative service tl_C, service tl_S;
+// entry d's cumulative service is its successor's minus the successor's
+// service).  c_self: cumulative service of entry head+d0.
 __device__ __forceinline__ uint32_t c_arrived(const Slot& st, const u32x4 nhw, int64_t done, uint32_t S,
                                               uint32_t d0, uint32_t c_self, int64_t dl, uint32_t tl_C,
-                                              const RingEntry* ring, uint32_t qmask, uint32_t& scan) {
+                                              uint32_t tl_S, const RingWord* ring, uint32_t qmask,
+                                              uint32_t& scan) {
   if (arrives_before(st.tl_a, done, dl, S)) return tl_C;
   const uint32_t pend = pending(st);
+  uint32_t C = tl_C, S_next = tl_S;  // entry d + 1's
   // entries head+d for d = pend-2 .. d0+1 (the tail, d = pend-1, did not qualify)
   for (uint32_t d = pend - 1u; d-- > d0 + 1u;) {
-    int64_t a;
-    uint32_t C;
+    RingWord w;
     if (d == 1u) {
-      a = nh_a(nhw);
-      C = nhw.z;
+      w = nh_word(nhw, nh_odd(st));
     } else {
       PROF(scan += 1u;)
-      const RingEntry e = ring[(n_head(st) + d) & qmask];
-      a = e.a;
-      C = e.C;
+      w = ring[(n_head(st) + d) & qmask];
     }
-    if (arrives_before(a, done, dl, S)) return C;
+    C -= S_next;
+    if (arrives_before(rw_a(w), done, dl, S)) return C;
+    S_next = rw_S(w);
   }
   return c_self;  // only the completing task itself
 }
 
 // Apply the advert of the head completion of node k (lane-local): the broker
-// view takes busyTime after releaseResource (:232, :254), the head advances
-// and entry head+2 is prefetched.  nhw: st.nh read after its wait.
+// view takes busyTime after releaseResource (:232, :254) and the head
+// advances; the pair of the new head+1 is prefetched when it starts a new
+// pair (an odd new head+1 shares the pair already held).  nhw: the held pair,
+// read after its wait.
 template <int SL, int SET>
 __device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, int64_t dl, int64_t ul, uint32_t tl_C,
-                                             const RingEntry* ring, uint32_t qmask, uint32_t ops, uint32_t& scan) {
+                                             uint32_t tl_S, const RingWord* ring, uint32_t qmask, uint32_t ops,
+                                             uint32_t& scan) {
   const int64_t hd_done = st.nxt - ul;
-  const uint32_t busy = c_arrived(st, nhw, hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask, scan) - st.hd_C;
+  const uint32_t busy =
+      c_arrived(st, nhw, hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, tl_S, ring, qmask, scan) - st.hd_C;
+  const RingWord w = nh_word(nhw, nh_odd(st));
   st.vkey = (busy << 8) | (uint32_t)k;  // busy < 2^24 (max_s * ring capacity)
   st.cnt += 0x10000u;
   const uint32_t pend = pending(st);
@@ -436,13 +452,14 @@ __device__ __forceinline__ void apply_advert(Slot& st, const u32x4 nhw, int k, i
     st.nxt = kNever;
     return;
   }
-  const int64_t na = nh_a(nhw);
+  const int64_t na = rw_a(w);
+  const uint32_t S1 = rw_S(w);
   const int64_t start = na > hd_done ? na : hd_done;
-  const int64_t done = start + (int64_t)nhw.w * kTicksPerSecond;
-  st.hd_C = nhw.z;
-  st.hd_S = nhw.w;
+  const int64_t done = start + (int64_t)S1 * kTicksPerSecond;
+  st.hd_C += S1;
+  st.hd_S = S1;
   st.nxt = done + ul;
-  if (pend >= 2u) {  // the ring holds every pending entry, the tail included
+  if (pend >= 2u && nh_odd(st) == 0u) {  // the ring holds every pending entry, the tail included
     nh_prefetch<SL + SET>(ring + ((n_head(st) + 1u) & qmask));  // the caller stamps slot SL
   }
 }
@@ -473,20 +490,23 @@ __device__ __forceinline__ int64_t horizon_all_in(const Slot& st, int j, uint32_
 // them the closed form above applies once the queue has fully arrived,
 // otherwise the horizon stops at the second.
 __device__ __forceinline__ int64_t horizon(const Slot& st, const u32x4 nhw, int j, uint32_t best, uint32_t tl_C,
-                                           int64_t dl, int64_t ul, const RingEntry* ring, uint32_t qmask,
-                                           uint32_t& scan) {
+                                           uint32_t tl_S, int64_t dl, int64_t ul, const RingWord* ring,
+                                           uint32_t qmask, uint32_t& scan) {
   const uint32_t pend = pending(st);
   const int64_t hd_done = st.nxt - ul;
-  const uint32_t v1 = c_arrived(st, nhw, hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, ring, qmask, scan) - st.hd_C;
+  const uint32_t v1 =
+      c_arrived(st, nhw, hd_done, head_S(st), 0u, st.hd_C, dl, tl_C, tl_S, ring, qmask, scan) - st.hd_C;
   if (((v1 << 8) | (uint32_t)j) < best) return st.nxt;
   if (pend < 2u) return kNever;
-  const int64_t na = nh_a(nhw);
-  const int64_t done2 = (na > hd_done ? na : hd_done) + (int64_t)nhw.w * kTicksPerSecond;
+  const RingWord w = nh_word(nhw, nh_odd(st));
+  const int64_t na = rw_a(w);
+  const uint32_t S1 = rw_S(w), C1 = st.hd_C + S1;
+  const int64_t done2 = (na > hd_done ? na : hd_done) + (int64_t)S1 * kTicksPerSecond;
   const int64_t x2 = done2 + ul;
-  const uint32_t v2 = c_arrived(st, nhw, done2, nhw.w, 1u, nhw.z, dl, tl_C, ring, qmask, scan) - nhw.z;
+  const uint32_t v2 = c_arrived(st, nhw, done2, S1, 1u, C1, dl, tl_C, tl_S, ring, qmask, scan) - C1;
   if (((v2 << 8) | (uint32_t)j) < best) return x2;
   if (pend == 2u) return kNever;
-  if (!arrives_before(st.tl_a, done2, dl, nhw.w)) return x2;
+  if (!arrives_before(st.tl_a, done2, dl, S1)) return x2;
   // fully arrived from completion 2 on: busy_m = v2 - (C_m - C_2), v2 >= thr
   const uint32_t need = min(v2 - busy_threshold(j, best) + 1u, 1u << 21);
   return x2 + ticks_of(need);
@@ -732,7 +752,7 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
   if (N <= 0) err = FOGNET_ERR_NO_NODES;
 
-  RingEntry* const ring_r = A.ring + (size_t)slot * (size_t)N * ((size_t)qmask + 1u);
+  RingWord* const ring_r = A.ring + (size_t)slot * (size_t)N * ((size_t)qmask + 1u);
   const int q_log2 = A.q_log2;
   // ring of this lane's node in slot s (lanes past N alias node 0: in bounds, never used)
   // Per-lane addresses are rebuilt at each use from wave-uniform bases and an
@@ -743,7 +763,7 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
     asm volatile("" : "+v"(l));
     return l;
   };
-  auto ring_s = [&](int s) -> RingEntry* {
+  auto ring_s = [&](int s) -> RingWord* {
     const uint32_t k = (uint32_t)(s * kWave) + lane_now();
     return ring_r + ((size_t)(k < (uint32_t)N ? k : 0u) << q_log2);
   };
@@ -848,15 +868,17 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
             TMARK(1)
             const u32x4 nhw = read_nh<s, kSet>((dm & lanes_ge(pd, 2u)) != 0, pf, ops);
             TMARK(8)
-            // apply_advert prefetches head+2 where >= 3 are pending: tally it
-            // first, so the stamp already counts the load itself
-            if (dm & lanes_ge(pd, 3u)) {
+            // apply_advert prefetches the pair of head+2 where >= 3 are pending
+            // and head+2 starts a pair (head even): tally it first, so the stamp
+            // already counts the load itself
+            if (dm & lanes_ge(pd, 3u) & ballot((st[s].cnt & 0x10000u) == 0u)) {
               ops += 1u;
               pf = set_stamp(pf, s, ops);
             }
             if (due) {
               const int k = s * kWave + lane;
-              apply_advert<s, kSet>(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], ring_s(s), qmask, ops, scan);
+              apply_advert<s, kSet>(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], s_tlS[k], ring_s(s), qmask, ops,
+                                    scan);
             }
           });
           if (!any) break;
@@ -902,7 +924,8 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
             const u32x4 nhw = read_nh<s, kSet>((dm & lanes_ge(pd, 2u)) != 0, pf, ops);
             TMARK(9)
             if (deep) {
-              const int64_t h = horizon(st[s], nhw, j, best, s_tlC[j], s_dl[j], s_ul[j], ring_s(s), qmask, scan);
+              const int64_t h =
+                  horizon(st[s], nhw, j, best, s_tlC[j], s_tlS[j], s_dl[j], s_ul[j], ring_s(s), qmask, scan);
               e_lane = h < e_lane ? h : e_lane;
             }
           }
@@ -963,7 +986,8 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
         a = ca + dl_k;
         dd = (int64_t)S * kTicksPerSecond;
         lerr = a > kMaxTick;
-        lwide = S > A.max_s;  // beyond this kernel's 24-bit busy key: the wide kernel replays it
+        // beyond this kernel's 24-bit busy key or its 8-B ring entry: the wide kernel replays it
+        lwide = S > A.max_s || S > kRingSMask || a > kRingAMax;
       }
       //    Unrolled: with P_m = sum_{i<=m} S_i 1e12 (a prefix sum) and
       //    X_m = a_m - P_{m-1},  done_m = max(done_before_run, max_{i<=m} X_i) + P_m,
@@ -1024,13 +1048,9 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
       }
       TMARK(4)
       // ring entries (consecutive slots of node k's ring) and per-task outputs
-      RingEntry* const ring_k = ring_r + ((size_t)k << q_log2);
+      RingWord* const ring_k = ring_r + ((size_t)k << q_log2);
       if (in_run) {
-        RingEntry e;
-        e.a = a;
-        e.C = tlC_k + Cs;
-        e.S = S;
-        ring_k[((cnt_k & 0xFFFFu) + (uint32_t)(lane - jp)) & qmask] = e;
+        ring_k[((cnt_k & 0xFFFFu) + (uint32_t)(lane - jp)) & qmask] = ((uint64_t)a << kRingSBits) | S;
         if constexpr (INL) {
           // the task's statistics (the fused epilogue's, rep_stats_kernel's)
           const int64_t resp = done - ca;
@@ -1083,8 +1103,10 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
             s_tlS[k] = S_z;
             st[s].cnt = (cnt_k & 0xFFFF0000u) | ((cnt_k + (uint32_t)L) & 0xFFFFu);
           }
-          // k's head+1 changed: reload it (uniform control flow, one lane)
-          if ((pend_k == 0u && L >= 2) || pend_k == 1u) {
+          // the run wrote into the held pair (entry head+1, or head+2 when it
+          // shares head+1's pair): reload it (uniform control flow, one lane)
+          const uint32_t pl = pend_k + (uint32_t)L;
+          if ((pend_k <= 1u && pl >= 2u) || ((cnt_k & 0x10000u) != 0u && pend_k <= 2u && pl >= 3u)) {
             refill_nh<kSet>(s, st[s], ring_s(s), qmask, kl);
             PROF(p_refill++;)
             ops += 1u;
