@@ -262,8 +262,25 @@ def test_service_past_register_kernel_bound(ctx):
     assert sep.rep_stats().tobytes() == g["stats"].tobytes()
 
 
+def test_compact_ring_bounds_hand_over(ctx):
+    """The register kernel's 8-B ring entries (internal.h RingWord: arrival
+    < 2^56 ticks, service < 256 s): a replication with a longer service time or
+    a later arrival is handed to the wide kernel inside the same call; mixed
+    with replications that stay, every record is bit-exact against the oracle."""
+    tr = tg.make_batch(14, 5, 8, 800, rho=0.8)
+    tr = {k: v.copy() for k, v in tr.items()}
+    tr["req"][1, 30] = 300 * int(tr["mips"][1].max())  # >= 300 s on any node
+    tr["req"][3, 100:140] = 256 * int(tr["mips"][3].max())  # 256 s: one past the entry's 8 bits
+    tr["arrive"][2] += 1 << 57  # past the entry's tick range, within the kernel's 2^61
+    g = run_gpu_full(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=4, hist=True)
+    assert (g["stats"]["status"] == 0).all()
+    assert_parity(tr, g, o)
+    np.testing.assert_array_equal(g["hist"], o["hist"].sum(axis=0))
+
+
 @pytest.mark.parametrize("N", [16, 300])  # register-resident and wide kernel
-@pytest.mark.parametrize("bad", ["unsorted", "neg_req", "mips0", "late_advert", "early_advert_send", "huge_service"])
+@pytest.mark.parametrize("bad",["unsorted", "neg_req", "mips0", "late_advert", "early_advert_send", "huge_service"])
 def test_precondition_errors(ctx, bad, N):
     tr = tg.make_batch(5, 2, N, 300)
     tr = {k: v.copy() for k, v in tr.items()}
