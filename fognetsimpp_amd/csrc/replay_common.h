@@ -188,10 +188,22 @@ __device__ __forceinline__ void add128(uint64_t& lo, uint64_t& hi, uint64_t vlo,
   hi += vhi + (lo < o ? 1u : 0u);
 }
 
+// v^2 as a 128-bit (lo, hi) from three 32x32 -> 64 products (v = h 2^32 + l:
+// v^2 = h^2 2^64 + 2 h l 2^32 + l^2), instead of the 64-bit low product plus
+// __umul64hi (about eight quarter-rate multiplies between them).
+__device__ __forceinline__ void sq128(uint64_t v, uint64_t& lo, uint64_t& hi) {
+  const uint32_t l = (uint32_t)v, h = (uint32_t)(v >> 32);
+  const uint64_t ll = (uint64_t)l * l, hl = (uint64_t)h * l, hh = (uint64_t)h * h;
+  lo = ll + (hl << 33);
+  hi = hh + (hl >> 31) + (lo < ll ? 1u : 0u);
+}
+
 __device__ __forceinline__ void add_moment(uint64_t& slo, uint64_t& shi, uint64_t& qlo, uint64_t& qhi,
                                            uint64_t v) {
   add128(slo, shi, v, 0u);
-  add128(qlo, qhi, v * v, __umul64hi(v, v));
+  uint64_t sl, sh;
+  sq128(v, sl, sh);
+  add128(qlo, qhi, sl, sh);
 }
 
 // 192-bit a += (b_lo, b_hi, b_top)
@@ -214,7 +226,9 @@ __device__ __forceinline__ void add_moment_signed(uint64_t& slo, uint64_t& shi, 
                                                   uint64_t& qtop, int64_t v) {
   const uint64_t m = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
   add128(slo, shi, (uint64_t)v, v < 0 ? ~(uint64_t)0 : 0u);
-  add192(qlo, qhi, qtop, m * m, __umul64hi(m, m), 0u);
+  uint64_t sl, sh;
+  sq128(m, sl, sh);
+  add192(qlo, qhi, qtop, sl, sh, 0u);
 }
 
 // one queueTime emission of a task enqueued at tick a, started at tick start
