@@ -414,6 +414,12 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
     const bool live = lane < cnt;
+    // this chunk's pushed tasks, one per lane (publish c0 + lane): their
+    // statistics are accumulated once per chunk with every pushed lane at once,
+    // not run by run (a per-publish policy pushes one lane per iteration)
+    bool q_on = false;
+    int64_t q_a = 0, q_start = 0, q_done = 0;
+    uint32_t q_S = 0u, q_status = 0u;
     int64_t ca;
     int32_t cr;
     if (gen) {
@@ -659,21 +665,12 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           A.out_start[o] = start == kNever ? -1 : start;
           A.out_done[o] = done == kNever ? -1 : done;
         }
-        if (done != kNever) {
-          acc_task(acc, ca, a, start, done, S, status, hist ? L.hist : nullptr);
-          if (hist) atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - ca)], 1u);
-        } else {
-          // node-down: acked at arrival (status 4/5) or lost; a queued task that
-          // started before the crash still emitted its queueTime (:238)
-          n_short += 1;
-          if (status == 5u) acc.n5 += 1u;
-          if (status == 4u) {
-            acc.n4 += 1u;
-            if (start != kNever)
-              acc_qtime(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, acc.qq_top, acc.qmin, acc.qmax, acc.nqt,
-                        acc.nqo, start, a, hist ? L.hist : nullptr);
-          }
-        }
+        q_on = true;
+        q_a = a;
+        q_start = start;
+        q_done = done;
+        q_S = S;
+        q_status = status;
       }
 
       // 6) node k's record after the run (owner lane)
@@ -729,6 +726,24 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       }
       n_done += Lr;
       jp = jq;
+    }
+    // the chunk's statistics (also after an error ended it: the tasks pushed so far)
+    if (q_on) {
+      if (q_done != kNever) {
+        acc_task(acc, ca, q_a, q_start, q_done, q_S, q_status, hist ? L.hist : nullptr);
+        if (hist) atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(q_done - ca)], 1u);
+      } else {
+        // node-down: acked at arrival (status 4/5) or lost; a queued task that
+        // started before the crash still emitted its queueTime (:238)
+        n_short += 1;
+        if (q_status == 5u) acc.n5 += 1u;
+        if (q_status == 4u) {
+          acc.n4 += 1u;
+          if (q_start != kNever)
+            acc_qtime(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, acc.qq_top, acc.qmin, acc.qmax, acc.nqt, acc.nqo,
+                      q_start, q_a, hist ? L.hist : nullptr);
+        }
+      }
     }
   }
 
