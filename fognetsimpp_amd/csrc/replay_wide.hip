@@ -417,9 +417,10 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     // this chunk's pushed tasks, one per lane (publish c0 + lane): their
     // statistics are accumulated once per chunk with every pushed lane at once,
     // not run by run (a per-publish policy pushes one lane per iteration)
+    // (and their per-task outputs are stored then, coalesced)
     bool q_on = false;
     int64_t q_a = 0, q_start = 0, q_done = 0;
-    uint32_t q_S = 0u, q_status = 0u;
+    uint32_t q_S = 0u, q_status = 0u, q_k = 0u;
     int64_t ca;
     int32_t cr;
     if (gen) {
@@ -658,14 +659,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       if (in_run) {
         const int32_t prev = lane == jp ? tl : i - 1;
         e[i] = WideEntry{a, done, C, S, prev, lane + 1 < jq ? i + 1 : -1, escalated ? 1 : 0};
-        if (!A.no_task_out) {  // (statistics-only replays keep no per-task outputs)
-          const size_t o = tbase + (size_t)i;
-          A.out_node[o] = (int32_t)k;
-          A.out_status[o] = (uint8_t)status;
-          A.out_start[o] = start == kNever ? -1 : start;
-          A.out_done[o] = done == kNever ? -1 : done;
-        }
         q_on = true;
+        q_k = k;
         q_a = a;
         q_start = start;
         q_done = done;
@@ -727,7 +722,14 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       n_done += Lr;
       jp = jq;
     }
-    // the chunk's statistics (also after an error ended it: the tasks pushed so far)
+    // the chunk's outputs and statistics (also after an error ended it: the tasks pushed so far)
+    if (q_on && !A.no_task_out) {  // (statistics-only replays keep no per-task outputs)
+      const size_t o = tbase + (size_t)(c0 + lane);
+      A.out_node[o] = (int32_t)q_k;
+      A.out_status[o] = (uint8_t)q_status;
+      A.out_start[o] = q_start == kNever ? -1 : q_start;
+      A.out_done[o] = q_done == kNever ? -1 : q_done;
+    }
     if (q_on) {
       if (q_done != kNever) {
         acc_task(acc, ca, q_a, q_start, q_done, q_S, q_status, hist ? L.hist : nullptr);
