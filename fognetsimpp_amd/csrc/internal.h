@@ -272,10 +272,13 @@ constexpr int kGenWavesPerCu = 12;
 constexpr int32_t kNeedsWide = 0x57494445;
 
 // FOGNET_HIST_BINS rule (fognet_hip.h): whole milliseconds, log2 bins.
+// Bit length of q = ticks / 1e9 without the 64-bit division: with L the bit
+// length of ticks, 1e9 * 2^j (bit length 30 + j) is below ticks for every
+// j < L - 30 and the one j = L - 30 takes a compare.
 __device__ __forceinline__ int hist_bin(int64_t ticks) {
-  const uint64_t q = (uint64_t)ticks / 1000000000ull;
-  if (ticks < 0 || q == 0) return 0;
-  const int b = 64 - __clzll((long long)q);
+  if (ticks < 1000000000ll) return 0;
+  const int j = 34 - __clzll((long long)ticks);  // L - 30 >= 0
+  const int b = j + ((uint64_t)ticks >= (1000000000ull << j) ? 1 : 0);
   return b > FOGNET_HIST_BINS - 1 ? FOGNET_HIST_BINS - 1 : b;
 }
 

@@ -684,6 +684,11 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   __shared__ uint32_t s_tlC[NPL * kWave];  // tail cumulative service (mod 2^32)
   __shared__ uint32_t s_tlS[NPL * kWave];  // tail service seconds
   __shared__ uint32_t s_ch[3 * kWave];     // staged trace chunk: arrive lo | arrive hi | req
+  // in-loop statistics (INL): the chunk's pushed tasks, one slot per lane (publish c0 + lane): arrival at
+  // the node, completion, service << 8 | status (0: not pushed); accumulated once per chunk
+  __shared__ int64_t s_qa[INL ? kWave : 1];
+  __shared__ int64_t s_qd[INL ? kWave : 1];
+  __shared__ uint32_t s_qs[INL ? kWave : 1];
   // in-loop statistics: the histogram rows (generated mode: in the unused chunk stage)
   __shared__ uint32_t s_hl[(INL && !GEN) ? FOGNET_HIST_METRICS * FOGNET_HIST_BINS : 1];
   uint32_t* const s_hs = GEN ? s_ch : s_hl;
@@ -744,6 +749,7 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   }
   if (INL && A.hist)
     for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) s_hs[h] = 0u;
+  if constexpr (INL) s_qs[lane] = 0u;  // (each lane reads and writes only its own slot)
   __syncthreads();
   int64_t gen_carry = 0;
   if constexpr (GEN) gen_carry = (int64_t)~wave_min_u64(~ul_max) + 1;
@@ -1052,19 +1058,11 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
       if (in_run) {
         ring_k[((cnt_k & 0xFFFFu) + (uint32_t)(lane - jp)) & qmask] = ((uint64_t)a << kRingSBits) | S;
         if constexpr (INL) {
-          // the task's statistics (the fused epilogue's, rep_stats_kernel's)
-          const int64_t resp = done - ca;
-          add_moment(gacc.rs_lo, gacc.rs_hi, gacc.rq_lo, gacc.rq_hi, (uint64_t)resp);
-          gacc.rmin = min(gacc.rmin, resp);
-          gacc.rmax = max(gacc.rmax, resp);
-          if (A.hist) atomicAdd(&s_hs[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
-          if (status == 4u) {
-            gacc.n4 += 1u;
-            acc_qtime(gacc.qs_lo, gacc.qs_hi, gacc.qq_lo, gacc.qq_hi, gacc.qq_top, gacc.qmin, gacc.qmax, gacc.nqt,
-                      gacc.nqo, start, a, A.hist ? s_hs : nullptr);
-          } else {
-            gacc.n5 += 1u;
-          }
+          // the task's statistics: accumulated at the end of the chunk, with every pushed lane at
+          // once (a run pushes 1..64 lanes; S < 256 in a replay that stays in this kernel)
+          s_qa[lane] = a;
+          s_qd[lane] = done;
+          s_qs[lane] = (S << 8) | status;
         }
         if (!GEN && !(INL && A.no_task_out)) {
           // chunk bases are wave-uniform (SGPR) and the lane index a 32-bit
@@ -1125,6 +1123,27 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
       PROF(p_pk0 += pend_k == 0u; if (jq >= cnt) p_end_c++; else if (E == E_other) p_end_j++; else p_end_k++;
            prev_k = k; prev_end_h = jq < cnt && E == E_other;)
       jp = jq;
+    }
+    if constexpr (INL) {
+      // the chunk's statistics (the fused epilogue's, rep_stats_kernel's), also after an
+      // error ended it (the tasks pushed so far)
+      const uint32_t qs = s_qs[lane];
+      if (qs != 0u) {
+        const int64_t a_q = s_qa[lane], done_q = s_qd[lane];
+        const int64_t resp = done_q - ca;
+        add_moment(gacc.rs_lo, gacc.rs_hi, gacc.rq_lo, gacc.rq_hi, (uint64_t)resp);
+        gacc.rmin = min(gacc.rmin, resp);
+        gacc.rmax = max(gacc.rmax, resp);
+        if (A.hist) atomicAdd(&s_hs[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
+        if ((qs & 0xFFu) == 4u) {
+          gacc.n4 += 1u;
+          acc_qtime(gacc.qs_lo, gacc.qs_hi, gacc.qq_lo, gacc.qq_hi, gacc.qq_top, gacc.qmin, gacc.qmax, gacc.nqt,
+                    gacc.nqo, done_q - ticks_of(qs >> 8), a_q, A.hist ? s_hs : nullptr);
+        } else {
+          gacc.n5 += 1u;
+        }
+        s_qs[lane] = 0u;
+      }
     }
   }
   // drain the inline-asm prefetches before the wave retires

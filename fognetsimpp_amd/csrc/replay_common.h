@@ -134,11 +134,12 @@ __device__ __forceinline__ bool ms_raw(int64_t d, int64_t& raw) {
 }
 
 // histogram bin of a raw ms signal: whole part of the recorded double (ms)
+// (the bit length of (uint64)v for v >= 1 is v's binary exponent + 1, frexp's e)
 __device__ __forceinline__ int hist_bin_raw(int64_t raw) {
   const double v = simtime_dbl(raw);
   if (!(v >= 1.0)) return 0;
-  const uint64_t q = (uint64_t)v;
-  const int b = 64 - __clzll((long long)q);
+  int b;
+  (void)frexp(v, &b);
   return b > FOGNET_HIST_BINS - 1 ? FOGNET_HIST_BINS - 1 : b;
 }
 
