@@ -185,9 +185,11 @@ typedef struct fognet_batch_in {
     int32_t ring_capacity;    /* per-node pending-task ring of the register-resident replay kernel
                                  (N <= 256), power of two in [2, 2^15] (0 = default 2048).  Not a
                                  limit on the inputs: a replication with a node past it (or with a
-                                 service time past 2^24 / ring_capacity s) is replayed again from
-                                 the start by the wide kernel, whose per-node chains are unbounded,
-                                 inside the same call.  Only sizes the workspace and the common path. */
+                                 service time past min(2^24 / ring_capacity, 255) s, or a task
+                                 reaching its node past 2^56 ticks, the 8-B ring entry's ranges) is
+                                 replayed again from the start by the wide kernel, whose per-node
+                                 chains are unbounded, inside the same call.  Only sizes the
+                                 workspace (8 B per entry) and the common path.                  */
     const int64_t *arrive_tick;   /* [R][T] publish arrival at the broker, nondecreasing          */
     const int32_t *req_mips;      /* [R][T] MqttMsgPublish.MIPSRequired, >= 0                      */
     const int32_t *mips;          /* [R|1][N] node MIPS (> 0), CONNECT order = index order         */
