@@ -409,6 +409,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   uint32_t k = 0u;
   uint64_t k_key = 0ull;  // REF_V3: the decision's view key (busy << 32 | k)
   uint64_t reg_valid = 0ull, glob_key = 0ull;  // EXT_HIER decision cache (regions < 64)
+  uint64_t reg_dirty = 0ull;                   // regions with an advert applied since the last decision
   bool glob_valid = false;
 
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
@@ -447,6 +448,17 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       bool lerr = false;
       if (ballot(mn < t)) view_changed = true;
       while (ballot(mn < t)) {
+        if constexpr (kHier) {
+          // the regions whose view changes in this round (one advert per due lane): only
+          // their cached regional minima are dropped
+          const int gd = mn < t ? mj / (kWave * kWideGroupSlots) : -1;
+          uint64_t m = ballot(gd >= 0);
+          while (m) {
+            const int rg = __builtin_amdgcn_readlane(gd, (int)__builtin_ctzll(m));
+            reg_dirty |= 1ull << rg;
+            m &= ~ballot(gd == rg);
+          }
+        }
         if (mn < t) {
           const int j = mj;
           const int sl = j / kWave;
@@ -512,7 +524,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         // are kept until an advert changes the view (the LDS region cache, bit b of reg_valid).
         const int b = __builtin_amdgcn_readlane(cg, jp);
         if (view_changed) {
-          reg_valid = 0ull;
+          reg_valid &= ~reg_dirty;
+          reg_dirty = 0ull;
           glob_valid = false;
           view_changed = false;
         }
