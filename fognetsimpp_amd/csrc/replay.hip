@@ -682,8 +682,16 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   __shared__ uint8_t s_dvs[NPL * kWave];   //   and shifts sh1 | sh2 << 1 (sh1 <= 1, sh2 <= 31)
   __shared__ int64_t s_tld[NPL * kWave];   // tail completion tick (INT64_MIN: node never used)
   __shared__ uint32_t s_tlC[NPL * kWave];  // tail cumulative service (mod 2^32)
-  __shared__ uint32_t s_tlS[NPL * kWave];  // tail service seconds
+  __shared__ uint8_t s_tlS[NPL * kWave];   // tail service seconds (< 256 while the replication stays here)
   __shared__ uint32_t s_ch[3 * kWave];     // staged trace chunk: arrive lo | arrive hi | req
+  // replay_kernel: the chunk's per-task outputs, one slot per lane (publish c0 + lane), stored to HBM once
+  // per chunk (coalesced, one instruction per array) instead of once per run: node (N <= 256), status
+  // (0: not pushed), service seconds (start = done - S * 1e12), completion tick
+  constexpr bool kBufOut = !GEN && !INL;
+  __shared__ uint8_t s_on[kBufOut ? kWave : 1];
+  __shared__ uint8_t s_os[kBufOut ? kWave : 1];
+  __shared__ uint8_t s_oS[kBufOut ? kWave : 1];
+  __shared__ int64_t s_od[kBufOut ? kWave : 1];
   // in-loop statistics (INL): the chunk's pushed tasks, one slot per lane (publish c0 + lane): arrival at
   // the node, completion, service << 8 | status (0: not pushed); accumulated once per chunk
   __shared__ int64_t s_qa[INL ? kWave : 1];
@@ -750,6 +758,7 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   if (INL && A.hist)
     for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) s_hs[h] = 0u;
   if constexpr (INL) s_qs[lane] = 0u;  // (each lane reads and writes only its own slot)
+  if constexpr (kBufOut) s_os[lane] = 0u;
   __syncthreads();
   int64_t gen_carry = 0;
   if constexpr (GEN) gen_carry = (int64_t)~wave_min_u64(~ul_max) + 1;
@@ -1064,7 +1073,12 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
           s_qd[lane] = done;
           s_qs[lane] = (S << 8) | status;
         }
-        if (!GEN && !(INL && A.no_task_out)) {
+        if constexpr (kBufOut) {
+          s_on[lane] = (uint8_t)k;
+          s_os[lane] = (uint8_t)status;
+          s_oS[lane] = (uint8_t)S;
+          s_od[lane] = done;
+        } else if (!GEN && !(INL && A.no_task_out)) {
           // chunk bases are wave-uniform (SGPR) and the lane index a 32-bit
           // offset, so no per-lane 64-bit addresses stay live across the chunk
           const size_t o = tbase + (size_t)c0;
@@ -1077,7 +1091,8 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
           __builtin_nontemporal_store(done, (A.out_done + o) + l);
         }
       }
-      ops += (GEN || (INL && A.no_task_out)) ? 1u : 5u;  // the ring store (+ the four output stores)
+      // the ring store (+ the four output stores)
+      ops += (kBufOut || GEN || (INL && A.no_task_out)) ? 1u : 5u;
       TMARK(5)
 
       // 6) node k's state after the run
@@ -1123,6 +1138,25 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
       PROF(p_pk0 += pend_k == 0u; if (jq >= cnt) p_end_c++; else if (E == E_other) p_end_j++; else p_end_k++;
            prev_k = k; prev_end_h = jq < cnt && E == E_other;)
       jp = jq;
+    }
+    if constexpr (kBufOut) {
+      // the chunk's outputs (also after an error ended it: the tasks pushed so far)
+      const uint32_t so = s_os[lane];
+      if (ballot(so != 0u)) {
+        if (so != 0u) {
+          const size_t o = tbase + (size_t)c0;
+          const uint32_t l = lane_now();
+          const int64_t dn = s_od[lane];
+          // nontemporal: the outputs are re-read only by the epilogue, long
+          // after they left L2; the ring's head lines keep the cache
+          __builtin_nontemporal_store((int32_t)s_on[lane], (A.out_node + o) + l);
+          __builtin_nontemporal_store((uint8_t)so, (A.out_status + o) + l);
+          __builtin_nontemporal_store(dn - ticks_of(s_oS[lane]), (A.out_start + o) + l);
+          __builtin_nontemporal_store(dn, (A.out_done + o) + l);
+          s_os[lane] = 0u;
+        }
+        ops += 4u;
+      }
     }
     if constexpr (INL) {
       // the chunk's statistics (the fused epilogue's, rep_stats_kernel's), also after an
