@@ -56,10 +56,28 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
 def algorithmic_bytes_per_decision(T: int, N: int) -> float:
-    """Trace in (arrive i64 + req i32) + results out (node i32 + status u8 +
-    start i64 + done i64) + node parameters read once per replication
-    (mips i32 + dl, ul, init i64) amortised over T tasks."""
-    return 12.0 + 21.0 + N * 28.0 / T
+    """trace in (arrive i64 + req i32 = 12 B) + results out
+    (node i32 + status u8 padded to 4 + start i64 + done i64 = 24 B) + the node
+    SoA loaded and stored once per replication (2 x N x 48 B) amortised over T
+    tasks: 36.25 B at C3, 132 B at C5."""
+    return 12.0 + 24.0 + 2.0 * N * 48.0 / T
+
+
+def reference_prefix(stats_np, arrive=None):
+    """The reference's abort point over a batch (fognet_hip.h "Reference signal
+    values"): replications whose reference run ends at an overflowing queueTime
+    emission, and the decisions the reference defines (publishes with
+    arrive_tick <= abort_tick; every publish of a replication that completes).
+    ``arrive``: the device trace [R, T] (None: statistics-only, no count)."""
+    big = np.iinfo(np.int64).max
+    ab = stats_np["abort_tick"]
+    out = {"ref_aborted_replications": int((ab != big).sum()), "replications": int(len(ab))}
+    if arrive is not None:
+        abt = torch.from_numpy(np.ascontiguousarray(ab)).to(arrive.device)
+        out["ref_defined_decisions"] = int((arrive <= abt[:, None]).sum().item())
+    if (ab != big).any():
+        out["first_abort_task_median"] = int(np.median(stats_np["abort_task"][ab != big]))
+    return out
 
 
 def log(msg: str):
@@ -216,6 +234,7 @@ def main():
     achieved_gbs = R * T * bpd / replay_avg_s / 1e9
 
     traffic = None
+    valu = None
     default_policy = "EXT_HIER" if args.workload == "c5" else "REF_V3"
     prof = os.path.join(ROOT, "profiles", ("pmc_traffic" if args.workload == "c3" else f"pmc_traffic_{args.workload}")
                         + ("" if args.policy == default_policy else f"_{args.policy}") + ".json")
@@ -224,9 +243,18 @@ def main():
             pj = json.load(open(prof))
             if pj.get("config") == {"R": R, "T": T, "N": N, "ring": args.ring} and \
                     pj.get("policy", "REF_V3" if args.workload == "c3" else "EXT_HIER") == args.policy:
-                traffic = pj.get("replay_hbm_bytes_per_launch")
+                traffic = pj.get("replay_hbm_bytes_per_launch") or pj.get("hbm_bytes_per_launch")
+                if pj.get("valu_busy") is not None:
+                    # the resource the replay is bound by (SQ_ACTIVE_INST_VALU x 4 cycles / SIMD / active
+                    # cycles): the issue-side roofline beside the byte-count one
+                    valu = {"busy": pj["valu_busy"], "peak": 1.0, "unit": "VALU busy fraction",
+                            "valu_per_decision": pj.get("SQ_INSTS_VALU_per_decision"),
+                            "salu_per_decision": pj.get("SQ_INSTS_SALU_per_decision"),
+                            "hbm_bytes_per_decision": (traffic / (R * T) if traffic else None),
+                            "source": os.path.relpath(prof, ROOT)}
         except Exception:
             traffic = None
+    ref = reference_prefix(rep, trace["arrive"])
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -260,9 +288,14 @@ def main():
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": ("replay_wide_kernel (statistics inline)" if N > 256
                                     else "replay_kernel (statistics pass fused)"), "kernel_avg_ms": replay_avg_s * 1e3,
-                         "bytes_per_decision": bpd},
+                         "bytes_per_decision": bpd, "bytes_per_decision_source": "SURVEY.md §8(d)",
+                         "valu_issue": valu},
             "cpu_baseline": cpu,
             "failed_replications": failed,
+            # the reference run of a replication ends at its first overflowing queueTime emission
+            # (ComputeBrokerApp3.cc:238, no handler): what it defines is the prefix up to that tick; the
+            # decisions after it are the engine's extension (fognet_hip.h "Reference signal values")
+            "reference_abort": ref,
             "stats": {"queueTime_ms_mean": summary["queueTime_ms"].get("mean"),
                       "queueTime_overflows": summary["queueTime_ms"].get("overflow"),
                       "response_ms_mean": summary["response_ms"].get("mean"),
@@ -383,6 +416,7 @@ def bench_c4(args, ctx, dev, dist, world, rank):
                                  "profiles/pmc_valu_c4.json) replaces the HBM fraction"},
             "cpu_baseline": cpu,
             "failed_replications": summary["failed"],
+            "reference_abort": {"ref_aborted_replications": summary["ref_aborted"], "replications": args.R_total},
             "stats": {"decisions": summary["decisions"], "queueTime_ms_mean": summary["queueTime_ms"].get("mean"),
                       "response_ms_mean": summary["response_ms"].get("mean"), "energy_j": summary["energy_j"],
                       "max_pending": summary["max_pending"], "hist_counts": [int(hist[0].sum()), int(hist[1].sum())]},
@@ -457,9 +491,22 @@ def bench_c1(args, ctx, dev, dist, world, rank):
         dt = time.perf_counter() - t1
         same = bool(np.array_equal(o["node"], out.node[:reps].cpu().numpy()) and
                     np.array_equal(o["done"], out.done_tick[:reps].cpu().numpy()))
-        cpu = {"value": float(o["stats"]["n_tasks"].sum()) / dt, "unit": "decisions/s", "cores": threads,
-               "kind": "port", "sample": f"{reps} replications of the same C1 traces (v2 oracle DES), "
-                                         f"outputs identical to the device: {same}", "wall_s": dt}
+        share_value = float(o["stats"]["n_tasks"].sum()) / dt
+        model, nproc, avail, _ = host_cpu_info()
+        acc = {}
+
+        def run_all(n, th):
+            acc["o"] = oracle_lib.run_v2(arrive[:n], req[:n], 1000, np.full(n_nodes, 1000, np.int32),
+                                         np.full(n_nodes, MS), np.full(n_nodes, MS), np.full(n_nodes, 20 * MS), stop,
+                                         0.01, threads=th)
+
+        n_all, r_all, dt_all = cpu_all_cores(run_all, R, per_thread=4)
+        cpu = {"value": float(acc["o"]["stats"]["n_tasks"].sum()) / dt_all, "unit": "decisions/s", "cores": n_all,
+               "kind": "port", "sample": f"{r_all} replications of the same C1 traces (v2 oracle DES) on all {n_all} "
+                                         f"CPUs of this job's affinity mask", "wall_s": dt_all,
+               "share_value": share_value, "share_cores": threads,
+               "share_sample": f"{reps} replications, outputs identical to the device: {same}", "share_wall_s": dt,
+               "parity": same, "host_cpu": model, "host_nproc": nproc, "job_cpus": avail}
     if rank == 0:
         line = {
             "metric": METRIC, "value": decisions * args.steps / elapsed, "unit": "decisions/s", "n_gpus": world,
@@ -483,9 +530,9 @@ def bench_c1(args, ctx, dev, dist, world, rank):
 
 
 def host_cpu_info():
-    """CPU model, host logical CPUs, and the CPUs this process may run on (the
-    GPU box allots each GPU's job a share of the host: its affinity mask, or
-    OMP_NUM_THREADS when the mask shows the whole host)."""
+    """CPU model, host logical CPUs, the CPUs in this process's affinity mask,
+    and the share the GPU box allots this job (OMP_NUM_THREADS when set, else
+    the mask)."""
     model = ""
     try:
         for ln in open("/proc/cpuinfo"):
@@ -501,30 +548,50 @@ def host_cpu_info():
     return model, nproc, avail, cores
 
 
+def cpu_all_cores(run, reps_max, per_thread=8):
+    """Time ``run(reps, threads)`` (the oracle over the first ``reps``
+    replications, statistics only) on EVERY CPU of this job's affinity mask
+    ("with 1 thread, and with all cores"), one replication per
+    thread at a time, ``per_thread`` replications per thread when the sample
+    allows.  Returns (threads, reps, seconds)."""
+    _, _, avail, _ = host_cpu_info()
+    reps = min(reps_max, max(avail * per_thread, 1))
+    t0 = time.perf_counter()
+    run(reps, avail)
+    return avail, reps, time.perf_counter() - t0
+
+
 def cpu_baseline(trace, args, R, T, N, out=None):
     """Oracle (tests/oracle_lib: the CPU restatement, kind "port") timed on this
-    host on a bounded sample of the same workload: on every core this job may
-    use (one replication per thread) and on 1 thread over >= 16 replications.
-    With ``out`` (the device outputs of the timed steps) the oracle's outputs on
-    the sample are compared with the device's: ``parity``."""
+    host on a bounded sample of the same workload: on every CPU of this job's
+    affinity mask (``value``), on the job's CPU share (OMP_NUM_THREADS; also the
+    parity sample) and on 1 thread.  With ``out`` (the device outputs of the
+    timed steps) the oracle's outputs on the share sample are compared with the
+    device's: ``parity``."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
 
     reps = min(args.cpu_reps, R)
-    h = {k: trace[k][:reps].cpu().numpy() for k in ("arrive", "req", "mips", "dl", "ul", "init")}
+    keys = ("arrive", "req", "mips", "dl", "ul", "init")
+    model, nproc, avail, cores = host_cpu_info()
+    reps_all = min(R, max(reps, 8 * avail))
+    h = {k: trace[k][:reps_all].cpu().numpy() for k in keys}
     # the power model rides along when the device run used it (energy_j is part of the record compared),
     # and so do the policy and its inputs
-    pw = {k: trace[k][:reps].cpu().numpy() for k in ("p_busy", "p_idle")} if "p_busy" in trace else {}
+    pw = {k: trace[k][:reps_all].cpu().numpy() for k in ("p_busy", "p_idle")} if "p_busy" in trace else {}
     pw["policy"] = oracle_lib.POLICIES[args.policy]
     if args.policy == "EXT_HIER":
-        pw.update(region=trace["region"][:reps].cpu().numpy(), hier_threshold_s=args.hier_threshold_s,
+        pw.update(region=trace["region"][:reps_all].cpu().numpy(), hier_threshold_s=args.hier_threshold_s,
                   hier_up_tick=args.hier_up_ms * 10**9)
-    model, nproc, avail, cores = host_cpu_info()
+
+    def cut(n):
+        return {k: (v[:n] if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == reps_all else v)
+                for k, v in pw.items()}
+
     threads = max(1, min(args.cpu_threads, cores)) if args.cpu_threads > 0 else cores
     log(f"cpu baseline: {reps} replications on {threads} threads (host {nproc} CPUs, {avail} in this job's mask) ...")
     t0 = time.perf_counter()
-    o = oracle_lib.run_batch(h["arrive"], h["req"], h["mips"], h["dl"], h["ul"], h["init"], threads=threads,
-                             outputs=True, **pw)
+    o = oracle_lib.run_batch(*(h[k][:reps] for k in keys), threads=threads, outputs=True, **cut(reps))
     dt = time.perf_counter() - t0
     ok = int((o["stats"]["status"] == 0).sum())
     parity = None
@@ -537,20 +604,31 @@ def cpu_baseline(trace, args, R, T, N, out=None):
                       and np.array_equal(o["done"], out.done_tick[:reps].cpu().numpy())
                       and o["stats"].tobytes() == out.stats[: reps * _abi.REP_STATS_DTYPE.itemsize].cpu().numpy().tobytes())
     del o
+    log(f"cpu baseline: {reps_all} replications on all {avail} CPUs of the mask ...")
+    n_all, r_all, dt_all = cpu_all_cores(
+        lambda n, th: oracle_lib.run_batch(*(h[k][:n] for k in keys), threads=th, outputs=False, **cut(n)), reps_all)
     s1 = min(max(16, args.cpu_reps_1t), reps)
     t1 = time.perf_counter()
-    pw1 = {k: (v[:s1] if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == reps else v) for k, v in pw.items()}
-    oracle_lib.run_batch(h["arrive"][:s1], h["req"][:s1], h["mips"][:s1], h["dl"][:s1], h["ul"][:s1], h["init"][:s1],
-                         threads=1, outputs=False, **pw1)  # the same policy, power model and regions
+    oracle_lib.run_batch(*(h[k][:s1] for k in keys), threads=1, outputs=False, **cut(s1))  # same policy/power/regions
     dt1 = time.perf_counter() - t1
-    return {"value": reps * T / dt, "unit": "decisions/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} replications x {T} tasks x {N} nodes (rank 0's first replications of the same "
-                      f"trace), one replication per thread, {ok}/{reps} completed",
-            "wall_s": dt, "single_thread_value": s1 * T / dt1, "single_thread_sample": f"{s1} replications",
+    return {"value": r_all * T / dt_all, "unit": "decisions/s", "cores": n_all, "kind": "port",
+            "sample": f"{r_all} replications x {T} tasks x {N} nodes (rank 0's first replications of the same "
+                      f"trace, statistics only) on all {n_all} CPUs of this job's affinity mask, one replication "
+                      f"per thread at a time",
+            "wall_s": dt_all,
+            "share_value": reps * T / dt, "share_cores": threads,
+            "share_sample": f"{reps} replications with per-task outputs on the job's CPU share ({threads} threads), "
+                            f"{ok}/{reps} completed",
+            "share_wall_s": dt,
+            "single_thread_value": s1 * T / dt1, "single_thread_sample": f"{s1} replications",
             "single_thread_wall_s": dt1, "host_cpu": model, "host_nproc": nproc, "job_cpus": avail,
             "parity": parity,
             "parity_sample": f"oracle vs device outputs (node, status, start, done, stats record) on the {reps} "
-                             f"replications"}
+                             f"replications of the share sample",
+            "parity_scope": "device == oracle over the whole replay; where a replication's reference run aborts "
+                            "(reference_abort), only the prefix up to its abort_tick is the reference's -- the "
+                            "oracle continues past it exactly like the engine (the extension), and its "
+                            "stop-at-abort mode reproduces the reference's end of run (tests)"}
 
 
 if __name__ == "__main__":

@@ -22,6 +22,8 @@ FOGNET_ERR_DEVICE = 5
 FOGNET_ERR_OOM = 6
 FOGNET_ERR_CAPACITY = 7
 FOGNET_ERR_UNSUPPORTED = 8
+FOGNET_REF_ABORTED = 9  # replication status under FLAG_REF_ABORT
+FLAG_REF_ABORT = 1  # fognet_batch_in.flags
 TASK_QUEUED, TASK_STARTED, TASK_LOST = 4, 5, 9  # fognet_task_status
 
 FOGNET_POLICY_REF_V3 = 1
@@ -32,7 +34,7 @@ HIER_REGION_NODES = 1024
 TICKS_PER_SECOND = 10**12
 # fognet_v2_action (BrokerBaseApp2 decision outcome)
 V2_LOCAL, V2_FORWARD, V2_DROPPED, V2_NO_NODES = 3, 4, 5, 6
-ABI_VERSION = 9
+ABI_VERSION = 10
 HIST_METRICS = 2  # 0 queueTime, 1 response
 HIST_BINS = 64
 COMM_ID_BYTES = 128  # FOGNET_COMM_ID_BYTES
@@ -51,6 +53,7 @@ class RepStats(C.Structure):
         ("events", C.c_int64), ("max_pending", C.c_int32), ("status", C.c_int32),
         ("busy_s", C.c_int64), ("energy_j", C.c_double),
         ("queue_sq_top", C.c_uint64), ("n_qtime", C.c_int64), ("n_qtime_overflow", C.c_int64),
+        ("abort_tick", C.c_int64), ("abort_task", C.c_int64),
     ]
 
 
@@ -82,7 +85,7 @@ class JobStats(C.Structure):
         ("resp_sum", C.c_uint64 * 3), ("resp_sq", C.c_uint64 * 3),
         ("events", C.c_int64), ("max_pending", C.c_int64),
         ("busy_s", C.c_int64), ("energy_j", C.c_double),
-        ("n_qtime", C.c_int64), ("n_qtime_overflow", C.c_int64),
+        ("n_qtime", C.c_int64), ("n_qtime_overflow", C.c_int64), ("n_ref_aborted", C.c_int64),
     ]
 
 
@@ -115,7 +118,7 @@ class BatchIn(C.Structure):
         ("dl_tick", C.c_void_p), ("ul_tick", C.c_void_p), ("init_adv_tick", C.c_void_p),
         ("p_busy_w", C.c_void_p), ("p_idle_w", C.c_void_p), ("down_tick", C.c_void_p),
         ("region", C.c_void_p), ("hier_up_tick", C.c_int64), ("hier_threshold_s", C.c_int32),
-        ("pad_hier", C.c_int32),
+        ("flags", C.c_int32),
     ]
 
 

@@ -111,6 +111,7 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a, boo
     return fail(c, FOGNET_ERR_UNSUPPORTED, "the power model assumes nodes that stay up (down_tick with p_busy_w)");
   if (in->node_stride != 0 && in->node_stride != in->N)
     return fail(c, FOGNET_ERR_ARG, "node_stride must be 0 or N");
+  if (in->flags & ~FOGNET_FLAG_REF_ABORT) return fail(c, FOGNET_ERR_ARG, "unknown flags");
   int q = in->ring_capacity ? in->ring_capacity : kDefaultRing;
   if (q < 2 || (q & (q - 1)) != 0 || q > (1 << 15)) return fail(c, FOGNET_ERR_ARG, "ring_capacity must be a power of two in [2, 2^15]");
   int qlog = 0;
@@ -141,6 +142,7 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a, boo
   a->p_busy = in->p_busy_w;
   a->p_idle = in->p_idle_w;
   a->down = in->down_tick;
+  a->ref_abort = (in->flags & FOGNET_FLAG_REF_ABORT) ? 1 : 0;
   if (in->policy == FOGNET_POLICY_EXT_HIER) {
     a->region = in->region;
     a->hier_up = in->hier_up_tick;
@@ -185,6 +187,7 @@ const char* fognet_status_string(int s) {
     case FOGNET_ERR_OOM: return "out of device memory";
     case FOGNET_ERR_CAPACITY: return "capacity exceeded";
     case FOGNET_ERR_UNSUPPORTED: return "unsupported configuration";
+    case FOGNET_REF_ABORTED: return "the reference run aborts (queueTime simtime overflow)";
   }
   return "unknown status";
 }
@@ -714,6 +717,7 @@ void fognet_job_stats_merge(fognet_job_stats* a, const fognet_job_stats* b) {
   if (b->queue_max_raw > a->queue_max_raw) a->queue_max_raw = b->queue_max_raw;
   a->n_qtime += b->n_qtime;
   a->n_qtime_overflow += b->n_qtime_overflow;
+  a->n_ref_aborted += b->n_ref_aborted;
   if (b->resp_min_ticks < a->resp_min_ticks) a->resp_min_ticks = b->resp_min_ticks;
   if (b->resp_max_ticks > a->resp_max_ticks) a->resp_max_ticks = b->resp_max_ticks;
   if (b->max_pending > a->max_pending) a->max_pending = b->max_pending;
@@ -743,6 +747,7 @@ void fognet_job_stats_add_rep(fognet_job_stats* a, const fognet_rep_stats* s) {
   b.queue_max_raw = s->queue_max_raw;
   b.n_qtime = s->n_qtime;
   b.n_qtime_overflow = s->n_qtime_overflow;
+  b.n_ref_aborted = s->abort_tick != INT64_MAX ? 1 : 0;
   b.resp_min_ticks = s->resp_min_ticks;
   b.resp_max_ticks = s->resp_max_ticks;
   b.max_pending = s->max_pending;

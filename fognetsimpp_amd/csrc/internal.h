@@ -261,6 +261,8 @@ struct ReplayArgs {
   // the wave's replay progress, read by the other waves of its SIMD to set
   // their issue priority (least progress first).  Nullable.
   uint32_t* board;
+  // FOGNET_FLAG_REF_ABORT: a replication with an abort point gets status FOGNET_REF_ABORTED
+  int32_t ref_abort;
 };
 constexpr size_t kBoardWords = (size_t)1 << 17;  // 8 XCC x 8 SE x 2 SH x 16 CU x 4 SIMD x 16 slots
 

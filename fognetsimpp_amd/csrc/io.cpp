@@ -445,6 +445,8 @@ int fognet_write_sca(const char* path, const char* run_id, const char* network, 
   fprintf(f, "scalar %s \t\"makespan s\" \t%s\n", nodes.c_str(),
           job->n_tasks > 0 ? simtime_str(job->last_tick).c_str() : "-nan");
   fprintf(f, "scalar %s \t\"queueTime simtime overflows\" \t%lld\n", nodes.c_str(), (long long)job->n_qtime_overflow);
+  fprintf(f, "scalar %s \t\"replications the reference aborts (queueTime overflow)\" \t%lld\n", nodes.c_str(),
+          (long long)job->n_ref_aborted);
   const Moments q = moments(job->n_qtime, job->queue_sum, job->queue_sq, job->queue_min_raw, job->queue_max_raw, true, true);
   const Moments r = moments(job->n_tasks, job->resp_sum, job->resp_sq, job->resp_min_ticks, job->resp_max_ticks, false,
                             false);

@@ -586,9 +586,14 @@ __device__ __forceinline__ int64_t scan_max_level(int64_t v, int64_t& tmp) {
 // before any is used.  dl_of(k): node k's downlink latency.
 // kPerTask = false: busy seconds, per-node service and `last` are not
 // accumulated per task (the fused epilogue takes them from the node tails).
+// ab_tick/ab_task (LDS, one slot per thread, indexed by i0): the abort point
+// (replay_common.h AbortPt) is kept there, a read-modify-write only on an
+// overflow, which is rare, instead of in registers (the fused epilogue has
+// none to spare).
 template <int UNROLL, bool kPerTask = true, class DlOf>
 __device__ __forceinline__ void stats_accumulate(const ReplayArgs& A, size_t tbase, int n, int i0, int stride, Acc& a,
-                                                 unsigned long long* s_busy, uint32_t* s_hist, DlOf dl_of) {
+                                                 unsigned long long* s_busy, uint32_t* s_hist, DlOf dl_of,
+                                                 int64_t* ab_tick, int32_t* ab_task) {
   const bool energy = kPerTask && A.p_busy != nullptr;
   const bool hist = A.hist != nullptr;
   for (int ib = i0; ib < n; ib += stride * UNROLL) {
@@ -622,8 +627,9 @@ __device__ __forceinline__ void stats_accumulate(const ReplayArgs& A, size_t tba
         if (hist) atomicAdd(&s_hist[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
         if (stt[u] == 4u) {  // queueTime emission (ComputeBrokerApp3.cc:238), enqueued at its arrival
           a.n4 += 1u;
-          acc_qtime(a.qs_lo, a.qs_hi, a.qq_lo, a.qq_hi, a.qq_top, a.qmin, a.qmax, a.nqt, a.nqo, st0[u],
-                    t[u] + dl_of(k), hist ? s_hist : nullptr);
+          if (!acc_qtime(a.qs_lo, a.qs_hi, a.qq_lo, a.qq_hi, a.qq_top, a.qmin, a.qmax, a.nqt, a.nqo, st0[u],
+                         t[u] + dl_of(k), hist ? s_hist : nullptr))
+            abort_min(ab_tick[i0], ab_task[i0], st0[u], ib + u * stride);
         } else {
           a.n5 += 1u;
         }
@@ -699,6 +705,13 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   __shared__ uint32_t s_qs[INL ? kWave : 1];
   // in-loop statistics: the histogram rows (generated mode: in the unused chunk stage)
   __shared__ uint32_t s_hl[(INL && !GEN) ? FOGNET_HIST_METRICS * FOGNET_HIST_BINS : 1];
+  // in-loop statistics: the abort point so far (replay_common.h Acc::ab_*), kept in LDS (an overflow is
+  // rare; loop-carried registers are not)
+  __shared__ int64_t s_ab_tick[1];
+  __shared__ int32_t s_ab_task[1];
+  // fused epilogue: per-lane abort-point slots (i64 tick + i32 task), in s_dvm when it holds them
+  constexpr bool kAbInDvm = NPL * kWave * sizeof(uint32_t) >= kWave * (sizeof(int64_t) + sizeof(int32_t));
+  __shared__ int64_t s_abx[(kBufOut && !kAbInDvm) ? kWave * 3 / 2 : 1];
   uint32_t* const s_hs = GEN ? s_ch : s_hl;
 
   const int T = A.T, N = A.N;
@@ -757,7 +770,13 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   }
   if (INL && A.hist)
     for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) s_hs[h] = 0u;
-  if constexpr (INL) s_qs[lane] = 0u;  // (each lane reads and writes only its own slot)
+  if constexpr (INL) {
+    s_qs[lane] = 0u;  // (each lane reads and writes only its own slot)
+    if (lane == 0) {
+      s_ab_tick[0] = INT64_MAX;
+      s_ab_task[0] = INT32_MAX;
+    }
+  }
   if constexpr (kBufOut) s_os[lane] = 0u;
   __syncthreads();
   int64_t gen_carry = 0;
@@ -1162,6 +1181,8 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
       // the chunk's statistics (the fused epilogue's, rep_stats_kernel's), also after an
       // error ended it (the tasks pushed so far)
       const uint32_t qs = s_qs[lane];
+      bool ovf = false;  // this lane's queueTime emission overflows: the reference's abort point
+      int64_t st_o = 0;
       if (qs != 0u) {
         const int64_t a_q = s_qa[lane], done_q = s_qd[lane];
         const int64_t resp = done_q - ca;
@@ -1171,12 +1192,17 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
         if (A.hist) atomicAdd(&s_hs[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
         if ((qs & 0xFFu) == 4u) {
           gacc.n4 += 1u;
-          acc_qtime(gacc.qs_lo, gacc.qs_hi, gacc.qq_lo, gacc.qq_hi, gacc.qq_top, gacc.qmin, gacc.qmax, gacc.nqt,
-                    gacc.nqo, done_q - ticks_of(qs >> 8), a_q, A.hist ? s_hs : nullptr);
+          st_o = done_q - ticks_of(qs >> 8);
+          ovf = !acc_qtime(gacc.qs_lo, gacc.qs_hi, gacc.qq_lo, gacc.qq_hi, gacc.qq_top, gacc.qmin, gacc.qmax,
+                           gacc.nqt, gacc.nqo, st_o, a_q, A.hist ? s_hs : nullptr);
         } else {
           gacc.n5 += 1u;
         }
         s_qs[lane] = 0u;
+      }
+      if (ballot(ovf)) {  // rare: the chunk's earliest overflowing emission (ticks >= 0), then the lowest index
+        const AbortPt m = wave_min_abort(ovf ? AbortPt{st_o, c0 + lane} : abort_none());
+        if (lane == 0) abort_min(s_ab_tick[0], s_ab_task[0], m.tick, m.task);
       }
     }
   }
@@ -1250,7 +1276,7 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
       gacc = wave_merge(gacc);
       __syncthreads();
       fognet_rep_stats* S = A.out_stats + r;
-      if (lane == 0) write_rep_stats(S, gacc);
+      if (lane == 0) write_rep_stats(S, gacc, AbortPt{s_ab_tick[0], s_ab_task[0]}, A.ref_abort);
       stats_finish(A, r, n_done > 0 ? gacc.last : 0, S, e_busy, e_e, s_hs, lane, kWave);
     }
   } else if (A.fuse_stats && A.out_stats && err != kNeedsWide) {
@@ -1281,16 +1307,23 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
     }
     if (A.hist)
       for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) e_hist[h] = 0u;
+    // the abort point per lane: in the loop's division table where it is large enough (dead now)
+    int64_t* const ab_t = reinterpret_cast<int64_t*>(kAbInDvm ? (void*)s_dvm : (void*)s_abx);
+    int32_t* const ab_k = reinterpret_cast<int32_t*>(ab_t + kWave);
+    ab_t[lane] = INT64_MAX;
+    ab_k[lane] = INT32_MAX;
     __syncthreads();
     if (from_tails)
       stats_accumulate<4, false>(A, tbase, (int)n_done, lane, kWave, acc, e_busy, e_hist,
-                                 [&](int k) { return s_dl[k]; });
+                                 [&](int k) { return s_dl[k]; }, ab_t, ab_k);
     else
-      stats_accumulate<4>(A, tbase, (int)n_done, lane, kWave, acc, e_busy, e_hist, [&](int k) { return s_dl[k]; });
+      stats_accumulate<4>(A, tbase, (int)n_done, lane, kWave, acc, e_busy, e_hist, [&](int k) { return s_dl[k]; },
+                          ab_t, ab_k);
+    const AbortPt ab = wave_min_abort(AbortPt{ab_t[lane], ab_k[lane]});  // (each lane's own slot)
     acc = wave_merge(acc);
     __syncthreads();
     fognet_rep_stats* S = A.out_stats + r;
-    if (lane == 0) write_rep_stats(S, acc);
+    if (lane == 0) write_rep_stats(S, acc, ab, A.ref_abort);
     stats_finish(A, r, n_done > 0 ? acc.last : 0, S, e_busy, e_e, e_hist, lane, kWave);
   }
 #endif
@@ -1339,6 +1372,8 @@ constexpr int kStatThreads = 256;
 __global__ __launch_bounds__(kStatThreads) void rep_stats_kernel(ReplayArgs A) {
   const int r = blockIdx.x;
   __shared__ Acc s_acc[kStatThreads];
+  __shared__ int64_t s_abt[kStatThreads];  // per thread: the abort point (AbortPt), rare updates
+  __shared__ int32_t s_abk[kStatThreads];
   __shared__ unsigned long long s_busy[kWave * kMaxNodesPerLane];  // service seconds per node
   __shared__ double s_e[kWave * kMaxNodesPerLane];
   __shared__ uint32_t s_hist[FOGNET_HIST_METRICS * FOGNET_HIST_BINS];
@@ -1348,17 +1383,22 @@ __global__ __launch_bounds__(kStatThreads) void rep_stats_kernel(ReplayArgs A) {
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   for (int j = threadIdx.x; j < kWave * kMaxNodesPerLane; j += kStatThreads) s_busy[j] = 0ull;
   for (int h = threadIdx.x; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kStatThreads) s_hist[h] = 0u;
+  s_abt[threadIdx.x] = INT64_MAX;
+  s_abk[threadIdx.x] = INT32_MAX;
   __syncthreads();
   Acc a = acc_identity();
   stats_accumulate<2>(A, tbase, n, threadIdx.x, kStatThreads, a, s_busy, s_hist,
-                      [&](int k) { return A.dl[nbase + k]; });
+                      [&](int k) { return A.dl[nbase + k]; }, s_abt, s_abk);
   s_acc[threadIdx.x] = a;
   __syncthreads();
   for (int w = kStatThreads / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) acc_merge(s_acc[threadIdx.x], s_acc[threadIdx.x + w]);
+    if ((int)threadIdx.x < w) {
+      acc_merge(s_acc[threadIdx.x], s_acc[threadIdx.x + w]);
+      abort_min(s_abt[threadIdx.x], s_abk[threadIdx.x], s_abt[threadIdx.x + w], s_abk[threadIdx.x + w]);
+    }
     __syncthreads();
   }
-  if (threadIdx.x == 0) write_rep_stats(S, s_acc[0]);
+  if (threadIdx.x == 0) write_rep_stats(S, s_acc[0], AbortPt{s_abt[0], s_abk[0]}, A.ref_abort);
   stats_finish(A, r, n > 0 ? s_acc[0].last : 0, S, s_busy, s_e, s_hist, threadIdx.x, kStatThreads);
 }
 

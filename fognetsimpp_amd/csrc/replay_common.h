@@ -176,6 +176,32 @@ __device__ __forceinline__ uint32_t udiv(uint32_t n, UDiv q) {
   return (t + ((n - t) >> (q.sh & 0xFFu))) >> (q.sh >> 8);
 }
 
+// The reference's abort point: the earliest (tick, then task index) queueTime
+// emission that overflows (ComputeBrokerApp3.cc:238 throws and nothing up to
+// :84-86 catches, so OMNeT++ ends the run there).  Kept apart from Acc so the
+// register-bound statistics loops keep their footprint.
+struct AbortPt {
+  int64_t tick;  // INT64_MAX: none
+  int32_t task;  // INT32_MAX: none
+};
+
+__device__ __forceinline__ AbortPt abort_none() { return AbortPt{INT64_MAX, INT32_MAX}; }
+
+__device__ __forceinline__ void abort_min(int64_t& tick, int32_t& task, int64_t t, int32_t k) {
+  if (t < tick || (t == tick && k < task)) {
+    tick = t;
+    task = k;
+  }
+}
+__device__ __forceinline__ void abort_min(AbortPt& a, const AbortPt& b) { abort_min(a.tick, a.task, b.tick, b.task); }
+
+// Minimum over the 64 lanes (all active); ticks are >= 0.
+__device__ __forceinline__ AbortPt wave_min_abort(AbortPt a) {
+  const uint64_t mt = wave_min_u64((uint64_t)a.tick);
+  const uint32_t mk = wave_min_u32((uint64_t)a.tick == mt ? (uint32_t)a.task : ~0u);
+  return AbortPt{(int64_t)mt, (int32_t)mk};
+}
+
 __device__ __forceinline__ Acc acc_identity() {
   Acc a = {};
   a.qmin = a.rmin = INT64_MAX;
@@ -232,8 +258,9 @@ __device__ __forceinline__ void add_moment_signed(uint64_t& slo, uint64_t& shi, 
   add192(qlo, qhi, qtop, sl, sh, 0u);
 }
 
-// one queueTime emission of a task enqueued at tick a, started at tick start
-__device__ __forceinline__ void acc_qtime(uint64_t& qs_lo, uint64_t& qs_hi, uint64_t& qq_lo, uint64_t& qq_hi,
+// one queueTime emission of a task enqueued at tick a, started at tick start;
+// false: the emission overflows (the reference throws there: its abort point)
+__device__ __forceinline__ bool acc_qtime(uint64_t& qs_lo, uint64_t& qs_hi, uint64_t& qq_lo, uint64_t& qq_hi,
                                           uint64_t& qq_top, int64_t& qmin, int64_t& qmax, uint64_t& nqt,
                                           uint64_t& nqo, int64_t start, int64_t a, uint32_t* hist) {
   int64_t raw;
@@ -243,9 +270,18 @@ __device__ __forceinline__ void acc_qtime(uint64_t& qs_lo, uint64_t& qs_hi, uint
     qmax = max(qmax, raw);
     nqt += 1u;
     if (hist) atomicAdd(&hist[hist_bin_raw(raw)], 1u);
-  } else {
-    nqo += 1u;
+    return true;
   }
+  nqo += 1u;
+  return false;
+}
+
+// the same into an Acc, with the abort point (task: the task's index)
+__device__ __forceinline__ void acc_qtime(Acc& acc, AbortPt& ab, int64_t start, int64_t a, int32_t task,
+                                          uint32_t* hist) {
+  if (!acc_qtime(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, acc.qq_top, acc.qmin, acc.qmax, acc.nqt, acc.nqo, start,
+                 a, hist))
+    abort_min(ab.tick, ab.task, start, task);
 }
 
 __device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
@@ -267,9 +303,9 @@ __device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
 
 // One task's contribution: response = done - publish tick t; queued tasks
 // (status 4) also their queueTime emission (enqueued at arrival a, started at
-// start).  hist: the queueTime histogram row (nullable).
-__device__ __forceinline__ void acc_task(Acc& acc, int64_t t, int64_t a, int64_t start, int64_t done, uint32_t S,
-                                         uint32_t status, uint32_t* hist) {
+// start).  hist: the queueTime histogram row (nullable).  task: its index.
+__device__ __forceinline__ void acc_task(Acc& acc, AbortPt& ab, int64_t t, int64_t a, int64_t start, int64_t done,
+                                         uint32_t S, uint32_t status, int32_t task, uint32_t* hist) {
   acc.busy += S;
   const int64_t resp = done - t;
   add_moment(acc.rs_lo, acc.rs_hi, acc.rq_lo, acc.rq_hi, (uint64_t)resp);
@@ -278,8 +314,7 @@ __device__ __forceinline__ void acc_task(Acc& acc, int64_t t, int64_t a, int64_t
   acc.last = max(acc.last, done);
   if (status == 4u) {
     acc.n4 += 1u;
-    acc_qtime(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, acc.qq_top, acc.qmin, acc.qmax, acc.nqt, acc.nqo, start, a,
-              hist);
+    acc_qtime(acc, ab, start, a, task, hist);
   } else {
     acc.n5 += 1u;
   }
@@ -320,7 +355,12 @@ __device__ __forceinline__ Acc wave_merge(Acc a) {
   return a;
 }
 
-__device__ __forceinline__ void write_rep_stats(fognet_rep_stats* S, const Acc& b) {
+// (ref_abort: FOGNET_FLAG_REF_ABORT; S->status already holds the replay's status)
+__device__ __forceinline__ void write_rep_stats(fognet_rep_stats* S, const Acc& b, const AbortPt& ab,
+                                                bool ref_abort) {
+  S->abort_tick = ab.tick;
+  S->abort_task = ab.tick == INT64_MAX ? -1 : (int64_t)ab.task;
+  if (ref_abort && ab.tick != INT64_MAX && S->status == FOGNET_OK) S->status = FOGNET_REF_ABORTED;
   S->n_queued = (int64_t)b.n4;
   S->n_started = (int64_t)b.n5;
   S->last_tick = b.last;

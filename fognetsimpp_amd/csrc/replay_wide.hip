@@ -389,6 +389,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   lane_min(L, lane, mn, mj, mk);
   int64_t mw = kNever;  // REF_V3 run horizon: this lane's smallest node_w
   Acc acc = acc_identity();
+  AbortPt ab = abort_none();  // the reference's abort point (replay_common.h)
   uint32_t max_pend = 0u;  // over this lane's nodes
   int n_short = 0;         // tasks of this lane's nodes that never complete (node-down)
   int64_t prev_t = INT64_MIN;
@@ -745,7 +746,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     }
     if (q_on) {
       if (q_done != kNever) {
-        acc_task(acc, ca, q_a, q_start, q_done, q_S, q_status, hist ? L.hist : nullptr);
+        acc_task(acc, ab, ca, q_a, q_start, q_done, q_S, q_status, c0 + lane, hist ? L.hist : nullptr);
         if (hist) atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(q_done - ca)], 1u);
       } else {
         // node-down: acked at arrival (status 4/5) or lost; a queued task that
@@ -754,9 +755,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         if (q_status == 5u) acc.n5 += 1u;
         if (q_status == 4u) {
           acc.n4 += 1u;
-          if (q_start != kNever)
-            acc_qtime(acc.qs_lo, acc.qs_hi, acc.qq_lo, acc.qq_hi, acc.qq_top, acc.qmin, acc.qmax, acc.nqt, acc.nqo,
-                      q_start, q_a, hist ? L.hist : nullptr);
+          if (q_start != kNever) acc_qtime(acc, ab, q_start, q_a, c0 + lane, hist ? L.hist : nullptr);
         }
       }
     }
@@ -766,6 +765,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 
   // ---- per-replication record (the fields replay_kernel + its epilogue write)
   acc = wave_merge(acc);
+  ab = wave_min_abort(ab);
   const uint32_t mp = ~wave_min_u32(~max_pend);
   int shorts = n_short;
   for (int m = kWave / 2; m > 0; m >>= 1) shorts += __shfl_xor(shorts, m, kWave);
@@ -777,7 +777,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     // initial adverts + publish, arrival, release, advert per task (publish,
     // arrival for a task a crash keeps from completing)
     S->events = 2 * (int64_t)N + 4 * (int64_t)n_done - 2 * (int64_t)shorts;
-    write_rep_stats(S, acc);
+    write_rep_stats(S, acc, ab, A.ref_abort);
   }
   // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12)
   // with B_j = node j's service seconds (its tail's cumulative sum), summed in node order

@@ -118,6 +118,7 @@ __device__ __forceinline__ void job_merge(fognet_job_stats& a, const fognet_job_
   a.queue_max_raw = max(a.queue_max_raw, b.queue_max_raw);
   a.n_qtime += b.n_qtime;
   a.n_qtime_overflow += b.n_qtime_overflow;
+  a.n_ref_aborted += b.n_ref_aborted;
   a.resp_min_ticks = min(a.resp_min_ticks, b.resp_min_ticks);
   a.resp_max_ticks = max(a.resp_max_ticks, b.resp_max_ticks);
   a.max_pending = max(a.max_pending, b.max_pending);
@@ -152,6 +153,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_kernel(const fognet_rep_st
     a.queue_max_raw = max(a.queue_max_raw, s.queue_max_raw);
     a.n_qtime += s.n_qtime;
     a.n_qtime_overflow += s.n_qtime_overflow;
+    a.n_ref_aborted += s.abort_tick != INT64_MAX ? 1 : 0;
     a.resp_min_ticks = min(a.resp_min_ticks, s.resp_min_ticks);
     a.resp_max_ticks = max(a.resp_max_ticks, s.resp_max_ticks);
     a.max_pending = max(a.max_pending, (int64_t)s.max_pending);

@@ -228,7 +228,7 @@ def as_device_trace(trace: dict, device) -> dict:
 
 def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_capacity: int = 0,
               stream=None, stage: str = "all", policy: str | int = "REF_V3", hist: bool = False,
-              hier_threshold_s: int = 60, hier_up_tick: int = 20 * 10**9) -> BatchResult:
+              hier_threshold_s: int = 60, hier_up_tick: int = 20 * 10**9, ref_abort: bool = False) -> BatchResult:
     """Enqueue R trace replays (fognet_run_batch_dev) on the current stream.
 
     ``trace``: device tensors arrive/req [R, T], node params mips/dl/ul/init
@@ -242,7 +242,10 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
     [R, T], see :func:`mobility_regions`; escalation above
     ``hier_threshold_s`` busy seconds, extra hop ``hier_up_tick``); the two
     extensions are not in the reference.  ``hist``: allocate the job
-    histogram when ``out`` is None.
+    histogram when ``out`` is None.  ``ref_abort`` (FOGNET_FLAG_REF_ABORT): a
+    replication the reference run would end at a queueTime overflow gets status
+    FOGNET_REF_ABORTED (its abort point, ``abort_tick``/``abort_task``, is in
+    every record either way).
     """
     arrive, req = trace["arrive"], trace["req"]
     R, T = arrive.shape
@@ -269,7 +272,8 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
     bi = _abi.BatchIn(R, T, N, pol, stride, ring_capacity,
                       _ptr(arrive), _ptr(req), _ptr(mips), _ptr(trace["dl"]), _ptr(trace["ul"]),
                       _ptr(trace["init"]), _ptr(trace.get("p_busy")), _ptr(trace.get("p_idle")), _ptr(down),
-                      _ptr(region), int(hier_up_tick), int(hier_threshold_s), 0)
+                      _ptr(region), int(hier_up_tick), int(hier_threshold_s),
+                      _abi.FLAG_REF_ABORT if ref_abort else 0)
     bo = _abi.BatchOut(_ptr(out.node), _ptr(out.status), _ptr(out.start_tick), _ptr(out.done_tick),
                        _ptr(out.stats), _ptr(out.node_energy), _ptr(out.hist))
     s = C.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(arrive.device)
@@ -467,6 +471,8 @@ def summarize(job) -> dict:
         "max_pending": int(job["max_pending"]),
         "busy_s": int(job["busy_s"]),
         "energy_j": float(job["energy_j"]),
+        # replications the reference run would have ended at a queueTime overflow (fognet_hip.h)
+        "ref_aborted": int(job["n_ref_aborted"]),
     }
 
 

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define FOGNET_ABI_VERSION 9
+#define FOGNET_ABI_VERSION 10
 #define FOGNET_TICKS_PER_SECOND 1000000000000LL
 
 /* Latency histograms (device-side statistics, summed over replications; the
@@ -62,12 +62,24 @@ typedef enum fognet_status {
     FOGNET_ERR_ARG = 1,         /* invalid argument / precondition (see fognet_run_batch)            */
     FOGNET_ERR_NO_NODES = 2,    /* n == 0: BrokerBaseApp3.cc:268 reads brokers[0] first (UB)           */
     FOGNET_ERR_DIV0 = 3,        /* advertised MIPS of node 0 is 0: BrokerBaseApp3.cc:268 SIGFPE        */
-    FOGNET_ERR_STATE = 4,       /* selfMsg already scheduled: ComputeBrokerApp3.cc:301 cRuntimeError   */
+    FOGNET_ERR_STATE = 4,       /* scheduleAt on a scheduled selfMsg (ComputeBrokerApp3.cc:301): the
+                                   reference's cRuntimeError is swallowed by processPacket's catch
+                                   (:277,317), leaving the node busy with no completion pending;
+                                   unreachable under the fognet_batch_in preconditions            */
     FOGNET_ERR_DEVICE = 5,      /* HIP runtime failure or no gfx950 device                             */
     FOGNET_ERR_OOM = 6,
     FOGNET_ERR_CAPACITY = 7,    /* v2 queue_capacity exceeded, or an advertised busy time past 2^32 - 1 s */
-    FOGNET_ERR_UNSUPPORTED = 8  /* configuration not implemented (e.g. N > 256, unknown policy)        */
+    FOGNET_ERR_UNSUPPORTED = 8, /* configuration not implemented (e.g. N > 256, unknown policy)        */
+    FOGNET_REF_ABORTED = 9      /* replication status under FOGNET_FLAG_REF_ABORT: the reference run ends
+                                   at a queueTime emission that overflows (ComputeBrokerApp3.cc:238; see
+                                   "Reference signal values"); outputs are still written in full     */
 } fognet_status;
+
+/* fognet_batch_in.flags */
+#define FOGNET_FLAG_REF_ABORT 1 /* a replication the reference would abort (abort_tick set) gets status
+                                   FOGNET_REF_ABORTED, so job reductions count it as failed, as the
+                                   reference records no result for it; without the flag its status is
+                                   FOGNET_OK and the continuation past the abort is the extension's */
 
 typedef enum fognet_policy {
     FOGNET_POLICY_REF_V2 = 2,   /* BrokerBaseApp2: local-first, then the LAST node whose advertised MIPS
@@ -124,11 +136,22 @@ typedef enum fognet_v2_action {
  *              timeCreated a simtime_t (mqttApp2.cc:260,272,282): raw = toInt64(d * 1000.0);
  *   delay      simTime() - creationTime (BrokerBaseApp3.cc:143): raw = d ticks (s).
  * An emission whose product leaves the int64 range (a queue time above ~9223 s)
- * throws in the reference: at queueTime the run aborts (releaseResource has no
- * handler), at the user signals the exception is swallowed by mqttApp2's catch
- * and the emission is lost.  Such emissions are counted (n_qtime_overflow,
- * fognet_moments.overflow) and left out of the moments and histograms; the replay
- * itself goes on.  Signed sums are two's complement. */
+ * throws in the reference.  At the user signals the exception is swallowed by
+ * mqttApp2's catch and the emission is lost (fognet_moments.overflow).  At
+ * queueTime it ENDS THE REFERENCE RUN: ComputeBrokerApp3::releaseResource emits
+ * at ComputeBrokerApp3.cc:238 before it dequeues the next task (:240-250) and
+ * nothing up to handleMessageWhenUp (:84-86) catches, so OMNeT++ stops at that
+ * RELEASERESOURCE event.  The engine reports that point per replication
+ * (fognet_rep_stats.abort_tick / abort_task) and, as a builder-defined
+ * EXTENSION of the reference, keeps replaying past it: the emission is counted
+ * (n_qtime_overflow) and left out of the moments and histograms, and the node
+ * dequeues its next task as if the emit had returned.  What the reference
+ * defines of an aborted replication is the prefix before that event: every
+ * publish with arrive_tick <= abort_tick is decided (trace publishes precede
+ * same-tick dynamic events), and every arrival, start and
+ * completion at a tick < abort_tick has happened.  Everything later, and every
+ * statistic that includes it, is the extension's.  Signed sums are two's
+ * complement. */
 
 /* Per-replication statistics.  Exact integer moments, split into uint64 limbs
  * ([lo, hi, top] = bits 0-63, 64-127, 128-191) so results are bit-reproducible. */
@@ -155,6 +178,14 @@ typedef struct fognet_rep_stats {
     uint64_t queue_sq_top;    /* bits 128-191 of the queueTime sum of squares                     */
     int64_t n_qtime;          /* queueTime emissions in the moments (queued tasks that started)   */
     int64_t n_qtime_overflow; /* queueTime emissions the reference cannot make (simtime overflow) */
+    /* The reference's abort point (see "Reference signal values"): the RELEASERESOURCE
+     * tick at which the first overflowing queueTime emission throws and the index of the
+     * task it would have started; INT64_MAX / -1 when the reference run completes.
+     * Several overflowing emissions at that tick (different nodes): the lowest task index
+     * (the reference throws at the first in FES insertion order, which this does not
+     * resolve; the tick and so the reference-defined prefix are the same). */
+    int64_t abort_tick;
+    int64_t abort_task;
 } fognet_rep_stats;
 
 /* Job-level statistics: the exact sum of any set of fognet_rep_stats.  Sums
@@ -175,6 +206,7 @@ typedef struct fognet_job_stats {
                                  order across GPUs; differs from another sharding's sum by
                                  rounding only (within 1e-9 relative)                            */
     int64_t n_qtime, n_qtime_overflow;
+    int64_t n_ref_aborted;    /* replications the reference would have aborted (abort_tick set)  */
 } fognet_job_stats;
 
 /* R trace replays of T tasks over N fog nodes, SoA, row-major [R][T] / [R|1][N]. */
@@ -213,7 +245,7 @@ typedef struct fognet_batch_in {
     const int32_t *region;
     int64_t hier_up_tick;
     int32_t hier_threshold_s;
-    int32_t pad_hier;
+    int32_t flags;            /* FOGNET_FLAG_* (0: none)                                           */
 } fognet_batch_in;
 
 /* Per-task status (fognet_batch_out.status). */

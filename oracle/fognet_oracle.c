@@ -26,6 +26,8 @@
 
 enum { EV_PUBLISH = 0, EV_ADVERT = 1, EV_TASK = 2, EV_SELF = 3, EV_ACK_AT_BROKER = 4, EV_ACK_AT_USER = 5, EV_CRASH = 6 };
 enum { KIND_ADVERTISEMIPS = 1, KIND_RELEASERESOURCE = 2 }; /* ComputeBrokerApp3.h selfMsg kinds */
+/* internal: the reference run ended at a queueTime throw (stop_at_ref_abort) */
+#define ORC_STOPPED (-100)
 
 typedef struct {
     int64_t tick;
@@ -313,7 +315,15 @@ static int node_release(sim_t *s, int32_t k) {
             s->st.n_qtime++;
             hist_add_raw(s, 0, qt);
         } else {
+            /* cRuntimeError out of emit(): nothing catches it before the kernel
+             * (:84-86), the reference run ends here.  Events come in tick order, so the
+             * first overflow has the abort tick; at that tick the lowest task index. */
             s->st.n_qtime_overflow++;
+            if (s->now < s->st.abort_tick || (s->now == s->st.abort_tick && h->task < s->st.abort_task)) {
+                s->st.abort_tick = s->now;
+                s->st.abort_task = h->task;
+            }
+            if (s->in->stop_at_ref_abort) return ORC_STOPPED;
         }
         nd->currentTask = *h; /* :240-244 */
         nd->qh = (nd->qh + 1) % nd->qcap; /* requests.erase(begin) (:246) */
@@ -565,6 +575,8 @@ int orc_run_rep(const orc_rep_in *in, orc_rep_out *out) {
     s.st.queue_max_raw = INT64_MIN;
     s.st.resp_max_ticks = INT64_MIN;
     s.st.last_tick = INT64_MIN;
+    s.st.abort_tick = INT64_MAX;
+    s.st.abort_task = -1;
     if (out->user) {
         orc_moments *ms[4] = {&out->user->delay, &out->user->latency, &out->user->latencyH1, &out->user->taskTime};
         for (int i = 0; i < 4; i++) {
@@ -690,6 +702,7 @@ int orc_run_rep(const orc_rep_in *in, orc_rep_out *out) {
         s.st.energy_j = e_sum;
     }
 done:
+    if (rc == ORC_STOPPED) rc = ORC_OK; /* the reference's own end of run (stop_at_ref_abort) */
     s.st.status = rc;
     if (out->stats) *out->stats = s.st;
     if (s.nodes)
@@ -716,6 +729,7 @@ typedef struct {
     const int32_t *region;
     int32_t hier_threshold_s;
     int64_t hier_up_tick;
+    int32_t flags;
     int32_t *node;
     uint8_t *status;
     int64_t *start_tick, *done_tick;
@@ -741,7 +755,7 @@ static void *batch_worker(void *arg) {
                          b->p_busy ? b->p_busy + no : 0, b->p_idle ? b->p_idle + no : 0, b->policy,
                          b->user_ul ? b->user_ul + uo : 0, b->user_dl ? b->user_dl + uo : 0, b->user_per_task,
                          b->down ? b->down + no : 0, b->region ? b->region + to : 0, b->hier_threshold_s,
-                         b->hier_up_tick};
+                         b->hier_up_tick, b->flags & 1};
         orc_rep_out out = {b->node ? b->node + to : 0, b->status ? b->status + to : 0,
                            b->start_tick ? b->start_tick + to : 0, b->done_tick ? b->done_tick + to : 0,
                            0, b->stats ? b->stats + r : 0,
@@ -809,9 +823,25 @@ int orc_run_batch5(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t
                    int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
                    orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
                    int threads) {
+    return orc_run_batch6(R, T, N, node_stride, policy, arrive_tick, req_mips, mips, dl, ul, init_adv, p_busy_w,
+                          p_idle_w, user_ul, user_dl, user_per_task, down_tick, region, hier_threshold_s,
+                          hier_up_tick, 0, node, status, start_tick, done_tick, stats, node_energy_j, hist,
+                          user_stats, threads);
+}
+
+int orc_run_batch6(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
+                   const int64_t *arrive_tick, const int32_t *req_mips,
+                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                   const double *p_busy_w, const double *p_idle_w,
+                   const int64_t *user_ul, const int64_t *user_dl, int32_t user_per_task,
+                   const int64_t *down_tick, const int32_t *region, int32_t hier_threshold_s, int64_t hier_up_tick,
+                   int32_t flags,
+                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                   orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
+                   int threads) {
     batch_t b = {R, N, node_stride, policy, T, arrive_tick, req_mips, mips, dl, ul, init_adv, p_busy_w, p_idle_w,
-                 user_ul, user_dl, user_per_task, down_tick, region, hier_threshold_s, hier_up_tick, node, status,
-                 start_tick, done_tick, stats, node_energy_j, hist, user_stats, 0};
+                 user_ul, user_dl, user_per_task, down_tick, region, hier_threshold_s, hier_up_tick, flags, node,
+                 status, start_tick, done_tick, stats, node_energy_j, hist, user_stats, 0};
     pthread_mutex_init(&b.mu, 0);
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;

@@ -74,6 +74,13 @@ typedef struct {
     const int32_t *region;
     int32_t hier_threshold_s;
     int64_t hier_up_tick;
+    /* 1: end the run where the reference ends it, at the first queueTime emission
+     * that throws (ComputeBrokerApp3.cc:238; no handler up to :84-86): that
+     * RELEASERESOURCE has sent its status-6 ack and lowered busyTime (:228-234)
+     * and nothing after the emit runs, no later event either.  Per-task outputs
+     * not reached stay -1 (status 0).  0: count the emission and go on (the
+     * engine's extension).  Both record abort_tick / abort_task. */
+    int32_t stop_at_ref_abort;
 } orc_rep_in;
 
 /* Task status of a task that reached a crashed node (no ack, never served). */
@@ -116,6 +123,10 @@ typedef struct {
     int64_t n_qtime;              /* queueTime emissions in the moments                */
     int64_t n_qtime_overflow;     /* emissions at which the reference's simtime_t
                                      arithmetic leaves the int64 range (orc_qtime_raw) */
+    int64_t abort_tick;           /* the reference's abort point: tick of the first
+                                     overflowing emission (INT64_MAX: none) ...          */
+    int64_t abort_task;           /* ... and the task it would have started (-1: none);
+                                     at one tick the lowest index (fognet_hip.h)         */
 } orc_rep_stats;
 
 /* OMNeT++ 4.6 SimTime at the default scale 1e-12 (include/simtime.h, not in the
@@ -273,6 +284,18 @@ int orc_run_batch5(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t
                    const double *p_busy_w, const double *p_idle_w,
                    const int64_t *user_ul, const int64_t *user_dl, int32_t user_per_task,
                    const int64_t *down_tick, const int32_t *region, int32_t hier_threshold_s, int64_t hier_up_tick,
+                   int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
+                   orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
+                   int threads);
+
+/* orc_run_batch5 + flags (bit 0: orc_rep_in.stop_at_ref_abort). */
+int orc_run_batch6(int32_t R, int64_t T, int32_t N, int32_t node_stride, int32_t policy,
+                   const int64_t *arrive_tick, const int32_t *req_mips,
+                   const int32_t *mips, const int64_t *dl, const int64_t *ul, const int64_t *init_adv,
+                   const double *p_busy_w, const double *p_idle_w,
+                   const int64_t *user_ul, const int64_t *user_dl, int32_t user_per_task,
+                   const int64_t *down_tick, const int32_t *region, int32_t hier_threshold_s, int64_t hier_up_tick,
+                   int32_t flags,
                    int32_t *node, uint8_t *status, int64_t *start_tick, int64_t *done_tick,
                    orc_rep_stats *stats, double *node_energy_j, int64_t *hist, orc_user_stats *user_stats,
                    int threads);

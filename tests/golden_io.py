@@ -95,6 +95,9 @@ def check_qtime_record(st, exp):
         assert int(st["queue_min_raw"]) == exp["queue_min"] and int(st["queue_max_raw"]) == exp["queue_max"]
     else:
         assert int(st["queue_min_raw"]) == np.iinfo(np.int64).max
+    # the reference's abort point (first overflowing emission; fognet_hip.h)
+    ab = np.iinfo(np.int64).max if exp["abort_tick"] is None else exp["abort_tick"]
+    assert int(st["abort_tick"]) == ab and int(st["abort_task"]) == exp["abort_task"]
 
 
 def general0_v2_node():

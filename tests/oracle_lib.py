@@ -28,6 +28,7 @@ class OrcRepStats(C.Structure):
         ("events", C.c_int64), ("max_pending", C.c_int32), ("status", C.c_int32),
         ("busy_s", C.c_int64), ("energy_j", C.c_double),
         ("queue_sq_top", C.c_uint64), ("n_qtime", C.c_int64), ("n_qtime_overflow", C.c_int64),
+        ("abort_tick", C.c_int64), ("abort_task", C.c_int64),
     ]
 
 
@@ -70,6 +71,9 @@ def lib():
         _lib.orc_run_batch5.argtypes = ([C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [p] * 10 +
                                         [C.c_int32, p, p, C.c_int32, C.c_int64] + [p] * 8 + [C.c_int])
         _lib.orc_run_batch5.restype = C.c_int
+        _lib.orc_run_batch6.argtypes = ([C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [p] * 10 +
+                                        [C.c_int32, p, p, C.c_int32, C.c_int64, C.c_int32] + [p] * 8 + [C.c_int])
+        _lib.orc_run_batch6.restype = C.c_int
         _lib.orc_decide_hier.argtypes = [C.c_int32, p, p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32),
                                          C.POINTER(C.c_int32)]
         _lib.orc_decide_hier.restype = C.c_int
@@ -149,14 +153,17 @@ def decide_hier(adv_busy, adv_mips, region, threshold_s, req):
 
 def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool = True, policy: int = 1,
               p_busy=None, p_idle=None, hist: bool = False, user_ul=None, user_dl=None, down=None, region=None,
-              hier_threshold_s: int = 60, hier_up_tick: int = 20 * 10**9):
+              hier_threshold_s: int = 60, hier_up_tick: int = 20 * 10**9, stop_at_ref_abort: bool = False):
     """Replay R replications.  arrive/req: [R,T]; node params [R,N] or [N] (shared).
     ``p_busy``/``p_idle`` (same shape as mips) enable the energy model; ``hist``
     returns per-replication histograms [R, 2, 64]; ``user_ul``/``user_dl``
     ([R] one user per replication, or [R, T] per task) model the publishing
     users' links and return the user-side signals as ``user`` [R] (USER_STATS_DTYPE).
     ``down`` (same shape as mips, INT64_MAX = never): node crash ticks.
-    ``region`` ([R, T] int32): the EXT_HIER regional broker of each publish."""
+    ``region`` ([R, T] int32): the EXT_HIER regional broker of each publish.
+    ``stop_at_ref_abort``: end each replication where the reference ends it, at
+    the first queueTime emission that overflows (orc_rep_in.stop_at_ref_abort);
+    outputs the run never reached stay -1 (status 0)."""
     arrive = np.ascontiguousarray(np.atleast_2d(arrive), dtype=np.int64)
     req = np.ascontiguousarray(np.atleast_2d(req), dtype=np.int32)
     R, T = arrive.shape
@@ -184,9 +191,9 @@ def run_batch(arrive, req, mips, dl, ul, init, threads: int = 1, outputs: bool =
     stats = (OrcRepStats * R)()
     dn = np.ascontiguousarray(down, dtype=np.int64) if down is not None else None
     rg = np.ascontiguousarray(np.atleast_2d(region), dtype=np.int32) if region is not None else None
-    lib().orc_run_batch5(R, T, N, stride, policy, _ptr(arrive), _ptr(req), _ptr(mips), _ptr(dl), _ptr(ul),
+    lib().orc_run_batch6(R, T, N, stride, policy, _ptr(arrive), _ptr(req), _ptr(mips), _ptr(dl), _ptr(ul),
                          _ptr(init), _ptr(pb), _ptr(pi), _ptr(uu), _ptr(ud), per_task, _ptr(dn), _ptr(rg),
-                         int(hier_threshold_s), int(hier_up_tick), _ptr(node),
+                         int(hier_threshold_s), int(hier_up_tick), 1 if stop_at_ref_abort else 0, _ptr(node),
                          _ptr(status),
                          _ptr(start), _ptr(done), C.cast(stats, C.c_void_p), _ptr(energy), _ptr(h), _ptr(user),
                          threads)

@@ -66,7 +66,7 @@ def test_struct_layouts_match_header(tmp_path):
 
 def test_status_strings_and_version():
     lib = abi.load()
-    assert lib.fognet_abi_version() == abi.ABI_VERSION == 9
+    assert lib.fognet_abi_version() == abi.ABI_VERSION == 10
     assert lib.fognet_status_string(abi.FOGNET_ERR_CAPACITY) == b"capacity exceeded"
     assert lib.fognet_status_string(99) == b"unknown status"
 

@@ -41,6 +41,13 @@ def test_bench_c3_small():
     assert d["scaling"] == "weak" and d["roofline"]["bound"] == "hbm"
     assert d["cpu_baseline"]["parity"] is True
     assert d["stats"]["decisions"] == 64 * 4000
+    # N = 256: every replication's reference run ends at a queueTime overflow within its first few hundred
+    # publishes (the stale view herds them onto node 0); the line says so
+    ra = d["reference_abort"]
+    assert ra["replications"] == 64 and 0 < ra["ref_aborted_replications"] <= 64
+    assert 0 < ra["ref_defined_decisions"] < 64 * 4000
+    assert d["roofline"]["bytes_per_decision"] == 12 + 24 + 2 * 256 * 48 / 4000
+    assert d["cpu_baseline"]["cores"] == d["cpu_baseline"]["job_cpus"] and "share_value" in d["cpu_baseline"]
 
 
 @pytest.mark.parametrize("policy", ["EXT_HIER", "REF_V3"])
@@ -60,4 +67,6 @@ def test_bench_c4_small():
 
 def test_bench_c1_small():
     d = run_bench("--workload", "c1", "--R-total", "8", "--steps", "1", "--warmup", "1", "--cpu-threads", "4")
-    assert "outputs identical to the device: True" in d["cpu_baseline"]["sample"]
+    assert d["cpu_baseline"]["parity"] is True and "outputs identical to the device: True" in \
+        d["cpu_baseline"]["share_sample"]
+    assert d["cpu_baseline"]["cores"] == d["cpu_baseline"]["job_cpus"]  # all CPUs of the mask

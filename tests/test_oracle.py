@@ -349,6 +349,68 @@ def test_qtime_known_answers(case):
     assert o["hist"][0][0].sum() == exp["n_qtime"]
 
 
+@pytest.mark.parametrize("case", golden_io.qtime_cases(), ids=lambda c: c[0])
+def test_qtime_stop_at_reference_abort(case):
+    """The reference ends its run at the first queueTime emission that throws
+    (ComputeBrokerApp3.cc:238, no handler up to :84-86): the oracle's stop mode
+    reaches exactly the hand-traced prefix (kat_qtime.json stop_start /
+    stop_done) and reports the same abort point as the continuing run."""
+    name, tr, exp = case
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], stop_at_ref_abort=True)
+    np.testing.assert_array_equal(o["node"][0], exp["node"])
+    np.testing.assert_array_equal(o["status"][0], exp["status"])
+    np.testing.assert_array_equal(o["start"][0], exp["stop_start"])
+    np.testing.assert_array_equal(o["done"][0], exp["stop_done"])
+    st = o["stats"][0]
+    ab = np.iinfo(np.int64).max if exp["abort_tick"] is None else exp["abort_tick"]
+    assert st["status"] == 0 and int(st["abort_tick"]) == ab and int(st["abort_task"]) == exp["abort_task"]
+    assert int(st["n_qtime_overflow"]) == (1 if exp["abort_tick"] is not None else 0)
+
+
+def test_reference_abort_prefix_on_sweep_trace():
+    """C3-recipe replications (N = 256; the stale view herds the first
+    publishes onto node 0, whose queue passes ~9223 s within a few hundred
+    tasks, at every load of the sweep): the continuing oracle (the engine's
+    extension) and the stop-at-abort oracle (the reference) agree on every
+    value the reference defines -- the decisions of all publishes up to the
+    abort tick, every status, start and completion the aborted run reached --
+    and on the abort point; the prefix is exactly the publishes with
+    arrive_tick <= abort_tick.  The N = 16 replication never overflows."""
+    b = tg.make_batch(0x5EED0003, 3, 256, 3000, sweep=True)
+    s16 = tg.make_replication(0x5EED0003, 3, 16, 3000, rho=0.95)
+    full = ol.run_batch(b["arrive"], b["req"], b["mips"], b["dl"], b["ul"], b["init"], threads=3)
+    stop = ol.run_batch(b["arrive"], b["req"], b["mips"], b["dl"], b["ul"], b["init"], threads=3,
+                        stop_at_ref_abort=True)
+    big = np.iinfo(np.int64).max
+    n_abort = 0
+    for r in range(3):
+        fs, ss = full["stats"][r], stop["stats"][r]
+        assert int(fs["abort_tick"]) == int(ss["abort_tick"]) and int(fs["abort_task"]) == int(ss["abort_task"])
+        ab = int(fs["abort_tick"])
+        if ab == big:
+            assert int(fs["n_qtime_overflow"]) == 0
+            continue
+        n_abort += 1
+        k = int(fs["abort_task"])
+        assert full["status"][r][k] == 4 and full["start"][r][k] == ab  # the popped task starts at the abort tick
+        prefix = b["arrive"][r] <= ab
+        assert int(ss["n_tasks"]) == int(prefix.sum())
+        np.testing.assert_array_equal(stop["node"][r][prefix], full["node"][r][prefix])
+        assert (stop["node"][r][~prefix] == -1).all()
+        reached = stop["status"][r] != 0
+        np.testing.assert_array_equal(stop["status"][r][reached], full["status"][r][reached])
+        for key in ("start", "done"):
+            got = stop[key][r]
+            np.testing.assert_array_equal(got[got >= 0], full[key][r][got >= 0])
+            assert (got[got >= 0] <= ab).all()
+        assert stop["start"][r][k] == -1 and int(ss["n_qtime_overflow"]) == 1
+    assert n_abort == 3  # the recipe does reach the overflow
+    o16 = ol.run_batch(s16["arrive"], s16["req"], s16["mips"], s16["dl"], s16["ul"], s16["init"],
+                       stop_at_ref_abort=True)
+    assert int(o16["stats"][0]["abort_tick"]) == big and int(o16["stats"][0]["abort_task"]) == -1
+    assert int(o16["stats"][0]["n_tasks"]) == 3000 and (o16["done"][0] >= 0).all()
+
+
 def test_qtime_raw_function():
     # below 2^51 ticks the round trip is exact: raw = 1000 x the tick difference
     assert ol.qtime_raw(5 * 10**12 + 7, 10**12) == (4 * 10**12 + 7) * 1000

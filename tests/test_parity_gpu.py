@@ -32,7 +32,7 @@ def assert_parity(tr, g, o):
         np.testing.assert_array_equal(g[k], o[k], err_msg=k)
     for f in ("n_tasks", "n_queued", "n_started", "last_tick", "queue_min_raw", "queue_max_raw",
               "resp_min_ticks", "resp_max_ticks", "queue_sum_lo", "queue_sum_hi", "queue_sq_lo", "queue_sq_hi",
-              "queue_sq_top", "n_qtime", "n_qtime_overflow",
+              "queue_sq_top", "n_qtime", "n_qtime_overflow", "abort_tick", "abort_task",
               "resp_sum_lo", "resp_sum_hi", "resp_sq_lo", "resp_sq_hi", "events", "max_pending"):
         np.testing.assert_array_equal(st_g[f], st_o[f], err_msg=f)
 
@@ -423,14 +423,18 @@ def test_full_size_sweep_properties(ctx):
     assert st[r].tobytes() == o["stats"][0].tobytes()
 
 
-@pytest.mark.parametrize("kernel", ["register", "wide"])
+@pytest.mark.parametrize("kernel", ["register", "wide", "inloop"])
 @pytest.mark.parametrize("case", golden_io.qtime_cases(), ids=lambda c: c[0])
 def test_qtime_known_answers_gpu(ctx, monkeypatch, case, kernel):
     """queueTime as the reference emits it (tests/golden/kat_qtime.json): the
     queueStartTime double round trip above 2^53 ticks, a negative value, the
-    simtime_t overflow; both replay kernels, fused statistics and histogram."""
+    simtime_t overflow and the reference's abort point (the earliest
+    overflowing emission, two_nodes: not the lowest index); both replay
+    kernels and the in-loop statistics, fused statistics and histogram."""
     if kernel == "wide":
         monkeypatch.setenv("FOGNET_REPLAY_KERNEL", "wide")
+    if kernel == "inloop":
+        monkeypatch.setenv("FOGNET_REPLAY_STATS", "inloop")
     name, tr, exp = case
     dev = torch.device("cuda", ctx.device)
     out = fa.run_batch(ctx, fa.as_device_trace(tr, dev), hist=True)
@@ -439,6 +443,74 @@ def test_qtime_known_answers_gpu(ctx, monkeypatch, case, kernel):
         np.testing.assert_array_equal(g[0].cpu().numpy(), exp[k], err_msg=k)
     golden_io.check_qtime_record(out.rep_stats()[0], exp)
     assert int(out.hist[0].sum()) == exp["n_qtime"]
+
+
+@pytest.mark.parametrize("kernel", ["register", "wide", "inloop", "separate", "generated"])
+def test_reference_abort_point_and_prefix(ctx, monkeypatch, kernel):
+    """The reference ends a run at its first overflowing queueTime emission
+    (ComputeBrokerApp3.cc:238, no handler up to :84-86).  On C3-recipe
+    replications (N = 256: the stale view herds the first publishes onto node 0
+    and its queue passes ~9223 s within a few hundred tasks) the device reports
+    the oracle's abort point, its outputs equal the stop-at-abort oracle (the
+    reference) on every value that run defines, and FOGNET_FLAG_REF_ABORT turns
+    those replications into FOGNET_REF_ABORTED (counted as failed by the job
+    reduction); the N = 16 replication completes in the reference too."""
+    if kernel == "wide":
+        monkeypatch.setenv("FOGNET_REPLAY_KERNEL", "wide")
+    if kernel == "inloop":
+        monkeypatch.setenv("FOGNET_REPLAY_STATS", "inloop")
+    T, N, R = 3000, 256, 6
+    dev = torch.device("cuda", ctx.device)
+    mg, sc = fa.sweep_params(np.arange(R), N)
+    d = fa.generate_trace(ctx, 0x5EED0003, R, T, N, mg, sc)
+    tr = {k: v for k, v in d.items() if not k.startswith("_")}
+    h = {k: tr[k].cpu().numpy() for k in tr}
+    big = np.iinfo(np.int64).max
+    full = ol.run_batch(h["arrive"], h["req"], h["mips"], h["dl"], h["ul"], h["init"], threads=6)
+    stop = ol.run_batch(h["arrive"], h["req"], h["mips"], h["dl"], h["ul"], h["init"], threads=6,
+                        stop_at_ref_abort=True)
+    assert (full["stats"]["abort_tick"] != big).all()
+    if kernel == "generated":  # statistics-only, trace generated in the kernel: the records
+        g = fa.run_generated(ctx, 0x5EED0003, R, T, N, mg, sc, hist=False)
+        torch.cuda.synchronize()
+        assert g.rep_stats().tobytes() == full["stats"].tobytes()
+        return
+    if kernel == "separate":  # fognet_replay_dev, then fognet_rep_stats_dev
+        out = fa.run_batch(ctx, tr, stage="replay")
+        fa.run_batch(ctx, tr, out=out, stage="stats")
+    else:
+        out = fa.run_batch(ctx, tr)
+    torch.cuda.synchronize()
+    st = out.rep_stats()
+    assert st.tobytes() == full["stats"].tobytes()
+    g = {k: getattr(out, a).cpu().numpy() for k, a in (("node", "node"), ("status", "status"),
+                                                      ("start", "start_tick"), ("done", "done_tick"))}
+    for r in range(R):
+        ab = int(st[r]["abort_tick"])
+        prefix = h["arrive"][r] <= ab
+        np.testing.assert_array_equal(g["node"][r][prefix], stop["node"][r][prefix])
+        reached = stop["status"][r] != 0
+        np.testing.assert_array_equal(g["status"][r][reached], stop["status"][r][reached])
+        for k in ("start", "done"):
+            m = stop[k][r] >= 0
+            np.testing.assert_array_equal(g[k][r][m], stop[k][r][m])
+    # the reference mode: aborted replications fail, with outputs still written in full
+    out2 = fa.run_batch(ctx, tr, ref_abort=True)
+    torch.cuda.synchronize()
+    st2 = out2.rep_stats()
+    assert (st2["status"] == _abi.FOGNET_REF_ABORTED).all()
+    assert torch.equal(out2.done_tick, out.done_tick) and torch.equal(out2.node, out.node)
+    job = fa.reduce_stats(ctx, out2.stats, R)
+    assert int(job["n_failed"]) == R and int(job["n_ref_aborted"]) == 0  # (failed records contribute nothing)
+    job = fa.reduce_stats(ctx, out.stats, R)
+    assert int(job["n_failed"]) == 0 and int(job["n_ref_aborted"]) == R
+    # a replication the reference completes: no abort point, status OK under the flag
+    one = tg.make_replication(0x5EED0003, 3, 16, T, rho=0.95)
+    o16 = fa.run_batch(ctx, fa.as_device_trace({k: v[None] if k in ("arrive", "req") else v for k, v in one.items()},
+                                               dev), ref_abort=True)
+    torch.cuda.synchronize()
+    s16 = o16.rep_stats()[0]
+    assert s16["status"] == 0 and int(s16["abort_tick"]) == big and int(s16["abort_task"]) == -1
 
 
 def _sharded_sample(ctx, seed, R_total, T, N, reps, ring, params):
