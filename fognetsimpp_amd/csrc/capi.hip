@@ -164,6 +164,19 @@ bool use_inloop() {
   return f != nullptr && strcmp(f, "inloop") == 0;
 }
 
+// Workspace slots of the hand-over launch: the wide kernel walks the hand-over
+// list with a grid stride, so fewer slots than handed-over replications are
+// still exact.  At most kWideFallbackSlots, and no more than fit in the ring
+// workspace the register kernel needs anyway (floor 1), so a replay that never
+// hands over allocates nothing extra.
+int32_t fallback_slots(int32_t R, int32_t T, int32_t N, size_t ring_bytes, bool gen) {
+  int32_t slots = R < kWideFallbackSlots ? R : kWideFallbackSlots;
+  const size_t per = fognet::replay_wide_workspace_bytes(1, T, N, gen);
+  const size_t fit = per ? ring_bytes / per : (size_t)slots;
+  if ((size_t)slots > fit) slots = fit < 1 ? 1 : (int32_t)fit;
+  return slots;
+}
+
 bool use_wide(int32_t N) {
   if (N > fognet::kWave * fognet::kMaxNodesPerLane) return true;
   const char* f = getenv("FOGNET_REPLAY_KERNEL");
@@ -421,7 +434,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     // replay of the handed-over replications once the register kernel is done (stream order)]
     // + for a statistics-only replay the per-task outputs the fused statistics epilogue reads back
     const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingWord);
-    const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
+    const int32_t slots = fallback_slots(a.R, a.T, a.N, ring_bytes, false);
     const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
     const size_t o_board = align256(256 + (size_t)a.R * sizeof(int32_t));
     const size_t head = o_board + fognet::kBoardWords * sizeof(uint32_t);
@@ -450,8 +463,16 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     }
     e = fognet::launch_replay(a, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "replay launch");
-    // the handed-over replications (usually none: every workgroup leaves at once)
-    e = fognet::launch_replay_wide(a, base + head, slots, (hipStream_t)stream);
+    // the handed-over replications (usually none: every workgroup leaves at once).  The wide kernel
+    // accumulates its statistics inline; in a replay-only call the statistics stage that follows
+    // recomputes them for every replication from the per-task outputs, so the hand-over must not add
+    // its histogram and energy as well
+    fognet::ReplayArgs hw = a;
+    if (!a.fuse_stats) {
+      hw.hist = nullptr;
+      hw.out_energy = nullptr;
+    }
+    e = fognet::launch_replay_wide(hw, base + head, slots, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "wide hand-over launch");
   }
   if (which & 2) {
@@ -504,7 +525,7 @@ int fognet_run_generated_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t 
   const int64_t resident = (int64_t)c->cus * fognet::kGenWavesPerCu;
   a.gen_slots = (int32_t)(a.R < resident ? a.R : resident);
   const size_t ring_bytes = (size_t)a.gen_slots * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingWord);
-  const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
+  const int32_t slots = fallback_slots(a.R, a.T, a.N, ring_bytes, true);
   const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N, true);
   const size_t head = align256(256 + (size_t)a.R * sizeof(int32_t));
   rc = ensure(c, (void**)&c->ring, &c->ring_bytes, head + (ring_bytes > fb_bytes ? ring_bytes : fb_bytes),

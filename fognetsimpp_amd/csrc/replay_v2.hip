@@ -411,6 +411,400 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
   }
 }
 
+// ---- four replications per wavefront (N <= 16): replication 4 * blockIdx.x + q
+// on the 16-lane DPP row q = lane / 16, node j on lane 16 q + j.  The v2 loop is
+// VALU-issue-bound (round 2: VALU busy 0.87 at 5 of 64 lanes holding nodes), so
+// packing four replications into the lanes the one-per-wave kernel leaves idle
+// runs four event loops per instruction stream.  Broker state that
+// replay_v2_kernel keeps wave-uniform is row-uniform here (every lane of a row
+// holds the same value); the earliest event is a row minimum (the four in-row
+// DPP butterflies leave it in every lane of the row), a node's values reach the
+// rest of its row with ds_bpermute, and every handler runs under a row-uniform
+// condition, so rows in different handlers only serialise those handlers.
+// Same arithmetic, same FES order, same outputs as replay_v2_kernel.
+constexpr int kRowLanes = 16;
+constexpr int kRowsPerWave = kWave / kRowLanes;
+
+__device__ __forceinline__ uint64_t row_min_u64(uint64_t v) {
+  v = umin64(v, dpp_u64<0xB1>(v));
+  v = umin64(v, dpp_u64<0x4E>(v));
+  v = umin64(v, dpp_u64<0x141>(v));
+  v = umin64(v, dpp_u64<0x140>(v));
+  return v;
+}
+
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
+  v = min(v, dpp_u32<0xB1>(v));
+  v = min(v, dpp_u32<0x4E>(v));
+  v = min(v, dpp_u32<0x141>(v));
+  v = min(v, dpp_u32<0x140>(v));
+  return v;
+}
+
+__device__ __forceinline__ int64_t row_sum_i64(int64_t v) {
+  v += (int64_t)dpp_u64<0xB1>((uint64_t)v);
+  v += (int64_t)dpp_u64<0x4E>((uint64_t)v);
+  v += (int64_t)dpp_u64<0x141>((uint64_t)v);
+  v += (int64_t)dpp_u64<0x140>((uint64_t)v);
+  return v;
+}
+
+// value of lane w (0..15) of this lane's row (every lane of the row active)
+__device__ __forceinline__ uint32_t row_bcast_u32(uint32_t v, int w) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((threadIdx.x & ~(kRowLanes - 1u)) | (uint32_t)w) << 2), (int)v);
+}
+
+__device__ __forceinline__ uint64_t row_bcast_u64(uint64_t v, int w) {
+  return ((uint64_t)row_bcast_u32((uint32_t)(v >> 32), w) << 32) | row_bcast_u32((uint32_t)v, w);
+}
+
+// some lane of this lane's row has p (the row's lanes active)
+__device__ __forceinline__ bool row_any(bool p) {
+  return ((ballot(p) >> (threadIdx.x & ~(kRowLanes - 1u))) & 0xFFFFull) != 0ull;
+}
+
+__global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
+  const fognet_v2_in& A = P.in;
+  const fognet_v2_out& O = P.out;
+  const int lane = threadIdx.x;
+  const int li = lane & (kRowLanes - 1);
+  const int r = blockIdx.x * kRowsPerWave + lane / kRowLanes;
+  const bool live = r < A.R;  // rows past R idle from the start
+  const int rr = live ? r : 0;  // (their addresses stay in bounds)
+  const int N = A.N, T = A.T;
+  const bool own = live && li < N;
+  const uint32_t Q = 1u << P.q_log2, qm = Q - 1u;
+  const size_t nbase = (size_t)rr * (size_t)A.node_stride;
+  const size_t tbase = (size_t)rr * (size_t)T;
+  const size_t qbase = ((size_t)rr * (size_t)FOGNET_V2_MAX_NODES + (size_t)li) << P.q_log2;
+  V2Msg* const inq = P.inq + qbase;
+  V2Msg* const outq = P.outq + qbase;
+  V2Res* const res = P.res + qbase;
+  uint8_t* const list = P.list + tbase;
+  const int64_t* const arrive = A.arrive_tick + tbase;
+  const int32_t* const reqs = A.req_mips + tbase;
+
+  const double rt = A.required_time_s[rr];
+  const double rtx = mul_rn(rt, 1e12);  // SimTime + double: the double in ticks
+  const int64_t rt_ticks = (int64_t)add_rn(rtx, rtx >= 0.0 ? 0.5 : -0.5);
+  const int64_t stop = A.stop_tick[rr];
+
+  // ---- node li of the row's replication
+  int32_t mips = 0, view = 0;  // the broker's Broker record starts at MIPS 0 (BrokerBaseApp2.cc:105)
+  int64_t dl = 0, ul = 0;
+  bool t_sched = false;  // selfMsg->isScheduled()
+  int64_t t_tick = kNever;
+  uint64_t t_seq = ~0ull;
+  uint32_t t_kind = kKindAdvertise;
+  bool bad = !(stop <= kMaxV2Tick) || !(rtx >= 0.0) || rt_ticks > kMaxV2Tick;
+  if (own) {
+    mips = A.mips[nbase + li];
+    dl = A.dl_tick[nbase + li];
+    ul = A.ul_tick[nbase + li];
+    const int64_t fa = A.first_adv_tick[nbase + li];
+    bad |= dl < 0 || ul < 0 || fa < 0 || dl > kMaxV2Tick || ul > kMaxV2Tick || fa > kMaxV2Tick;
+    t_sched = true;  // the first ADVERTISEMIPS firing, pre-inserted in node order
+    t_tick = fa;
+    t_seq = (uint64_t)li;
+  }
+  uint32_t in_h = 0u, in_n = 0u, out_h = 0u, out_n = 0u, rs_h = 0u, rs_n = 0u;
+  V2Msg in_hd = {kNever, ~0ull, 0, 0}, out_hd = {kNever, ~0ull, 0, 0};
+
+  // ---- broker (row-uniform)
+  int32_t pool = live ? A.broker_mips[rr] : 0;
+  bool b_sched = false;
+  int64_t b_tick = kNever;
+  uint64_t b_seq = ~0ull;
+  uint64_t seq = (uint64_t)N + (uint64_t)T;  // the publishes hold N .. N+T-1
+  int next = 0, list_h = 0;
+  int64_t prev_pub = INT64_MIN;
+  int64_t p_tick = (live && T > 0) ? arrive[0] : kNever;  // the next publish, loaded one publish ahead
+  int32_t p_req = (live && T > 0) ? reqs[0] : 0;
+  fognet_v2_stats st = {};
+  uint32_t err = row_any(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
+  bool fin = !live || err != FOGNET_OK;  // row-uniform: this replication's loop has ended
+  bad = false;
+
+  while (ballot(!fin)) {
+    if (fin) continue;  // (finished rows wait for the others; their lanes stay off below)
+    // ---- the earliest event: the lanes' own sources, then the broker's
+    int64_t ct = kNever;
+    uint64_t cs = ~0ull;
+    int src = 0;  // 1 self-message, 2 task arrival, 3 message at the broker
+    if (t_sched) {
+      ct = t_tick;
+      cs = t_seq;
+      src = 1;
+    }
+    if (in_n && earlier(in_hd.tick, in_hd.seq, ct, cs)) {
+      ct = in_hd.tick;
+      cs = in_hd.seq;
+      src = 2;
+    }
+    if (out_n && earlier(out_hd.tick, out_hd.seq, ct, cs)) {
+      ct = out_hd.tick;
+      cs = out_hd.seq;
+      src = 3;
+    }
+    const int64_t m_tick = (int64_t)row_min_u64((uint64_t)ct);
+    const bool at = src != 0 && ct == m_tick;
+    const uint64_t m_seq = row_min_u64(at ? cs : ~0ull);  // same-tick events: insertion order decides
+    const uint32_t wl = row_min_u32(at && cs == m_seq ? (uint32_t)li : 0xFFu);
+    const int w = wl == 0xFFu ? 0 : (int)wl;
+    int kind = wl == 0xFFu ? 0 : 1;  // 1 node-side event of lane w, 2 publish, 3 broker timer
+    int64_t e_tick = kind ? m_tick : kNever;
+    uint64_t e_seq = kind ? m_seq : ~0ull;
+    if (next < T) {
+      if (earlier(p_tick, (uint64_t)N + (uint64_t)next, e_tick, e_seq)) {
+        e_tick = p_tick;
+        e_seq = (uint64_t)N + (uint64_t)next;
+        kind = 2;
+      }
+    }
+    if (b_sched && earlier(b_tick, b_seq, e_tick, e_seq)) {
+      e_tick = b_tick;
+      e_seq = b_seq;
+      kind = 3;
+    }
+    if (kind == 0 || e_tick >= stop) {  // nothing left, or the sim-time-limit
+      fin = true;
+      continue;
+    }
+    const int64_t now = e_tick;
+    ++st.events;
+
+    if (kind == 2) {
+      // ---- publish: BrokerBaseApp2.cc:176-195 + sendPubAck(:205-287)
+      const int t = next++;
+      if (p_tick < prev_pub || p_tick > kMaxV2Tick) {
+        err = FOGNET_ERR_ARG;  // trace not sorted / out of range
+        fin = true;
+        continue;
+      }
+      prev_pub = p_tick;
+      const int32_t req = p_req;
+      if (next < T) {  // the following publish, in flight while this one is handled
+        p_tick = arrive[next];
+        p_req = reqs[next];
+      }
+      ++st.n_tasks;
+      int32_t k = -1;
+      uint32_t status;
+      int64_t start = -1;
+      uint8_t lmark = kListNone;
+      if (req < pool) {  // :181 -> sendPubAck(true), :209-232
+        pool -= req;
+        lmark = kListLocal;
+        status = FOGNET_V2_ST_LOCAL;
+        start = now;
+        ++st.n_local;
+        b_sched = true;  // cancelEvent + scheduleAt(now + requiredTime) (:226-229)
+        b_tick = now + rt_ticks;
+        b_seq = seq++;
+      } else if (N == 0) {  // :273-285: scheduleAt without cancelEvent
+        status = FOGNET_V2_ST_NO_NODES;
+        ++st.n_no_nodes;
+        if (b_sched) {
+          err = FOGNET_ERR_STATE;  // "scheduleAt(): message already scheduled"
+          fin = true;
+        } else {
+          b_sched = true;
+          b_tick = now + rt_ticks;
+          b_seq = seq++;
+        }
+      } else {
+        // the LAST node whose advertised MIPS exceeds node 0's (:241-248), else node 0
+        const int32_t v0 = (int32_t)row_bcast_u32((uint32_t)view, 0);
+        k = (int32_t)(15u - row_min_u32(15u - ((own && li >= 1 && view > v0) ? (uint32_t)li : 0u)));
+        const int32_t vk = (int32_t)row_bcast_u32((uint32_t)view, k);
+        lmark = kListForwarded;  // :255-260, before the MIPS check
+        if (req < vk) {          // :262-270: FognetMsgTask to node k
+          status = FOGNET_V2_ST_FORWARDED;
+          ++st.n_forwarded;
+          if (li == k) {
+            const V2Msg m = {now + dl, seq, req, t};
+            if (in_n == Q) {
+              bad = true;
+            } else {
+              inq[(in_h + in_n) & qm] = m;
+              if (in_n == 0u) in_hd = m;
+              ++in_n;
+            }
+          }
+          ++seq;
+          if (row_any(bad)) {
+            err = FOGNET_ERR_CAPACITY;
+            fin = true;
+          }
+        } else {
+          status = FOGNET_V2_ST_DROPPED;
+          ++st.n_dropped;
+        }
+      }
+      if (li == 0) {
+        list[t] = lmark;
+        O.node[tbase + t] = k;
+        O.status[tbase + t] = (uint8_t)status;
+        O.start_tick[tbase + t] = start;
+        O.done_tick[tbase + t] = -1;
+      }
+    } else if (kind == 3) {
+      // ---- broker RELEASERESOURCE: BrokerBaseApp2::releaseResource (:382-406), the
+      // first request with deadline <= now (the oldest live one: deadlines follow
+      // the list order), local or forwarded
+      b_sched = false;
+      int rel = -1;
+      uint32_t mark = kListNone;
+      if (li == 0) {
+        while (list_h < next && list[list_h] == kListNone) ++list_h;
+        if (list_h < next) {
+          const double deadline = add_rn(dbl(arrive[list_h]), rt);
+          if (deadline <= dbl(now)) {
+            rel = list_h;
+            mark = list[list_h];
+            list[list_h] = kListNone;
+            if (mark == kListLocal) O.done_tick[tbase + list_h] = now;
+          }
+        }
+      }
+      list_h = (int)row_bcast_u32((uint32_t)list_h, 0);
+      rel = (int)row_bcast_u32((uint32_t)rel, 0);
+      mark = row_bcast_u32(mark, 0);
+      if (rel >= 0) {
+        pool += reqs[rel];  // :386
+        ++st.n_released_broker;
+        if (mark == kListForwarded) ++st.n_inflated;
+      }
+    } else {
+      // ---- an event of node w
+      const int wsrc = (int)row_bcast_u32((uint32_t)src, w);
+      if (wsrc == 3) {
+        // a node -> broker message reaches the broker (BrokerBaseApp2.cc:128-154)
+        const int32_t mk = (int32_t)row_bcast_u32((uint32_t)out_hd.kind, w);
+        const int32_t mv = (int32_t)row_bcast_u32((uint32_t)out_hd.val, w);
+        if (li == w) {
+          ++out_h;
+          --out_n;
+          if (out_n) out_hd = outq[out_h & qm];
+          if (mk == kMsgAdvert) view = mv;  // setMips (:132)
+        }
+        if (mk == kMsgAck6) {  // relay and erase the request if it is still listed (:145-153)
+          bool relayed = false;
+          if (li == 0 && list[mv] == kListForwarded) {
+            list[mv] = kListNone;
+            relayed = true;
+          }
+          if (row_any(relayed)) ++st.n_relayed;
+        }
+      } else {
+        // the node's own events: its self-message or a task arrival.  The owner
+        // lane runs the handler; sequence numbers and per-task results are
+        // broadcast afterwards (lane 0 of the row writes the outputs).
+        int32_t o_task = -1;   // task whose result changed
+        uint32_t o_what = 0u;  // 1 released, 2 accepted, 3 rejected
+        uint64_t my_seq = seq;
+        if (li == w) {
+          if (wsrc == 1) {
+            t_sched = false;
+            if (t_kind == kKindRelease && rs_n) {
+              // ComputeBrokerApp2::releaseResource (:222-245): the first reservation
+              // with deadline < now (the oldest: deadlines follow arrival order)
+              const V2Res h = res[rs_h & qm];
+              if (h.deadline < dbl(now)) {
+                mips += h.req;  // :226
+                ++rs_h;
+                --rs_n;
+                o_task = h.task;
+                o_what = 1u;
+                const V2Msg m = {now + ul, my_seq++, kMsgAck6, h.task};  // puback 6 (:231-235)
+                if (out_n == Q) bad = true;
+                else {
+                  outq[(out_h + out_n) & qm] = m;
+                  if (out_n == 0u) out_hd = m;
+                  ++out_n;
+                }
+              }
+            }
+            // advertiseMIPS (:202-220): advert, then the self-message again 0.01 s later
+            const V2Msg m = {now + ul, my_seq++, kMsgAdvert, mips};
+            if (out_n == Q) bad = true;
+            else {
+              outq[(out_h + out_n) & qm] = m;
+              if (out_n == 0u) out_hd = m;
+              ++out_n;
+            }
+            t_sched = true;
+            t_tick = now + kAdvertPeriod;
+            t_seq = my_seq++;
+          } else {
+            // ComputeBrokerApp2::processPacket, FognetMsgTask (:258-318)
+            const int32_t t = in_hd.val;
+            const int32_t req = in_hd.kind;
+            ++in_h;
+            --in_n;
+            if (in_n) in_hd = inq[in_h & qm];
+            o_task = t;
+            if (req < mips) {  // :269
+              mips -= req;     // :272
+              o_what = 2u;
+              if (rs_n == Q) bad = true;
+              else {
+                res[(rs_h + rs_n) & qm] = V2Res{t, req, add_rn(dbl(now), rt)};  // :274
+                ++rs_n;
+              }
+              // cancelEvent + RELEASERESOURCE at now + requiredTime (:292-295)
+              t_kind = kKindRelease;
+              t_sched = true;
+              t_tick = now + rt_ticks;
+              t_seq = my_seq++;
+            } else {
+              o_what = 3u;  // TaskAck(false) (:299-306)
+            }
+          }
+        }
+        if (row_any(bad)) {
+          err = FOGNET_ERR_CAPACITY;
+          fin = true;
+          continue;
+        }
+        seq = row_bcast_u64(my_seq, w);
+        o_task = (int32_t)row_bcast_u32((uint32_t)o_task, w);
+        o_what = row_bcast_u32(o_what, w);
+        if (o_what == 1u) {
+          ++st.n_released_node;
+          if (li == 0) O.done_tick[tbase + o_task] = now;
+        } else if (o_what == 2u) {
+          ++st.n_accepted;
+          if (li == 0) {
+            O.status[tbase + o_task] = FOGNET_V2_ST_ACCEPTED;
+            O.start_tick[tbase + o_task] = now;
+          }
+        } else if (o_what == 3u) {
+          ++st.n_rejected;
+          if (li == 0) O.status[tbase + o_task] = FOGNET_V2_ST_REJECTED;
+        }
+      }
+    }
+  }
+
+  // ---- tasks not published before the stop (or the error), and the record
+  if (live) {
+    for (int t = next + li; t < T; t += kRowLanes) {
+      O.node[tbase + t] = -1;
+      O.status[tbase + t] = 0;
+      O.start_tick[tbase + t] = -1;
+      O.done_tick[tbase + t] = -1;
+    }
+  }
+  const int64_t msum = row_sum_i64(own ? (int64_t)mips : 0);
+  if (live && li == 0) {
+    st.node_mips_final_sum = msum;
+    st.broker_mips_final = pool;
+    st.status = (int32_t)err;
+    O.stats[r] = st;
+  }
+}
+
 }  // namespace
 
 size_t replay_v2_workspace_bytes(int32_t R, int32_t T, int32_t q_log2) {
@@ -430,7 +824,10 @@ hipError_t launch_replay_v2(const fognet_v2_in& in, const fognet_v2_out& out, vo
   a.outq = a.inq + q;
   a.res = reinterpret_cast<V2Res*>(a.outq + q);
   a.list = reinterpret_cast<uint8_t*>(a.res + q);
-  hipLaunchKernelGGL(replay_v2_kernel, dim3(in.R), dim3(kWave), 0, s, a);
+  if (in.N <= kRowLanes)  // four replications per wavefront
+    hipLaunchKernelGGL(replay_v2_rows_kernel, dim3((in.R + kRowsPerWave - 1) / kRowsPerWave), dim3(kWave), 0, s, a);
+  else
+    hipLaunchKernelGGL(replay_v2_kernel, dim3(in.R), dim3(kWave), 0, s, a);
   return hipGetLastError();
 }
 

@@ -441,7 +441,9 @@ int fognet_user_stats_dev(fognet_ctx *ctx, const fognet_batch_in *in, const fogn
 
 /* Exact reduction of R per-replication stats (device pointers) into one job
  * record (device pointer).  Replications with status != OK count in n_failed
- * and contribute nothing else. */
+ * and contribute nothing else.  R > 4096 reduces through partial records in
+ * the context's workspace: reductions on one context must then be enqueued
+ * on one stream (or synchronised), since concurrent ones share it. */
 int fognet_reduce_stats_dev(fognet_ctx *ctx, const fognet_rep_stats *stats, int32_t R,
                             fognet_job_stats *out, void *hip_stream);
 /* Host-side exact merge (used to combine per-GPU records after an all-gather):

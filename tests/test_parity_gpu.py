@@ -740,6 +740,43 @@ def test_fused_statistics_equal_separate_pass(ctx, N, T):
     assert int(fused.hist.cpu().numpy()[1].sum()) == 5 * T
 
 
+@pytest.mark.parametrize("ring", [2, 8])
+def test_fused_statistics_equal_separate_pass_with_hand_over(ctx, ring):
+    """The same with rings so small that replications are handed over to the
+    wide kernel inside the replay stage: its inline histogram and energy must
+    not be added on top of the statistics stage's."""
+    N, T, R = 64, 2000, 5
+    tr = tg.make_batch(0x5EED0078, R, N, T, sweep=True)
+    pb, pi = fa.power_model(tr["mips"])
+    d = fa.as_device_trace(dict(tr, p_busy=pb, p_idle=pi), torch.device("cuda", ctx.device))
+    fused = fa.run_batch(ctx, d, hist=True, ring_capacity=ring)
+    sep = fa.allocate_outputs(R, T, d["arrive"].device, N=N, energy=True, hist=True)
+    fa.run_batch(ctx, d, out=sep, stage="replay", ring_capacity=ring)
+    fa.run_batch(ctx, d, out=sep, stage="stats", ring_capacity=ring)
+    torch.cuda.synchronize()
+    assert (fused.rep_stats()["max_pending"] > ring).any()  # the hand-over happened
+    assert fused.stats.cpu().numpy().tobytes() == sep.stats.cpu().numpy().tobytes()
+    np.testing.assert_array_equal(fused.hist.cpu().numpy(), sep.hist.cpu().numpy())
+    np.testing.assert_array_equal(fused.node_energy.cpu().numpy(), sep.node_energy.cpu().numpy())
+    assert int(sep.hist.cpu().numpy()[1].sum()) == R * T
+
+
+def test_decide_batch_rejects_other_policies(ctx):
+    """fognet_decide_batch_dev, like fognet_decide and fognet_decide_window,
+    evaluates REF_V3 only."""
+    import ctypes as C
+    dev = torch.device("cuda", ctx.device)
+    busy = torch.zeros((1, 4), dtype=torch.float64, device=dev)
+    mips = torch.full((1, 4), 1000, dtype=torch.int32, device=dev)
+    req = torch.full((1,), 5000, dtype=torch.int32, device=dev)
+    node = torch.empty(1, dtype=torch.int32, device=dev)
+    for pol in (_abi.FOGNET_POLICY_EXT_LAT, _abi.FOGNET_POLICY_EXT_HIER, 0):
+        rc = ctx._lib.fognet_decide_batch_dev(ctx.handle, pol, 1, 4, C.c_void_p(busy.data_ptr()),
+                                              C.c_void_p(mips.data_ptr()), C.c_void_p(req.data_ptr()),
+                                              C.c_void_p(node.data_ptr()), None, None)
+        assert rc == _abi.FOGNET_ERR_UNSUPPORTED
+
+
 def test_histogram_accumulates_across_calls(ctx):
     tr = tg.make_batch(3, 4, 32, 1000)
     dev = torch.device("cuda", ctx.device)
@@ -985,9 +1022,12 @@ def v2_random(seed, R, N, T):
     return dict(arrive=arrive, req=req, mips=mips, dl=dl, ul=ul, first_adv=first), broker, stop, rt
 
 
-@pytest.mark.parametrize("seed,N", [(0, 1), (1, 2), (2, 5), (3, 13), (4, 64), (5, 5)])
-def test_v2_random_matches_oracle(ctx, seed, N):
-    tr, broker, stop, rt = v2_random(seed, 16, N, 3000)
+@pytest.mark.parametrize("seed,N,R", [(0, 1, 16), (1, 2, 16), (2, 5, 16), (3, 13, 16), (4, 64, 16), (5, 5, 16),
+                                      (6, 16, 7), (7, 17, 5), (8, 3, 1), (9, 5, 13)])
+def test_v2_random_matches_oracle(ctx, seed, N, R):
+    """N <= 16: replay_v2_rows_kernel (four replications per wavefront, R not a
+    multiple of four included); N > 16: replay_v2_kernel."""
+    tr, broker, stop, rt = v2_random(seed, R, N, 3000)
     g = run_v2_gpu(ctx, tr, broker, stop, rt, qcap=4096)
     o = ol.run_v2(tr["arrive"], tr["req"], broker, tr["mips"], tr["dl"], tr["ul"], tr["first_adv"], stop, rt,
                   threads=8)
