@@ -22,6 +22,9 @@
 // that one handler.  Broker state is wave-uniform; per-task outputs and the
 // broker's request list are written by lane 0 only and a node's queues by its
 // own lane only, so every memory location has one writer in program order.
+#include <stdlib.h>
+#include <string.h>
+
 #include "replay_common.h"
 
 namespace fognet {
@@ -422,48 +425,59 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
 // rest of its row with ds_bpermute, and every handler runs under a row-uniform
 // condition, so rows in different handlers only serialise those handlers.
 // Same arithmetic, same FES order, same outputs as replay_v2_kernel.
-constexpr int kRowLanes = 16;
-constexpr int kRowsPerWave = kWave / kRowLanes;
-
+// Row width W (16 or 32 lanes): W = 16 packs four replications per wavefront
+// (1,024 waves at the C1 size, one per SIMD); W = 32 packs two (2,048 waves, two
+// per SIMD, so one wave's latencies overlap the other's work).
+template <int W>
 __device__ __forceinline__ uint64_t row_min_u64(uint64_t v) {
   v = umin64(v, dpp_u64<0xB1>(v));
   v = umin64(v, dpp_u64<0x4E>(v));
   v = umin64(v, dpp_u64<0x141>(v));
   v = umin64(v, dpp_u64<0x140>(v));
+  if constexpr (W == 32) v = umin64(v, shfl_xor_u64(v, 16));
   return v;
 }
 
+template <int W>
 __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
   v = min(v, dpp_u32<0xB1>(v));
   v = min(v, dpp_u32<0x4E>(v));
   v = min(v, dpp_u32<0x141>(v));
   v = min(v, dpp_u32<0x140>(v));
+  if constexpr (W == 32) v = min(v, (uint32_t)__shfl_xor((int)v, 16, kWave));
   return v;
 }
 
+template <int W>
 __device__ __forceinline__ int64_t row_sum_i64(int64_t v) {
   v += (int64_t)dpp_u64<0xB1>((uint64_t)v);
   v += (int64_t)dpp_u64<0x4E>((uint64_t)v);
   v += (int64_t)dpp_u64<0x141>((uint64_t)v);
   v += (int64_t)dpp_u64<0x140>((uint64_t)v);
+  if constexpr (W == 32) v += (int64_t)shfl_xor_u64((uint64_t)v, 16);
   return v;
 }
 
-// value of lane w (0..15) of this lane's row (every lane of the row active)
+// value of lane w of this lane's row (every lane of the row active)
+template <int W>
 __device__ __forceinline__ uint32_t row_bcast_u32(uint32_t v, int w) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((threadIdx.x & ~(kRowLanes - 1u)) | (uint32_t)w) << 2), (int)v);
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((threadIdx.x & ~(W - 1u)) | (uint32_t)w) << 2), (int)v);
 }
 
+template <int W>
 __device__ __forceinline__ uint64_t row_bcast_u64(uint64_t v, int w) {
-  return ((uint64_t)row_bcast_u32((uint32_t)(v >> 32), w) << 32) | row_bcast_u32((uint32_t)v, w);
+  return ((uint64_t)row_bcast_u32<W>((uint32_t)(v >> 32), w) << 32) | row_bcast_u32<W>((uint32_t)v, w);
 }
 
 // some lane of this lane's row has p (the row's lanes active)
+template <int W>
 __device__ __forceinline__ bool row_any(bool p) {
-  return ((ballot(p) >> (threadIdx.x & ~(kRowLanes - 1u))) & 0xFFFFull) != 0ull;
+  return ((ballot(p) >> (threadIdx.x & ~(W - 1u))) & ((1ull << W) - 1ull)) != 0ull;
 }
 
+template <int kRowLanes>
 __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
+  constexpr int kRowsPerWave = kWave / kRowLanes;
   const fognet_v2_in& A = P.in;
   const fognet_v2_out& O = P.out;
   const int lane = threadIdx.x;
@@ -521,7 +535,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   int64_t p_tick = (live && T > 0) ? arrive[0] : kNever;  // the next publish, loaded one publish ahead
   int32_t p_req = (live && T > 0) ? reqs[0] : 0;
   fognet_v2_stats st = {};
-  uint32_t err = row_any(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
+  uint32_t err = row_any<kRowLanes>(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
   bool fin = !live || err != FOGNET_OK;  // row-uniform: this replication's loop has ended
   bad = false;
 
@@ -546,10 +560,10 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       cs = out_hd.seq;
       src = 3;
     }
-    const int64_t m_tick = (int64_t)row_min_u64((uint64_t)ct);
+    const int64_t m_tick = (int64_t)row_min_u64<kRowLanes>((uint64_t)ct);
     const bool at = src != 0 && ct == m_tick;
-    const uint64_t m_seq = row_min_u64(at ? cs : ~0ull);  // same-tick events: insertion order decides
-    const uint32_t wl = row_min_u32(at && cs == m_seq ? (uint32_t)li : 0xFFu);
+    const uint64_t m_seq = row_min_u64<kRowLanes>(at ? cs : ~0ull);  // same-tick events: insertion order decides
+    const uint32_t wl = row_min_u32<kRowLanes>(at && cs == m_seq ? (uint32_t)li : 0xFFu);
     const int w = wl == 0xFFu ? 0 : (int)wl;
     int kind = wl == 0xFFu ? 0 : 1;  // 1 node-side event of lane w, 2 publish, 3 broker timer
     int64_t e_tick = kind ? m_tick : kNever;
@@ -614,9 +628,9 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
         }
       } else {
         // the LAST node whose advertised MIPS exceeds node 0's (:241-248), else node 0
-        const int32_t v0 = (int32_t)row_bcast_u32((uint32_t)view, 0);
-        k = (int32_t)(15u - row_min_u32(15u - ((own && li >= 1 && view > v0) ? (uint32_t)li : 0u)));
-        const int32_t vk = (int32_t)row_bcast_u32((uint32_t)view, k);
+        const int32_t v0 = (int32_t)row_bcast_u32<kRowLanes>((uint32_t)view, 0);
+        k = (int32_t)((kRowLanes - 1u) - row_min_u32<kRowLanes>((kRowLanes - 1u) - ((own && li >= 1 && view > v0) ? (uint32_t)li : 0u)));
+        const int32_t vk = (int32_t)row_bcast_u32<kRowLanes>((uint32_t)view, k);
         lmark = kListForwarded;  // :255-260, before the MIPS check
         if (req < vk) {          // :262-270: FognetMsgTask to node k
           status = FOGNET_V2_ST_FORWARDED;
@@ -632,7 +646,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
             }
           }
           ++seq;
-          if (row_any(bad)) {
+          if (row_any<kRowLanes>(bad)) {
             err = FOGNET_ERR_CAPACITY;
             fin = true;
           }
@@ -667,9 +681,9 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
           }
         }
       }
-      list_h = (int)row_bcast_u32((uint32_t)list_h, 0);
-      rel = (int)row_bcast_u32((uint32_t)rel, 0);
-      mark = row_bcast_u32(mark, 0);
+      list_h = (int)row_bcast_u32<kRowLanes>((uint32_t)list_h, 0);
+      rel = (int)row_bcast_u32<kRowLanes>((uint32_t)rel, 0);
+      mark = row_bcast_u32<kRowLanes>(mark, 0);
       if (rel >= 0) {
         pool += reqs[rel];  // :386
         ++st.n_released_broker;
@@ -677,11 +691,11 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       }
     } else {
       // ---- an event of node w
-      const int wsrc = (int)row_bcast_u32((uint32_t)src, w);
+      const int wsrc = (int)row_bcast_u32<kRowLanes>((uint32_t)src, w);
       if (wsrc == 3) {
         // a node -> broker message reaches the broker (BrokerBaseApp2.cc:128-154)
-        const int32_t mk = (int32_t)row_bcast_u32((uint32_t)out_hd.kind, w);
-        const int32_t mv = (int32_t)row_bcast_u32((uint32_t)out_hd.val, w);
+        const int32_t mk = (int32_t)row_bcast_u32<kRowLanes>((uint32_t)out_hd.kind, w);
+        const int32_t mv = (int32_t)row_bcast_u32<kRowLanes>((uint32_t)out_hd.val, w);
         if (li == w) {
           ++out_h;
           --out_n;
@@ -694,7 +708,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
             list[mv] = kListNone;
             relayed = true;
           }
-          if (row_any(relayed)) ++st.n_relayed;
+          if (row_any<kRowLanes>(relayed)) ++st.n_relayed;
         }
       } else {
         // the node's own events: its self-message or a task arrival.  The owner
@@ -762,14 +776,14 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
             }
           }
         }
-        if (row_any(bad)) {
+        if (row_any<kRowLanes>(bad)) {
           err = FOGNET_ERR_CAPACITY;
           fin = true;
           continue;
         }
-        seq = row_bcast_u64(my_seq, w);
-        o_task = (int32_t)row_bcast_u32((uint32_t)o_task, w);
-        o_what = row_bcast_u32(o_what, w);
+        seq = row_bcast_u64<kRowLanes>(my_seq, w);
+        o_task = (int32_t)row_bcast_u32<kRowLanes>((uint32_t)o_task, w);
+        o_what = row_bcast_u32<kRowLanes>(o_what, w);
         if (o_what == 1u) {
           ++st.n_released_node;
           if (li == 0) O.done_tick[tbase + o_task] = now;
@@ -796,7 +810,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       O.done_tick[tbase + t] = -1;
     }
   }
-  const int64_t msum = row_sum_i64(own ? (int64_t)mips : 0);
+  const int64_t msum = row_sum_i64<kRowLanes>(own ? (int64_t)mips : 0);
   if (live && li == 0) {
     st.node_mips_final_sum = msum;
     st.broker_mips_final = pool;
@@ -824,8 +838,13 @@ hipError_t launch_replay_v2(const fognet_v2_in& in, const fognet_v2_out& out, vo
   a.outq = a.inq + q;
   a.res = reinterpret_cast<V2Res*>(a.outq + q);
   a.list = reinterpret_cast<uint8_t*>(a.res + q);
-  if (in.N <= kRowLanes)  // four replications per wavefront
-    hipLaunchKernelGGL(replay_v2_rows_kernel, dim3((in.R + kRowsPerWave - 1) / kRowsPerWave), dim3(kWave), 0, s, a);
+  // rows of 16 lanes (four replications per wavefront) unless FOGNET_V2_ROW=32 (two) or N > 16
+  const char* rw = getenv("FOGNET_V2_ROW");
+  const int row = (in.N > 16 || (rw && strcmp(rw, "32") == 0)) ? 32 : 16;
+  if (in.N <= 16 && row == 16)
+    hipLaunchKernelGGL(replay_v2_rows_kernel<16>, dim3((in.R + 3) / 4), dim3(kWave), 0, s, a);
+  else if (in.N <= 32)
+    hipLaunchKernelGGL(replay_v2_rows_kernel<32>, dim3((in.R + 1) / 2), dim3(kWave), 0, s, a);
   else
     hipLaunchKernelGGL(replay_v2_kernel, dim3(in.R), dim3(kWave), 0, s, a);
   return hipGetLastError();

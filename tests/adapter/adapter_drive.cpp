@@ -38,6 +38,7 @@ struct Harness : BrokerBaseAppHip {
     std::vector<std::string> ids;
     void setup(int n) {
         initialize(INITSTAGE_LOCAL);
+        ids.reserve(n);  // Broker keeps the id's pointer
         for (int j = 0; j < n; ++j) {
             ids.push_back("node" + std::to_string(j));
             brokers.push_back(new Broker(ids.back().c_str(), L3Address(100 + j), 2000 + j, 0));

@@ -6,19 +6,19 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 rm -rf gpurun_out/pmc_c1; mkdir -p gpurun_out/pmc_c1
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE \
   --output-format csv -d gpurun_out/pmc_c1/p1 -o p1 -- \
   python3 bench.py --workload c1 --steps 1 --warmup 0 --no-cpu > gpurun_out/pmc_c1/p1.log 2>&1 || exit 1
 python3 - <<'PY'
-import json, sys
+import json, os, sys
 sys.path.insert(0, "tools")
 import pmc_summary
-d = pmc_summary.load("gpurun_out/pmc_c1", kernel="replay_v2_kernel")
+d = pmc_summary.load("gpurun_out/pmc_c1", kernel=os.environ.get("KERNEL", "replay_v2_rows_kernel"))
 per = {k: v / n for k, (v, n) in d.items()}
 line = [l for l in open("gpurun_out/pmc_c1/p1.log") if l.startswith("{")][-1]
 b = json.loads(line)
 dec, ev = b["stats"]["decisions"], b["stats"]["events"]
-out = {"kernel": "replay_v2_kernel", "per_dispatch": per,
+out = {"kernel": os.environ.get("KERNEL", "replay_v2_rows_kernel"), "per_dispatch": per,
        "valu_busy": per["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (per["GRBM_GUI_ACTIVE"] / 8),
        "SQ_INSTS_VALU_per_event": per["SQ_INSTS_VALU"] / ev, "SQ_INSTS_SALU_per_event": per["SQ_INSTS_SALU"] / ev,
        "SQ_INSTS_VALU_per_decision": per["SQ_INSTS_VALU"] / dec,
