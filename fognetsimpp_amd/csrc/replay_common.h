@@ -9,8 +9,9 @@
 namespace fognet {
 
 constexpr int64_t kNever = INT64_MAX;
-// Simulated ticks are kept below 2^61 (26.7 days) and service times below
-// 2^16 s, so no intermediate of the replay arithmetic can overflow int64.
+// Simulated ticks are kept below 2^61 (26.7 days); service seconds enter the
+// tick arithmetic clamped (2^22 s in the wide kernel, 255 s in the register
+// kernel), so no intermediate of the replay arithmetic can overflow int64.
 constexpr int64_t kMaxTick = (int64_t)1 << 61;
 
 // FOGNET_POLICY_EXT_LAT bounds (fognet_hip.h): service saturates at 2^20 s,
@@ -27,8 +28,10 @@ __device__ __forceinline__ int64_t ticks_of(uint32_t s) {
 // arrival at tick `a` happens before the completion at `done` of a task with
 // service S on a node with downlink latency dl (FES insertion-order rule,
 // DESIGN.md §3.3).
+// (S is clamped at 2^22 s: dl < 2^61 ticks is below 2^22 s in ticks, so the
+// comparison is unchanged and S * 1e12 cannot overflow)
 __device__ __forceinline__ bool arrives_before(int64_t a, int64_t done, int64_t dl, uint32_t S) {
-  return a < done || (a == done && dl >= (int64_t)S * kTicksPerSecond);
+  return a < done || (a == done && dl >= (int64_t)min(S, 1u << 22) * kTicksPerSecond);
 }
 
 // Separately rounded IEEE double operations.  hipcc contracts a*b+c into an

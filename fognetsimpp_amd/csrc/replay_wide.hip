@@ -47,7 +47,18 @@ namespace fognet {
 
 namespace {
 
-constexpr uint32_t kWideMaxS = 0xFFFFu;  // service seconds < 2^16 (kMaxTick arithmetic)
+// Service seconds are any int / int (ComputeBrokerApp3.cc:276: up to 2^31 - 1).
+// The tick arithmetic clamps them at kWideSCap: a task that is served with
+// a service time (or a run prefix) of 2^22 s or more completes past kMaxTick
+// (2^61 ticks = 26.7 days, 2^22 s = 48.5 days) and the replication is refused
+// by the completion-tick check, so the clamp never changes a result; the
+// cumulative service sums (advertised busy values) stay exact in 64 bits.
+constexpr uint32_t kWideSCap = 1u << 22;
+// Saturated advertised busy time in the 32-bit view (also the busy value of the
+// view's slots past N, which never win: their index is larger).
+constexpr uint32_t kBusySat = 0xFFFFFFFFu;
+// A start or completion tick at or past base + 2^22 s (beyond kMaxTick).
+constexpr int64_t kPastRange = kMaxTick + 1;
 
 // Per-lane minima are kept in two levels: for each group of kWideGroupSlots
 // of the lane's slots the earliest pending advert, its node and the smallest
@@ -204,7 +215,8 @@ __device__ __forceinline__ int64_t lane_min_w(const WideLds& L, int lane) {
 // the view takes busyTime after releaseResource (ComputeBrokerApp3.cc:232,
 // :254) = the service of the tasks that reached j before that completion and
 // are not done yet, a difference of cumulative sums; the head advances.
-// Returns false when the advertised busy time does not fit 32 bits.
+// Returns false when the advertised busy time is 2^24 s or more (only the
+// EXT_LAT cost cares: its uint64 tick arithmetic needs busy < 2^24).
 // h: node j's record (loaded from HBM or the lane's cached copy), updated in place.
 // up: FOGNET_POLICY_EXT_HIER's extra hop, which an escalated task (entry pad
 // != 0, bit 31 of the record's tl_S for the tail) took before its downlink:
@@ -229,7 +241,9 @@ __device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, in
     }
   }
   const uint64_t busy = c_arrived - h.hd_C;
-  busy_j = (uint32_t)busy;
+  // the view keeps 32 bits, saturated: a saturated node can only be chosen when the
+  // decision's minimum itself is saturated, which the decision refuses (kBusySat)
+  busy_j = busy < (uint64_t)kBusySat ? (uint32_t)busy : kBusySat;
   h.npend -= 1;
   if (h.npend == 0) {
     nxt_j = kNever;
@@ -243,7 +257,7 @@ __device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, in
     h.hd_next = nx.next;  // valid while npend >= 2
     nxt_j = nx.done == kNever ? kNever : nx.done + ul;  // never: crashed before it completes
   }
-  return busy < 0xFFFFFFFFull;
+  return busy < ((uint64_t)1 << 24);  // FOGNET_POLICY_EXT_LAT's cost needs busy < 2^24
 }
 
 // Workspace layout (launch_replay_wide, replay_wide_workspace_bytes).
@@ -472,7 +486,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           if constexpr (!kPerPublish) group_load_w(V, g, gw);
           WideNode h = hit ? ch : nd[j];
           const int64_t dl_j = hit ? c_dl : P_dl[j];
-          lerr |= !apply_advert(h, e, dl_j, hit ? c_ul : P_ul[j], kHier ? A.hier_up : 0, nxt_j, busy_j);
+          const bool fits = apply_advert(h, e, dl_j, hit ? c_ul : P_ul[j], kHier ? A.hier_up : 0, nxt_j, busy_j);
+          if constexpr (kExt) lerr |= !fits;
           if (hit) ch = h;
           else nd[j] = h;
           V.nxt[sl] = nxt_j;
@@ -543,6 +558,10 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           glob_key = wave_min_u64(mk);
           glob_valid = true;
         }
+        if (((escalated ? glob_key : kb) >> 32) >= kBusySat) {  // the minimum is past 32 bits
+          err = FOGNET_ERR_CAPACITY;
+          break;
+        }
         k = escalated ? (uint32_t)glob_key : (uint32_t)kb;
       } else if (view_changed) {
         // BrokerBaseApp3.cc:267-281: busy_j + req/mips_0 < tempp over exact
@@ -550,6 +569,10 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         k_key = wave_min_u64(mk);
         k = (uint32_t)k_key;
         view_changed = false;
+        if ((k_key >> 32) >= kBusySat) {  // the minimum is past 32 bits: exact order unknown
+          err = FOGNET_ERR_CAPACITY;
+          break;
+        }
       }
       const int kl = (int)(k % kWave);
 
@@ -599,7 +622,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           int64_t x0 = kNever;
           if (a0 < down_k && base_done != kNever) {
             const int64_t st0 = a0 > base_done ? a0 : base_done;
-            const int64_t d0 = st0 + ticks_of(min(S0, kWideMaxS));
+            const int64_t d0 = st0 + ticks_of(min(S0, kWideSCap));
             if (st0 < down_k && d0 < down_k) x0 = d0 + ul_k;
           }
           E = x0 < E ? x0 : E;
@@ -620,19 +643,26 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         S = udiv((uint32_t)cr, div_k);  // double tskTime = requiredMIPS / MIPS (:276)
         a = ca + dl_k;
       }
-      const uint32_t Sd = min(S, kWideMaxS);  // (a larger service time is an error unless the task is lost)
-      const bool one = Lr == 1;                // a single publish needs no wave scans
-      // service seconds of the run up to this task
+      const uint32_t Sd = min(S, kWideSCap);  // tick arithmetic (kWideSCap)
+      const bool one = Lr == 1;               // a single publish needs no wave scans
+      // service seconds of the run up to this task: clamped for the ticks (<= 64 * 2^22 < 2^32),
+      // exact in 64 bits for the cumulative service (a run with a longer service time is rare)
       const uint32_t Cs = one ? (in_run ? Sd : 0u) : wave_scan_add_u32(in_run ? Sd : 0u);
-      const uint64_t C = tl_C + (uint64_t)Cs;  // cumulative assigned service
+      uint64_t Cs64 = Cs;
+      if (ballot(in_run && S >= kWideSCap))
+        Cs64 = one ? (uint64_t)(in_run ? S : 0u) : (uint64_t)wave_scan_add_i64(in_run ? (int64_t)S : 0);
+      const uint64_t C = tl_C + Cs64;  // cumulative assigned service
       int64_t start = kNever, done = kNever;
       uint32_t status = FOGNET_TASK_LOST;
       if (base_done != kNever) {
-        int64_t X = in_run ? (int64_t)((uint64_t)a - (uint64_t)ticks_of(Cs - Sd)) : INT64_MIN;
+        int64_t X = in_run ? (int64_t)((uint64_t)a - (uint64_t)ticks_of(min(Cs - Sd, kWideSCap))) : INT64_MIN;
         if (!one) X = wave_scan_max_i64(X);
         const int64_t dmax = base_done > X ? base_done : X;
-        const int64_t dn = (int64_t)((uint64_t)dmax + (uint64_t)ticks_of(Cs));  // unclamped
-        const int64_t st = dn - ticks_of(Sd);
+        // start = dmax + the run's service before the task, done = dmax + through it; a prefix of
+        // 2^22 s or more puts the tick past kMaxTick (kPastRange: lost to a crash, else refused below;
+        // a clamped X only over-estimates lanes whose own prefix is past the cap)
+        const int64_t st = Cs - Sd < kWideSCap ? dmax + ticks_of(Cs - Sd) : kPastRange;
+        const int64_t dn = Cs < kWideSCap ? dmax + ticks_of(Cs) : kPastRange;
         int64_t prev_done = base_done;
         uint32_t prev_S = tl_S;
         if (!one) {
@@ -646,15 +676,14 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         if (in_run && a < down_k) {
           if (prev_done < a) status = 5u;       // idle: "task assigned" (:282-301)
           else if (prev_done > a) status = 4u;  // busy: "task queued" (:304-313)
-          else status = dl_k < (int64_t)prev_S * kTicksPerSecond ? 5u : 4u;  // same-tick completion
+          else status = dl_k < (int64_t)min(prev_S, kWideSCap) * kTicksPerSecond ? 5u : 4u;  // same-tick completion
           start = st < down_k ? st : kNever;   // the crash cancels its RELEASERESOURCE
           done = dn < down_k ? dn : kNever;
         }
       } else if (in_run && a < down_k) {
         status = 4u;  // queued behind a task the crashed node never completes
       }
-      lerr2 = in_run && ((status != FOGNET_TASK_LOST && S > kWideMaxS) || a > kMaxTick ||
-                         (done != kNever && done > kMaxTick));
+      lerr2 = in_run && (a > kMaxTick || (done != kNever && done > kMaxTick));
       if (ballot(lerr2)) {
         err = FOGNET_ERR_ARG;
         break;

@@ -242,6 +242,17 @@ static void user_ack(sim_t *s, const ev_t *e) {
     else if (e->mips == 6) moment_add_ms(&u->taskTime, v);  /* :279-291 */
 }
 
+/* The engine's simulated-time range (fognet_hip.h: every tick below 2^61, 26.7
+ * days).  A RELEASERESOURCE past it is refused (ORC_ERR_ARG) like the engine
+ * refuses it; it also keeps tskTime * 1e12 clear of int64 overflow. */
+#define ORC_MAX_TICK ((int64_t)1 << 61)
+
+static int release_tick(const sim_t *s, double tskTime, int64_t *tick) {
+    if (!(tskTime < 4194304.0)) return ORC_ERR_ARG; /* 2^22 s > 2^61 ticks */
+    *tick = s->now + (int64_t)tskTime * TICKS_PER_SECOND;
+    return *tick > ORC_MAX_TICK ? ORC_ERR_ARG : ORC_OK;
+}
+
 /* cSimpleModule::scheduleAt for a node's selfMsg. */
 static int node_schedule_self(sim_t *s, int32_t k, int64_t tick, int kind) {
     node_t *nd = &s->nodes[k];
@@ -330,8 +341,10 @@ static int node_release(sim_t *s, int32_t k) {
         nd->qn--;
         if (s->out->start_tick) s->out->start_tick[nd->currentTask.task] = s->now;
         node_cancel_self(s, k); /* :248-249 */
-        int64_t d = (int64_t)nd->currentTask.required_time * TICKS_PER_SECOND;
-        int rc = node_schedule_self(s, k, s->now + d, KIND_RELEASERESOURCE); /* :250 */
+        int64_t at;
+        int rc = release_tick(s, nd->currentTask.required_time, &at);
+        if (rc) return rc;
+        rc = node_schedule_self(s, k, at, KIND_RELEASERESOURCE); /* :250 */
         if (rc) return rc;
     }
     return node_advertise(s, k, t); /* :254 */
@@ -358,8 +371,10 @@ static int node_task(sim_t *s, int32_t k, int64_t t) {
         nd->currentTask.qstart_tick = s->now;
         if (s->out->start_tick) s->out->start_tick[t] = s->now;
         s->st.n_started++;
-        int64_t d = (int64_t)tskTime * TICKS_PER_SECOND;
-        return node_schedule_self(s, k, s->now + d, KIND_RELEASERESOURCE); /* :299-301, no cancelEvent */
+        int64_t at;
+        int rc = release_tick(s, tskTime, &at);
+        if (rc) return rc;
+        return node_schedule_self(s, k, at, KIND_RELEASERESOURCE); /* :299-301, no cancelEvent */
     }
     /* busy: FIFO enqueue (:305-309), ack status 4 "task queued" (:310-313) */
     if (nd->qn == nd->qcap) {

@@ -262,6 +262,62 @@ def test_service_past_register_kernel_bound(ctx):
     assert sep.rep_stats().tobytes() == g["stats"].tobytes()
 
 
+@pytest.mark.parametrize("N", [8, 300])  # handed over by the register kernel / the wide kernel
+def test_service_times_past_2_16_seconds(ctx, N):
+    """The reference accepts any int / int service time (ComputeBrokerApp3.cc:276):
+    tasks of 65,536 s to 1,000,000 s (11.6 days), runs of them on one node, all
+    completing within the engine's 2^61-tick range, match the oracle; a task
+    completing past it is refused (FOGNET_ERR_ARG) by both."""
+    tr = tg.make_batch(29, 3, N, 500, rho=0.5)
+    tr = {k: v.copy() for k, v in tr.items()}
+    m0 = int(tr["mips"][0, 0])
+    tr["req"][0, 40] = 65536 * m0            # exactly 2^16 s on node 0 (ties -> node 0 decides it)
+    tr["req"][1, 10:14] = 300_000 * 1000     # a run of 300,000 s tasks
+    tr["req"][1, 200] = 1_000_000 * 1000     # 11.6 days
+    tr["req"][2, ::97] = 2**31 - 1           # up to 2^31 - 1 s: completes past 2^61 ticks
+    g = run_gpu_full(ctx, tr)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=3, hist=True)
+    assert list(g["stats"]["status"][:2]) == [0, 0] and g["stats"]["status"][2] == _abi.FOGNET_ERR_ARG
+    assert o["stats"]["status"][2] == 1  # ORC_ERR_ARG
+    two = {k: (v[:2] if k in ("node", "status", "start", "done", "stats") else v) for k, v in g.items()}
+    ref = {k: (v[:2] if k in ("node", "status", "start", "done", "stats") else v) for k, v in o.items()}
+    assert_parity(tr, two, ref)
+    assert (g["done"][1] - g["start"][1]).max() == 1_000_000 * TPS
+
+
+def test_saturated_advertised_busy(ctx):
+    """A node that advertises 2^32 s or more of queued service (2,200 tasks of
+    2e6 s queued on it that its crash keeps from ever completing, node-down
+    extension): the
+    32-bit view saturates, the node is never the minimum, decisions equal the
+    oracle's; with one node the minimum itself is saturated and the replication
+    is refused (FOGNET_ERR_CAPACITY) instead of guessing the order."""
+    MS = 10**9
+    res = {}
+    for N in (2, 1):
+        mips = np.full(N, 1, np.int32)  # service = MIPSRequired seconds
+        dl = np.full(N, MS, np.int64)
+        ul = np.full(N, MS, np.int64)
+        init = np.full(N, MS, np.int64)
+        q = 2200  # queued tasks of 2,000,000 s each: 4.4e9 s > 2^32 s advertised
+        arrive = np.concatenate([[50 * MS], 50 * MS + 1 + np.arange(q), [5 * TPS, 6 * TPS, 7 * TPS]]).astype(np.int64)
+        req = np.concatenate([[1], np.full(q, 2_000_000), [1, 1, 1]]).astype(np.int32)
+        down = np.full(N, np.iinfo(np.int64).max, np.int64)
+        down[0] = 51 * MS + TPS + 1  # just after task 0 (1 s) completes and advertises
+        tr = dict(arrive=arrive[None], req=req[None], mips=mips, dl=dl, ul=ul, init=init, down=down)
+        dev = torch.device("cuda", ctx.device)
+        out = fa.run_batch(ctx, fa.as_device_trace(tr, dev))
+        torch.cuda.synchronize()
+        st = out.rep_stats()[0]
+        o = ol.run_batch(arrive[None], req[None], mips, dl, ul, init, down=down)
+        res[N] = (st, out.node[0].cpu().numpy(), o)
+    st, node, o = res[2]
+    assert st["status"] == 0
+    np.testing.assert_array_equal(node, o["node"][0])
+    assert list(node[-3:]) == [1, 1, 1]  # node 0 advertised 4.4e9 s of work
+    assert res[1][0]["status"] == _abi.FOGNET_ERR_CAPACITY
+
+
 def test_compact_ring_bounds_hand_over(ctx):
     """The register kernel's 8-B ring entries (internal.h RingWord: arrival
     < 2^56 ticks, service < 256 s): a replication with a longer service time or
