@@ -71,8 +71,19 @@ struct WideLds {
   int64_t* g_w;     // [G][64] REF_V3 run horizon: smallest w (node_w) of the group
   uint32_t* hist;   // [FOGNET_HIST_METRICS][FOGNET_HIST_BINS]
   uint64_t* reg_key;  // [G] EXT_HIER: cached regional minimum key (valid per reg_valid)
+  // EXT_HIER: escalated tasks decided but not yet pushed onto their node (slot per lane)
+  int64_t* p_t;     // [64] publish tick
+  int64_t* p_a;     // [64] arrival tick at the node
+  int32_t* p_i;     // [64] task index (-1: free slot)
+  int32_t* p_k;     // [64] node
+  int32_t* p_r;     // [64] MIPSRequired
   int G;
 };
+
+// EXT_HIER pending escalated tasks: at most one per lane (a replication with more
+// escalated tasks in flight at once, i.e. decided within one hop latency of each
+// other, is refused with FOGNET_ERR_UNSUPPORTED).
+constexpr int kHierPending = kWave;
 
 // This lane's view in HBM: slot s (node s * 64 + lane) at [s].
 struct WideView {
@@ -333,6 +344,11 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   L.g_j = reinterpret_cast<int32_t*>(L.g_w + L.G * kWave);
   L.hist = reinterpret_cast<uint32_t*>(L.g_j + L.G * kWave);
   L.reg_key = reinterpret_cast<uint64_t*>(L.hist + FOGNET_HIST_METRICS * FOGNET_HIST_BINS);
+  L.p_t = reinterpret_cast<int64_t*>(L.reg_key + L.G);
+  L.p_a = L.p_t + kHierPending;
+  L.p_i = reinterpret_cast<int32_t*>(L.p_a + kHierPending);
+  L.p_k = L.p_i + kHierPending;
+  L.p_r = L.p_k + kHierPending;
   const int SP = L.G * kWideGroupSlots;
   const WideView V{VN + ((size_t)wr * kWave + lane) * SP, VB + ((size_t)wr * kWave + lane) * SP,
                    VW + ((size_t)wr * kWave + lane) * SP};
@@ -386,6 +402,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     if constexpr (!kPerPublish) V.w[s] = kNever;
   }
   for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) L.hist[h] = 0u;
+  L.p_i[lane] = -1;  // EXT_HIER pending slots: free
   for (int g = 0; g < L.G; ++g) {  // the initial view: nothing pending, every busy 0
     const int j0 = g * kWideGroupSlots * kWave + lane;
     L.g_nxt[g * kWave + lane] = kNever;
@@ -417,6 +434,139 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   int32_t c_mips = 1;
   uint64_t c_dv = 1ull;
   int64_t c_dl = 0, c_ul = 0, c_down = kNever;
+
+  // record and parameters of node kk into its owner lane's cache
+  auto cache_node = [&](uint32_t kk) {
+    if (lane == (int)(kk % kWave) && (int)kk != cj) {
+      if (cj >= 0) nd[cj] = ch;  // write back the previous node's record
+      cj = (int)kk;
+      ch = nd[kk];
+      c_mips = P_mips[kk];
+      c_dv = GN.dv[sbase + kk];
+      c_dl = P_dl[kk];
+      c_ul = P_ul[kk];
+      c_down = A.down ? A.down[nbase + kk] : kNever;
+    }
+  };
+
+  // ---- FOGNET_POLICY_EXT_HIER: an escalated task takes the extra hop, so a
+  // direct task decided after it can reach the same node first; the node serves
+  // in arrival order.  Escalated tasks therefore wait in the pending slots
+  // (LDS, one per lane) and are pushed onto their node's chain only once every
+  // task that reaches the node no later than them has been pushed: before a
+  // direct task to the node with a later (or the same) arrival, before the
+  // adverts of a publish tick past their arrival (whose completions they may
+  // precede), and at the end.  Each chain stays in arrival order, so the FIFO
+  // recurrence and the advert scans hold as for direct tasks.  A pushed pending
+  // task's statistics and outputs are recorded at once (uniform code).
+  int n_pend = 0;  // occupied pending slots (wave-uniform)
+  auto pend_count = [&](uint32_t kk) -> uint32_t {
+    return n_pend ? (uint32_t)__popcll(ballot(L.p_i[lane] >= 0 && (uint32_t)L.p_k[lane] == kk)) : 0u;
+  };
+  // push escalated task i (publish tick t_i, MIPSRequired req_i) onto node kk; false: past kMaxTick
+  auto push_one = [&](int i, int64_t t_i, uint32_t req_i, uint32_t kk) -> bool {
+    cache_node(kk);
+    const int kl = (int)(kk % kWave);
+    const UDiv div_k{readlane_u32((uint32_t)c_dv, kl), readlane_u32((uint32_t)(c_dv >> 32), kl)};
+    const int64_t dl_k = readlane_i64(c_dl, kl) + A.hier_up;  // (the hop, then the downlink)
+    const int64_t ul_k = readlane_i64(c_ul, kl), down_k = readlane_i64(c_down, kl);
+    const int32_t tl = (int32_t)readlane_u32((uint32_t)ch.tl, kl);
+    const int64_t tl_done = readlane_i64(ch.tl_done, kl);
+    const uint64_t tl_C = (uint64_t)readlane_i64((int64_t)ch.tl_C, kl);
+    const uint32_t tl_S = readlane_u32(ch.tl_S, kl) & 0x7FFFFFFFu;
+    const int64_t base_done = tl >= 0 ? tl_done : INT64_MIN;
+    const uint32_t S = udiv(req_i, div_k);  // double tskTime = requiredMIPS / MIPS (ComputeBrokerApp3.cc:276)
+    const int64_t a = t_i + dl_k;
+    const uint64_t C = tl_C + S;
+    int64_t start = kNever, done = kNever;
+    uint32_t status = FOGNET_TASK_LOST;
+    if (base_done != kNever) {  // FIFO: start = max(arrival, previous completion)
+      const int64_t st = a > base_done ? a : base_done;
+      const int64_t dn = S < kWideSCap ? st + ticks_of(S) : kPastRange;
+      if (a < down_k) {
+        if (base_done < a) status = 5u;
+        else if (base_done > a) status = 4u;
+        else status = dl_k < (int64_t)min(tl_S, kWideSCap) * kTicksPerSecond ? 5u : 4u;
+        start = st < down_k ? st : kNever;
+        done = dn < down_k ? dn : kNever;
+      }
+    } else if (a < down_k) {
+      status = 4u;
+    }
+    if (a > kMaxTick || (done != kNever && done > kMaxTick)) return false;
+    if (lane == 0) e[i] = WideEntry{a, done, C, S, tl, -1, 1};
+    if (lane == kl) {
+      WideNode h = ch;
+      if (h.npend == 0) {  // the node's head: its advert is the node's next one
+        h.hd = i;
+        h.hd_done = done;
+        h.hd_C = C;
+        h.hd_S = S;
+        const int64_t x = done == kNever ? kNever : done + ul_k;
+        const int g = ((int)kk / kWave) / kWideGroupSlots;
+        V.nxt[kk / kWave] = x;
+        if (x < L.g_nxt[g * kWave + lane]) {
+          L.g_nxt[g * kWave + lane] = x;
+          L.g_j[g * kWave + lane] = (int)kk;
+        }
+        if (x < mn) {
+          mn = x;
+          mj = (int)kk;
+        }
+      } else if (h.npend == 1) {
+        h.hd_next = i;
+      } else {
+        e[h.tl].next = i;
+      }
+      h.tl = i;
+      h.tl_a = a;
+      h.tl_done = done;
+      h.tl_C = C;
+      h.tl_S = S | 0x80000000u;  // escalated
+      h.npend += 1;
+      ch = h;
+    }
+    if (lane == 0) {
+      if (!A.no_task_out) {
+        const size_t o = tbase + (size_t)i;
+        A.out_node[o] = (int32_t)kk;
+        A.out_status[o] = (uint8_t)status;
+        A.out_start[o] = start == kNever ? -1 : start;
+        A.out_done[o] = done == kNever ? -1 : done;
+      }
+      if (done != kNever) {
+        acc_task(acc, ab, t_i, a, start, done, S, status, i, hist ? L.hist : nullptr);
+        if (hist) atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - t_i)], 1u);
+      } else {  // node-down, as at the chunk's end
+        n_short += 1;
+        if (status == 5u) acc.n5 += 1u;
+        if (status == 4u) {
+          acc.n4 += 1u;
+          if (start != kNever) acc_qtime(acc, ab, start, a, i, hist ? L.hist : nullptr);
+        }
+      }
+    }
+    return true;
+  };
+  // push the pending tasks of node kk arriving at or before lim (by_node), or of any
+  // node arriving before lim, in decision order (per node also arrival order)
+  auto flush_pending = [&](bool by_node, uint32_t kk, int64_t lim) -> bool {
+    while (n_pend > 0) {
+      const int32_t pi = L.p_i[lane];
+      const int64_t pa = L.p_a[lane];
+      const bool sel = pi >= 0 && (by_node ? ((uint32_t)L.p_k[lane] == kk && pa <= lim) : pa < lim);
+      const uint32_t mi = wave_min_u32(sel ? (uint32_t)pi : ~0u);
+      if (mi == ~0u) break;
+      const int sl = (int)__builtin_ctzll(ballot(sel && (uint32_t)pi == mi));
+      const int64_t t_i = readlane_i64(L.p_t[lane], sl);
+      const uint32_t k_i = readlane_u32((uint32_t)L.p_k[lane], sl);
+      const uint32_t r_i = readlane_u32((uint32_t)L.p_r[lane], sl);
+      if (lane == sl) L.p_i[lane] = -1;
+      --n_pend;
+      if (!push_one((int)mi, t_i, r_i, k_i)) return false;
+    }
+    return true;
+  };
 
   // the decision is recomputed only after an advert changed the view
   // (adverts are the only view updates, BrokerBaseApp3.cc:123-130)
@@ -458,6 +608,12 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     int jp = 0;
     while (jp < cnt) {
       const int64_t t = readlane_i64(ca, jp);
+      if constexpr (kHier) {  // escalated tasks that reached their node before t (before any advert of t)
+        if (n_pend && !flush_pending(false, 0u, t)) {
+          err = FOGNET_ERR_ARG;
+          break;
+        }
+      }
 
       // 1) completion adverts that reached the broker strictly before t
       bool lerr = false;
@@ -577,15 +733,40 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       const int kl = (int)(k % kWave);
 
       // 3) node k's record and parameters, in its owner lane (cached there)
-      if (lane == kl && (int)k != cj) {
-        if (cj >= 0) nd[cj] = ch;  // write back the previous node's record
-        cj = (int)k;
-        ch = nd[k];
-        c_mips = P_mips[k];
-        c_dv = GN.dv[sbase + k];
-        c_dl = P_dl[k];
-        c_ul = P_ul[k];
-        c_down = A.down ? A.down[nbase + k] : kNever;
+      cache_node(k);
+      uint32_t pend_k = 0u;  // EXT_HIER: k's escalated tasks still pending (decided, not pushed)
+      if constexpr (kHier) {
+        if (escalated) {  // wait in a pending slot until the tasks that reach k before it are pushed
+          const uint64_t fr = ballot(L.p_i[lane] < 0);
+          if (!fr) {
+            err = FOGNET_ERR_UNSUPPORTED;  // more than 64 escalated tasks in flight at once
+            break;
+          }
+          const int sl = (int)__builtin_ctzll(fr);
+          const int64_t a_esc = t + readlane_i64(c_dl, kl) + A.hier_up;
+          if (lane == sl) {
+            L.p_i[lane] = c0 + jp;
+            L.p_t[lane] = t;
+            L.p_a[lane] = a_esc;
+            L.p_k[lane] = (int32_t)k;
+            L.p_r[lane] = readlane_u32((uint32_t)cr, jp);
+          }
+          ++n_pend;
+          const uint32_t tot = (uint32_t)readlane_u32((uint32_t)ch.npend, kl) + pend_count(k);
+          max_pend = max(max_pend, tot);
+          n_done += 1;
+          jp += 1;
+          continue;
+        }
+        // a direct task: the pending escalated tasks that reach k no later than it go first
+        if (n_pend) {
+          if (!flush_pending(true, k, t + readlane_i64(c_dl, kl))) {
+            err = FOGNET_ERR_ARG;
+            break;
+          }
+          cache_node(k);
+          pend_k = pend_count(k);  // (those it overtakes)
+        }
       }
       const int32_t mips_k = (int32_t)readlane_u32((uint32_t)c_mips, kl);
       const UDiv div_k{readlane_u32((uint32_t)c_dv, kl), readlane_u32((uint32_t)(c_dv >> 32), kl)};
@@ -688,15 +869,6 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         err = FOGNET_ERR_ARG;
         break;
       }
-      if constexpr (kHier) {
-        // the node serves in arrival order; the chain is in decision order.  A task
-        // that reaches k before an escalated task decided earlier (which took the
-        // extra hop) would overtake it: not modelled, the replication fails loudly
-        if (ballot(lane == jp && in_run && a < readlane_i64(ch.tl_a, kl))) {
-          err = FOGNET_ERR_UNSUPPORTED;
-          break;
-        }
-      }
       // task entries: chained in publish order (consecutive task indices)
       const int i = c0 + lane;
       if (in_run) {
@@ -751,7 +923,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         h.tl_S = S_z | (escalated ? 0x80000000u : 0u);
         h.npend += Lr;
         ch = h;
-        max_pend = max(max_pend, (uint32_t)h.npend);
+        max_pend = max(max_pend, (uint32_t)h.npend + pend_k);
         if constexpr (!kPerPublish) {
           // k's w (a larger value may leave its group minimum stale-small: conservative)
           const int sk = (int)k / kWave, gk = sk / kWideGroupSlots;
@@ -790,6 +962,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     }
   }
 
+  if constexpr (kHier) {  // the escalated tasks still in flight at the end
+    if (err == FOGNET_OK && n_pend && !flush_pending(false, 0u, INT64_MAX)) err = FOGNET_ERR_ARG;
+  }
   if (cj >= 0) nd[cj] = ch;
 
   // ---- per-replication record (the fields replay_kernel + its epilogue write)
@@ -850,7 +1025,8 @@ void launch_wide_pol(const ReplayArgs& a, int32_t slots, WideEntry* e, WideNode*
 size_t replay_wide_lds_bytes(int32_t N) {
   const size_t G = (size_t)wide_groups(N);
   return G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int64_t) + sizeof(int32_t)) +
-         FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t) + G * sizeof(uint64_t);
+         FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t) + G * sizeof(uint64_t) +
+         kHierPending * (2 * sizeof(int64_t) + 3 * sizeof(int32_t));
 }
 
 size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen) { return wide_ws(R, T, N, gen).bytes; }

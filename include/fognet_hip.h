@@ -104,9 +104,11 @@ typedef enum fognet_policy {
                                    that busy exceeds hier_threshold_s the task is escalated to the
                                    parent broker, which applies the rule over ALL nodes, and
                                    reaches its node hier_up_tick later (the extra hop).  Adverts
-                                   reach every broker with the node's uplink latency.  A task
-                                   that would reach its node before an escalated task decided
-                                   earlier (overtaking it inside the hop) is not modelled: that
+                                   reach every broker with the node's uplink latency.  A direct
+                                   task can reach a node before an escalated task decided earlier
+                                   (it overtakes it inside the hop): the node serves in arrival
+                                   order.  More than 64 escalated tasks in flight at once
+                                   (decided within one hop of each other) are not modelled: that
                                    replication's status is FOGNET_ERR_UNSUPPORTED.            */
 } fognet_policy;
 
