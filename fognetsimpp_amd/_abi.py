@@ -24,6 +24,7 @@ FOGNET_ERR_CAPACITY = 7
 FOGNET_ERR_UNSUPPORTED = 8
 FOGNET_REF_ABORTED = 9  # replication status under FLAG_REF_ABORT
 FLAG_REF_ABORT = 1  # fognet_batch_in.flags
+FOGNET_ERR_INTERNAL = 10  # an internal invariant check failed
 TASK_QUEUED, TASK_STARTED, TASK_LOST = 4, 5, 9  # fognet_task_status
 
 FOGNET_POLICY_REF_V3 = 1

@@ -201,6 +201,7 @@ const char* fognet_status_string(int s) {
     case FOGNET_ERR_CAPACITY: return "capacity exceeded";
     case FOGNET_ERR_UNSUPPORTED: return "unsupported configuration";
     case FOGNET_REF_ABORTED: return "the reference run aborts (queueTime simtime overflow)";
+    case FOGNET_ERR_INTERNAL: return "internal invariant check failed";
   }
   return "unknown status";
 }

@@ -232,12 +232,25 @@ __device__ __forceinline__ int64_t lane_min_w(const WideLds& L, int lane) {
 // up: FOGNET_POLICY_EXT_HIER's extra hop, which an escalated task (entry pad
 // != 0, bit 31 of the record's tl_S for the tail) took before its downlink:
 // the same-tick rule compares the arrival's own insertion tick.
+// broken: the chain invariant failed (see below; a library bug, never an input).
 __device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, int64_t dl, int64_t ul, int64_t up,
-                                             int64_t& nxt_j, uint32_t& busy_j) {
+                                             int64_t& nxt_j, uint32_t& busy_j, bool& broken) {
   // the entry after the head, loaded first: for the lane's cached node h is in
   // registers, so this load issues together with the group's view loads
   WideEntry nx{};
-  if (h.npend >= 2) nx = e[h.hd_next];
+  if (h.npend >= 2) {
+    nx = e[h.hd_next];
+    // Chain invariant, checked at every applied advert: with two or more tasks
+    // pending, the record's hd_next names the entry whose prev is the head and
+    // whose cumulative service is the head's plus its own.  hd_next changes on
+    // three paths -- this advert, a push onto a node with exactly one pending
+    // task (hd_next := the pushed task) and a multi-task run onto an idle node
+    // (hd_next := its second task) -- so any copy of it elsewhere (the round-2
+    // experiment kept one in the HBM view, refreshed only where the view is
+    // written: here and on a push onto an idle node) goes stale on the second
+    // path, and the next advert then advances the head to a wrong entry.
+    broken = nx.prev != h.hd || nx.C != h.hd_C + nx.S;
+  }
   uint64_t c_arrived = h.hd_C;  // only the completing task itself ...
   if (arrives_before(h.tl_a, h.hd_done, dl + ((h.tl_S >> 31) ? up : 0), h.hd_S)) {
     c_arrived = h.tl_C;  // ... or everything up to the newest task (the common case)
@@ -616,7 +629,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       }
 
       // 1) completion adverts that reached the broker strictly before t
-      bool lerr = false;
+      bool lerr = false, lbroken = false;
       if (ballot(mn < t)) view_changed = true;
       while (ballot(mn < t)) {
         if constexpr (kHier) {
@@ -642,8 +655,11 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           if constexpr (!kPerPublish) group_load_w(V, g, gw);
           WideNode h = hit ? ch : nd[j];
           const int64_t dl_j = hit ? c_dl : P_dl[j];
-          const bool fits = apply_advert(h, e, dl_j, hit ? c_ul : P_ul[j], kHier ? A.hier_up : 0, nxt_j, busy_j);
+          bool broken = false;
+          const bool fits =
+              apply_advert(h, e, dl_j, hit ? c_ul : P_ul[j], kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
           if constexpr (kExt) lerr |= !fits;
+          lbroken |= broken;
           if (hit) ch = h;
           else nd[j] = h;
           V.nxt[sl] = nxt_j;
@@ -667,6 +683,10 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           if (gk_new < mk) mk = gk_new;
           else if (mk == gk_old && gk_new > gk_old) mk = lane_min_key(L, lane);
         }
+      }
+      if (ballot(lbroken)) {
+        err = FOGNET_ERR_INTERNAL;
+        break;
       }
       if (ballot(lerr)) {
         err = FOGNET_ERR_CAPACITY;

@@ -72,9 +72,10 @@ typedef enum fognet_status {
                                    time is 2^32 - 1 s or more (the view keeps 32 bits, saturated: larger
                                    values only lose); EXT_LAT: an advertised busy time of 2^24 s or more */
     FOGNET_ERR_UNSUPPORTED = 8, /* configuration not implemented (e.g. N > 256, unknown policy)        */
-    FOGNET_REF_ABORTED = 9      /* replication status under FOGNET_FLAG_REF_ABORT: the reference run ends
+    FOGNET_REF_ABORTED = 9,     /* replication status under FOGNET_FLAG_REF_ABORT: the reference run ends
                                    at a queueTime emission that overflows (ComputeBrokerApp3.cc:238; see
                                    "Reference signal values"); outputs are still written in full     */
+    FOGNET_ERR_INTERNAL = 10    /* an internal invariant check of the replay failed (a library bug)   */
 } fognet_status;
 
 /* fognet_batch_in.flags */

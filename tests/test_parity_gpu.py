@@ -909,6 +909,39 @@ def test_wide_kernel_forced_equals_register_kernel(ctx, monkeypatch, N):
     np.testing.assert_array_equal(wide["hist"], narrow["hist"])
 
 
+@pytest.mark.parametrize("policy", ["REF_V3", "EXT_LAT"])
+def test_wide_head_next_paths(ctx, monkeypatch, policy):
+    """The three paths that set a node record's hd_next (the
+    root cause of round 2's wrong-decision experiment), each followed by the
+    node's advert, which advances the head to hd_next: a push onto a node with
+    one pending task, a push onto one with two, a multi-task run onto an idle
+    node; on the wide kernel the chain invariant is checked at every advert
+    (FOGNET_ERR_INTERNAL) and every output equals the oracle."""
+    monkeypatch.setenv("FOGNET_REPLAY_KERNEL", "wide")
+    MS = 10**9
+    N = 3
+    base = 50 * MS
+    # bursts of 1, 2, 3 and 6 publishes one tick apart onto the argmin, spaced so adverts land in between
+    ticks, reqs = [], []
+    for b, (n, gap_s) in enumerate(((1, 3), (2, 5), (3, 7), (6, 11), (2, 2), (1, 1))):
+        t0 = base + sum((3, 5, 7, 11, 2, 1)[:b]) * 10**12 + b * MS
+        for q in range(n):
+            ticks.append(t0 + q)
+            reqs.append((1 + (q + b) % 3) * 1000)
+    arrive = np.array(ticks, np.int64)[None]
+    req = np.array(reqs, np.int32)[None]
+    mips = np.full(N, 1000, np.int32)
+    dl = np.array([MS, 2 * MS, 3 * MS], np.int64)
+    ul = np.array([MS, MS, 2 * MS], np.int64)
+    init = np.full(N, 2 * MS, np.int64)
+    tr = dict(arrive=arrive, req=req, mips=mips, dl=dl, ul=ul, init=init)
+    g = run_gpu_full(ctx, tr, policy=policy)
+    o = ol.run_batch(arrive, req, mips, dl, ul, init, hist=True, policy=ol.POLICIES[policy])
+    assert g["stats"]["status"][0] == 0
+    assert_parity(tr, g, o)
+    assert int(g["stats"]["max_pending"][0]) >= 3
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_wide_tie_heavy(ctx, monkeypatch, seed):
     tr = tie_heavy(seed, 8, 1 + 37 * seed, 2000)
