@@ -475,6 +475,24 @@ __device__ __forceinline__ bool row_any(bool p) {
   return ((ballot(p) >> (threadIdx.x & ~(W - 1u))) & ((1ull << W) - 1ull)) != 0ull;
 }
 
+// The rows kernel's queue entry: V2Msg with a 32-bit insertion sequence (the
+// same 24-B slot of the workspace).  Sequence numbers start at N + T and grow
+// by at most three per event; a replication that would pass 2^32 - 256 is
+// refused (FOGNET_ERR_CAPACITY), so they never wrap.
+struct V2MsgR {
+  int64_t tick;
+  uint32_t seq;
+  int32_t kind;
+  int32_t val;
+  int32_t pad;
+};
+static_assert(sizeof(V2MsgR) == sizeof(V2Msg), "same queue slot");
+constexpr uint32_t kSeqLimit = 0xFFFFFF00u;
+
+__device__ __forceinline__ bool earlier32(int64_t t, uint32_t s, int64_t t2, uint32_t s2) {
+  return t < t2 || (t == t2 && s < s2);
+}
+
 template <int kRowLanes>
 __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   constexpr int kRowsPerWave = kWave / kRowLanes;
@@ -491,8 +509,8 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   const size_t nbase = (size_t)rr * (size_t)A.node_stride;
   const size_t tbase = (size_t)rr * (size_t)T;
   const size_t qbase = ((size_t)rr * (size_t)FOGNET_V2_MAX_NODES + (size_t)li) << P.q_log2;
-  V2Msg* const inq = P.inq + qbase;
-  V2Msg* const outq = P.outq + qbase;
+  V2MsgR* const inq = reinterpret_cast<V2MsgR*>(P.inq) + qbase;
+  V2MsgR* const outq = reinterpret_cast<V2MsgR*>(P.outq) + qbase;
   V2Res* const res = P.res + qbase;
   uint8_t* const list = P.list + tbase;
   const int64_t* const arrive = A.arrive_tick + tbase;
@@ -508,7 +526,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   int64_t dl = 0, ul = 0;
   bool t_sched = false;  // selfMsg->isScheduled()
   int64_t t_tick = kNever;
-  uint64_t t_seq = ~0ull;
+  uint32_t t_seq = ~0u;
   uint32_t t_kind = kKindAdvertise;
   bool bad = !(stop <= kMaxV2Tick) || !(rtx >= 0.0) || rt_ticks > kMaxV2Tick;
   if (own) {
@@ -519,89 +537,94 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
     bad |= dl < 0 || ul < 0 || fa < 0 || dl > kMaxV2Tick || ul > kMaxV2Tick || fa > kMaxV2Tick;
     t_sched = true;  // the first ADVERTISEMIPS firing, pre-inserted in node order
     t_tick = fa;
-    t_seq = (uint64_t)li;
+    t_seq = (uint32_t)li;
   }
   uint32_t in_h = 0u, in_n = 0u, out_h = 0u, out_n = 0u, rs_h = 0u, rs_n = 0u;
-  V2Msg in_hd = {kNever, ~0ull, 0, 0}, out_hd = {kNever, ~0ull, 0, 0};
+  V2MsgR in_hd = {kNever, ~0u, 0, 0, 0}, out_hd = {kNever, ~0u, 0, 0, 0};
 
   // ---- broker (row-uniform)
   int32_t pool = live ? A.broker_mips[rr] : 0;
   bool b_sched = false;
   int64_t b_tick = kNever;
-  uint64_t b_seq = ~0ull;
-  uint64_t seq = (uint64_t)N + (uint64_t)T;  // the publishes hold N .. N+T-1
+  uint32_t b_seq = ~0u;
+  uint32_t seq = (uint32_t)N + (uint32_t)T;  // the publishes hold N .. N+T-1
   int next = 0, list_h = 0;
   int64_t prev_pub = INT64_MIN;
   int64_t p_tick = (live && T > 0) ? arrive[0] : kNever;  // the next publish, loaded one publish ahead
   int32_t p_req = (live && T > 0) ? reqs[0] : 0;
-  fognet_v2_stats st = {};
+  // per-replication counts (32-bit: each is at most T, except events)
+  uint32_t c_tasks = 0, c_local = 0, c_fwd = 0, c_acc = 0, c_rej = 0, c_drop = 0, c_nonodes = 0, c_relb = 0,
+           c_infl = 0, c_reln = 0, c_relay = 0;
+  uint64_t c_events = 0;
   uint32_t err = row_any<kRowLanes>(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
   bool fin = !live || err != FOGNET_OK;  // row-uniform: this replication's loop has ended
   bad = false;
 
+  // (no `continue` inside: every path of a step falls through to its end, so the
+  // loop-carried state needs no copies at extra loop exits)
   while (ballot(!fin)) {
-    if (fin) continue;  // (finished rows wait for the others; their lanes stay off below)
+    if (!fin) {  // (finished rows wait for the others; their lanes stay off)
     // ---- the earliest event: the lanes' own sources, then the broker's
     int64_t ct = kNever;
-    uint64_t cs = ~0ull;
+    uint32_t cs = ~0u;
     int src = 0;  // 1 self-message, 2 task arrival, 3 message at the broker
     if (t_sched) {
       ct = t_tick;
       cs = t_seq;
       src = 1;
     }
-    if (in_n && earlier(in_hd.tick, in_hd.seq, ct, cs)) {
+    if (in_n && earlier32(in_hd.tick, in_hd.seq, ct, cs)) {
       ct = in_hd.tick;
       cs = in_hd.seq;
       src = 2;
     }
-    if (out_n && earlier(out_hd.tick, out_hd.seq, ct, cs)) {
+    if (out_n && earlier32(out_hd.tick, out_hd.seq, ct, cs)) {
       ct = out_hd.tick;
       cs = out_hd.seq;
       src = 3;
     }
     const int64_t m_tick = (int64_t)row_min_u64<kRowLanes>((uint64_t)ct);
     const bool at = src != 0 && ct == m_tick;
-    const uint64_t m_seq = row_min_u64<kRowLanes>(at ? cs : ~0ull);  // same-tick events: insertion order decides
+    const uint32_t m_seq = row_min_u32<kRowLanes>(at ? cs : ~0u);  // same-tick events: insertion order decides
     const uint32_t wl = row_min_u32<kRowLanes>(at && cs == m_seq ? (uint32_t)li : 0xFFu);
     const int w = wl == 0xFFu ? 0 : (int)wl;
     int kind = wl == 0xFFu ? 0 : 1;  // 1 node-side event of lane w, 2 publish, 3 broker timer
     int64_t e_tick = kind ? m_tick : kNever;
-    uint64_t e_seq = kind ? m_seq : ~0ull;
+    uint32_t e_seq = kind ? m_seq : ~0u;
     if (next < T) {
-      if (earlier(p_tick, (uint64_t)N + (uint64_t)next, e_tick, e_seq)) {
+      if (earlier32(p_tick, (uint32_t)N + (uint32_t)next, e_tick, e_seq)) {
         e_tick = p_tick;
-        e_seq = (uint64_t)N + (uint64_t)next;
+        e_seq = (uint32_t)N + (uint32_t)next;
         kind = 2;
       }
     }
-    if (b_sched && earlier(b_tick, b_seq, e_tick, e_seq)) {
+    if (b_sched && earlier32(b_tick, b_seq, e_tick, e_seq)) {
       e_tick = b_tick;
       e_seq = b_seq;
       kind = 3;
     }
-    if (kind == 0 || e_tick >= stop) {  // nothing left, or the sim-time-limit
+    if (kind == 0 || e_tick >= stop) fin = true;  // nothing left, or the sim-time-limit
+    if (!fin && seq >= kSeqLimit) {
+      err = FOGNET_ERR_CAPACITY;  // (32-bit insertion sequence)
       fin = true;
-      continue;
     }
     const int64_t now = e_tick;
-    ++st.events;
+    if (!fin) ++c_events;
 
-    if (kind == 2) {
+    if (fin) {
+    } else if (kind == 2 && (p_tick < prev_pub || p_tick > kMaxV2Tick)) {
+      err = FOGNET_ERR_ARG;  // trace not sorted / out of range
+      fin = true;
+    } else if (kind == 2) {
       // ---- publish: BrokerBaseApp2.cc:176-195 + sendPubAck(:205-287)
       const int t = next++;
-      if (p_tick < prev_pub || p_tick > kMaxV2Tick) {
-        err = FOGNET_ERR_ARG;  // trace not sorted / out of range
-        fin = true;
-        continue;
-      }
       prev_pub = p_tick;
       const int32_t req = p_req;
       if (next < T) {  // the following publish, in flight while this one is handled
         p_tick = arrive[next];
         p_req = reqs[next];
       }
-      ++st.n_tasks;
+      ++c_tasks;
       int32_t k = -1;
       uint32_t status;
       int64_t start = -1;
@@ -611,13 +634,13 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
         lmark = kListLocal;
         status = FOGNET_V2_ST_LOCAL;
         start = now;
-        ++st.n_local;
+        ++c_local;
         b_sched = true;  // cancelEvent + scheduleAt(now + requiredTime) (:226-229)
         b_tick = now + rt_ticks;
         b_seq = seq++;
       } else if (N == 0) {  // :273-285: scheduleAt without cancelEvent
         status = FOGNET_V2_ST_NO_NODES;
-        ++st.n_no_nodes;
+        ++c_nonodes;
         if (b_sched) {
           err = FOGNET_ERR_STATE;  // "scheduleAt(): message already scheduled"
           fin = true;
@@ -634,9 +657,9 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
         lmark = kListForwarded;  // :255-260, before the MIPS check
         if (req < vk) {          // :262-270: FognetMsgTask to node k
           status = FOGNET_V2_ST_FORWARDED;
-          ++st.n_forwarded;
+          ++c_fwd;
           if (li == k) {
-            const V2Msg m = {now + dl, seq, req, t};
+            const V2MsgR m = {now + dl, seq, req, t, 0};
             if (in_n == Q) {
               bad = true;
             } else {
@@ -652,7 +675,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
           }
         } else {
           status = FOGNET_V2_ST_DROPPED;
-          ++st.n_dropped;
+          ++c_drop;
         }
       }
       if (li == 0) {
@@ -686,8 +709,8 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       mark = row_bcast_u32<kRowLanes>(mark, 0);
       if (rel >= 0) {
         pool += reqs[rel];  // :386
-        ++st.n_released_broker;
-        if (mark == kListForwarded) ++st.n_inflated;
+        ++c_relb;
+        if (mark == kListForwarded) ++c_infl;
       }
     } else {
       // ---- an event of node w
@@ -708,7 +731,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
             list[mv] = kListNone;
             relayed = true;
           }
-          if (row_any<kRowLanes>(relayed)) ++st.n_relayed;
+          if (row_any<kRowLanes>(relayed)) ++c_relay;
         }
       } else {
         // the node's own events: its self-message or a task arrival.  The owner
@@ -716,7 +739,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
         // broadcast afterwards (lane 0 of the row writes the outputs).
         int32_t o_task = -1;   // task whose result changed
         uint32_t o_what = 0u;  // 1 released, 2 accepted, 3 rejected
-        uint64_t my_seq = seq;
+        uint32_t my_seq = seq;
         if (li == w) {
           if (wsrc == 1) {
             t_sched = false;
@@ -730,7 +753,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
                 --rs_n;
                 o_task = h.task;
                 o_what = 1u;
-                const V2Msg m = {now + ul, my_seq++, kMsgAck6, h.task};  // puback 6 (:231-235)
+                const V2MsgR m = {now + ul, my_seq++, kMsgAck6, h.task, 0};  // puback 6 (:231-235)
                 if (out_n == Q) bad = true;
                 else {
                   outq[(out_h + out_n) & qm] = m;
@@ -740,7 +763,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
               }
             }
             // advertiseMIPS (:202-220): advert, then the self-message again 0.01 s later
-            const V2Msg m = {now + ul, my_seq++, kMsgAdvert, mips};
+            const V2MsgR m = {now + ul, my_seq++, kMsgAdvert, mips, 0};
             if (out_n == Q) bad = true;
             else {
               outq[(out_h + out_n) & qm] = m;
@@ -776,29 +799,30 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
             }
           }
         }
-        if (row_any<kRowLanes>(bad)) {
-          err = FOGNET_ERR_CAPACITY;
-          fin = true;
-          continue;
-        }
-        seq = row_bcast_u64<kRowLanes>(my_seq, w);
+        seq = row_bcast_u32<kRowLanes>(my_seq, w);
         o_task = (int32_t)row_bcast_u32<kRowLanes>((uint32_t)o_task, w);
         o_what = row_bcast_u32<kRowLanes>(o_what, w);
+        if (row_any<kRowLanes>(bad)) {  // the replication ends here (nothing of this event is recorded)
+          err = FOGNET_ERR_CAPACITY;
+          fin = true;
+          o_what = 0u;
+        }
         if (o_what == 1u) {
-          ++st.n_released_node;
+          ++c_reln;
           if (li == 0) O.done_tick[tbase + o_task] = now;
         } else if (o_what == 2u) {
-          ++st.n_accepted;
+          ++c_acc;
           if (li == 0) {
             O.status[tbase + o_task] = FOGNET_V2_ST_ACCEPTED;
             O.start_tick[tbase + o_task] = now;
           }
         } else if (o_what == 3u) {
-          ++st.n_rejected;
+          ++c_rej;
           if (li == 0) O.status[tbase + o_task] = FOGNET_V2_ST_REJECTED;
         }
       }
     }
+  }
   }
 
   // ---- tasks not published before the stop (or the error), and the record
@@ -812,6 +836,19 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   }
   const int64_t msum = row_sum_i64<kRowLanes>(own ? (int64_t)mips : 0);
   if (live && li == 0) {
+    fognet_v2_stats st = {};
+    st.n_tasks = c_tasks;
+    st.n_local = c_local;
+    st.n_forwarded = c_fwd;
+    st.n_accepted = c_acc;
+    st.n_rejected = c_rej;
+    st.n_dropped = c_drop;
+    st.n_no_nodes = c_nonodes;
+    st.n_released_broker = c_relb;
+    st.n_inflated = c_infl;
+    st.n_released_node = c_reln;
+    st.n_relayed = c_relay;
+    st.events = (int64_t)c_events;
     st.node_mips_final_sum = msum;
     st.broker_mips_final = pool;
     st.status = (int32_t)err;
