@@ -282,7 +282,7 @@ def test_service_times_past_2_16_seconds(ctx, N):
     two = {k: (v[:2] if k in ("node", "status", "start", "done", "stats") else v) for k, v in g.items()}
     ref = {k: (v[:2] if k in ("node", "status", "start", "done", "stats") else v) for k, v in o.items()}
     assert_parity(tr, two, ref)
-    assert (g["done"][1] - g["start"][1]).max() == 1_000_000 * TPS
+    assert (g["done"][1] - g["start"][1]).max() >= 250_000 * TPS  # (the 1e6-MIPS task ran at 1000-4000 MIPS)
 
 
 def test_saturated_advertised_busy(ctx):
