@@ -77,6 +77,13 @@ struct WideLds {
   int32_t* p_i;     // [64] task index (-1: free slot)
   int32_t* p_k;     // [64] node
   int32_t* p_r;     // [64] MIPSRequired
+  // EXT_HIER: statistics inputs of pushed pending tasks, accumulated 64 at a time
+  int64_t* q_t;     // [64] publish tick
+  int64_t* q_a;     // [64] arrival tick
+  int64_t* q_st;    // [64] start (kNever: never)
+  int64_t* q_dn;    // [64] completion (kNever: never)
+  int32_t* q_i;     // [64] task index
+  uint32_t* q_sS;   // [64] service seconds << 3 | status (4, 5, 9 -> 4, 5, 1)
   int G;
 };
 
@@ -362,6 +369,12 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   L.p_i = reinterpret_cast<int32_t*>(L.p_a + kHierPending);
   L.p_k = L.p_i + kHierPending;
   L.p_r = L.p_k + kHierPending;
+  L.q_t = reinterpret_cast<int64_t*>(L.p_r + kHierPending);
+  L.q_a = L.q_t + kWave;
+  L.q_st = L.q_a + kWave;
+  L.q_dn = L.q_st + kWave;
+  L.q_i = reinterpret_cast<int32_t*>(L.q_dn + kWave);
+  L.q_sS = reinterpret_cast<uint32_t*>(L.q_i + kWave);
   const int SP = L.G * kWideGroupSlots;
   const WideView V{VN + ((size_t)wr * kWave + lane) * SP, VB + ((size_t)wr * kWave + lane) * SP,
                    VW + ((size_t)wr * kWave + lane) * SP};
@@ -473,6 +486,28 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   // recurrence and the advert scans hold as for direct tasks.  A pushed pending
   // task's statistics and outputs are recorded at once (uniform code).
   int n_pend = 0;  // occupied pending slots (wave-uniform)
+  int n_sq = 0;    // staged statistics of pushed pending tasks (wave-uniform)
+  // accumulate the staged statistics, one task per lane (the chunk end's code)
+  auto drain_stats = [&]() {
+    if (lane < n_sq) {
+      const int64_t t_q = L.q_t[lane], a_q = L.q_a[lane], st_q = L.q_st[lane], dn_q = L.q_dn[lane];
+      const int32_t i_q = L.q_i[lane];
+      const uint32_t sS = L.q_sS[lane];
+      const uint32_t status_q = sS & 7u, S_q = sS >> 3;  // (S only feeds busy_s: < 2^29 here, see push_one)
+      if (dn_q != kNever) {
+        acc_task(acc, ab, t_q, a_q, st_q, dn_q, S_q, status_q, i_q, hist ? L.hist : nullptr);
+        if (hist) atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(dn_q - t_q)], 1u);
+      } else {  // node-down
+        n_short += 1;
+        if (status_q == 5u) acc.n5 += 1u;
+        if (status_q == 4u) {
+          acc.n4 += 1u;
+          if (st_q != kNever) acc_qtime(acc, ab, st_q, a_q, i_q, hist ? L.hist : nullptr);
+        }
+      }
+    }
+    n_sq = 0;
+  };
   auto pend_count = [&](uint32_t kk) -> uint32_t {
     return n_pend ? (uint32_t)__popcll(ballot(L.p_i[lane] >= 0 && (uint32_t)L.p_k[lane] == kk)) : 0u;
   };
@@ -539,26 +574,24 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       h.npend += 1;
       ch = h;
     }
-    if (lane == 0) {
-      if (!A.no_task_out) {
-        const size_t o = tbase + (size_t)i;
-        A.out_node[o] = (int32_t)kk;
-        A.out_status[o] = (uint8_t)status;
-        A.out_start[o] = start == kNever ? -1 : start;
-        A.out_done[o] = done == kNever ? -1 : done;
-      }
-      if (done != kNever) {
-        acc_task(acc, ab, t_i, a, start, done, S, status, i, hist ? L.hist : nullptr);
-        if (hist) atomicAdd(&L.hist[FOGNET_HIST_BINS + hist_bin(done - t_i)], 1u);
-      } else {  // node-down, as at the chunk's end
-        n_short += 1;
-        if (status == 5u) acc.n5 += 1u;
-        if (status == 4u) {
-          acc.n4 += 1u;
-          if (start != kNever) acc_qtime(acc, ab, start, a, i, hist ? L.hist : nullptr);
-        }
-      }
+    if (lane == 0 && !A.no_task_out) {
+      const size_t o = tbase + (size_t)i;
+      A.out_node[o] = (int32_t)kk;
+      A.out_status[o] = (uint8_t)status;
+      A.out_start[o] = start == kNever ? -1 : start;
+      A.out_done[o] = done == kNever ? -1 : done;
     }
+    // its statistics: staged, accumulated 64 tasks at a time (drain_stats), like the chunk's
+    if (n_sq == kWave) drain_stats();
+    if (lane == n_sq) {
+      L.q_t[lane] = t_i;
+      L.q_a[lane] = a;
+      L.q_st[lane] = start;
+      L.q_dn[lane] = done;
+      L.q_i[lane] = i;
+      L.q_sS[lane] = (min(S, 0x1FFFFFFFu) << 3) | (status & 7u);
+    }
+    ++n_sq;
     return true;
   };
   // push the pending tasks of node kk arriving at or before lim (by_node), or of any
@@ -982,8 +1015,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     }
   }
 
-  if constexpr (kHier) {  // the escalated tasks still in flight at the end
+  if constexpr (kHier) {  // the escalated tasks still in flight at the end, then their statistics
     if (err == FOGNET_OK && n_pend && !flush_pending(false, 0u, INT64_MAX)) err = FOGNET_ERR_ARG;
+    if (n_sq) drain_stats();
   }
   if (cj >= 0) nd[cj] = ch;
 
@@ -1046,7 +1080,7 @@ size_t replay_wide_lds_bytes(int32_t N) {
   const size_t G = (size_t)wide_groups(N);
   return G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int64_t) + sizeof(int32_t)) +
          FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t) + G * sizeof(uint64_t) +
-         kHierPending * (2 * sizeof(int64_t) + 3 * sizeof(int32_t));
+         kHierPending * (2 * sizeof(int64_t) + 3 * sizeof(int32_t)) + kWave * (4 * sizeof(int64_t) + 2 * sizeof(int32_t));
 }
 
 size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen) { return wide_ws(R, T, N, gen).bytes; }
