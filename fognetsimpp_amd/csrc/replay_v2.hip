@@ -37,6 +37,22 @@ constexpr uint32_t kKindAdvertise = 1u, kKindRelease = 2u;
 constexpr int32_t kMsgAdvert = 1, kMsgAck6 = 2;
 constexpr uint8_t kListNone = 0, kListLocal = 1, kListForwarded = 2;
 
+// Adverts that change nothing.  A node's ADVERTISEMIPS firing (ComputeBrokerApp2.cc
+// :202-220) sends its MIPS to the broker, whose handler only sets the node's view
+// (BrokerBaseApp2.cc:128-136) and schedules nothing.  Adverts of one node travel
+// one fixed-latency link, so they arrive in send order, and an advert carrying the
+// same MIPS as the node's previous one finds that value in the view already: its
+// arrival changes no state and inserts no event, so leaving it out of the queue
+// changes neither the FES order nor any sequence number of the events that remain
+// (its own insertion sequence is still consumed at the send).  Such an advert is
+// only counted, as the event it is (`events`), if it arrives before the stop.  Per
+// node at most one is in flight (a firing leaves it out only once the previous one
+// has arrived; else it is queued like any other), so an error that ends the
+// replication early un-counts at most that one.  At C1 these are the nodes'
+// 10-ms adverts between two MIPS changes: about half of all FES events.
+constexpr bool kPhantomAdverts = true;
+constexpr int32_t kNoAdvert = INT32_MIN;  // no advert sent yet (the broker's view starts at MIPS 0)
+
 struct V2Msg {  // a message in flight: arrival tick, insertion sequence, payload
   int64_t tick;
   uint64_t seq;
@@ -120,6 +136,12 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
   }
   uint32_t in_h = 0u, in_n = 0u, out_h = 0u, out_n = 0u, rs_h = 0u, rs_n = 0u;
   V2Msg in_hd = {kNever, ~0ull, 0, 0}, out_hd = {kNever, ~0ull, 0, 0};
+  // adverts that change nothing at the broker (kPhantomAdverts): the MIPS of the
+  // node's last advert sent, its one unqueued advert in flight and the count of those
+  int32_t last_sent = kNoAdvert;
+  int64_t ph_tick = INT64_MIN;  // (none in flight)
+  uint64_t ph_seq = 0ull;
+  uint32_t ph_cnt = 0u;
 
   // ---- broker (wave-uniform)
   int32_t pool = A.broker_mips[r];
@@ -135,6 +157,8 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
   fognet_v2_stats st = {};
   uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
   bad = false;
+  int64_t end_tick = kNever;  // the last event dispatched (where an error ends the replication)
+  uint64_t end_seq = ~0ull;
 
   while (err == FOGNET_OK) {
     // ---- the earliest event: the lanes' own sources, then the broker's
@@ -185,6 +209,8 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
     if (kind == 0 || e_tick >= stop) break;  // nothing left, or the sim-time-limit
     const int64_t now = e_tick;
     ++st.events;
+    end_tick = e_tick;
+    end_seq = e_seq;
 
     if (kind == 2) {
       // ---- publish: BrokerBaseApp2.cc:176-195 + sendPubAck(:205-287)
@@ -336,12 +362,20 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
               }
             }
             // advertiseMIPS (:202-220): advert, then the self-message again 0.01 s later
-            const V2Msg m = {now + ul, my_seq++, kMsgAdvert, mips};
-            if (out_n == Q) bad = true;
-            else {
-              outq[(out_h + out_n) & qm] = m;
-              if (out_n == 0u) out_hd = m;
-              ++out_n;
+            if (kPhantomAdverts && mips == last_sent && earlier(ph_tick, ph_seq, now, e_seq)) {
+              // carries the value of the node's previous advert, which the broker already holds
+              ph_tick = now + ul;
+              ph_seq = my_seq++;
+              ph_cnt += ph_tick < stop ? 1u : 0u;
+            } else {
+              const V2Msg m = {now + ul, my_seq++, kMsgAdvert, mips};
+              last_sent = mips;
+              if (out_n == Q) bad = true;
+              else {
+                outq[(out_h + out_n) & qm] = m;
+                if (out_n == 0u) out_hd = m;
+                ++out_n;
+              }
             }
             t_sched = true;
             t_tick = now + kAdvertPeriod;
@@ -397,6 +431,12 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
     }
   }
 
+  // ---- unqueued adverts dispatched before the end (an error ends the replication at
+  // event end_*: the one still in flight after it is not)
+  if (err != FOGNET_OK && ph_tick < stop && !earlier(ph_tick, ph_seq, end_tick, end_seq)) ph_cnt -= 1u;
+  int64_t ph_sum = (int64_t)ph_cnt;
+  for (int m = kWave / 2; m > 0; m >>= 1) ph_sum += (int64_t)shfl_xor_u64((uint64_t)ph_sum, m);
+  st.events += ph_sum;
   // ---- tasks not published before the stop (or the error), and the record
   for (int t = next + lane; t < T; t += kWave) {
     O.node[tbase + t] = -1;
@@ -541,6 +581,10 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   }
   uint32_t in_h = 0u, in_n = 0u, out_h = 0u, out_n = 0u, rs_h = 0u, rs_n = 0u;
   V2MsgR in_hd = {kNever, ~0u, 0, 0, 0}, out_hd = {kNever, ~0u, 0, 0, 0};
+  // unqueued adverts (kPhantomAdverts)
+  int32_t last_sent = kNoAdvert;
+  int64_t ph_tick = INT64_MIN;  // (none in flight)
+  uint32_t ph_seq = 0u, ph_cnt = 0u;
 
   // ---- broker (row-uniform)
   int32_t pool = live ? A.broker_mips[rr] : 0;
@@ -559,6 +603,8 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   uint32_t err = row_any<kRowLanes>(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
   bool fin = !live || err != FOGNET_OK;  // row-uniform: this replication's loop has ended
   bad = false;
+  int64_t end_tick = kNever;  // the last event dispatched (where an error ends the replication)
+  uint32_t end_seq = ~0u;
 
   // (no `continue` inside: every path of a step falls through to its end, so the
   // loop-carried state needs no copies at extra loop exits)
@@ -609,7 +655,11 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       fin = true;
     }
     const int64_t now = e_tick;
-    if (!fin) ++c_events;
+    if (!fin) {
+      ++c_events;
+      end_tick = e_tick;
+      end_seq = e_seq;
+    }
 
     if (fin) {
     } else if (kind == 2 && (p_tick < prev_pub || p_tick > kMaxV2Tick)) {
@@ -763,12 +813,20 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
               }
             }
             // advertiseMIPS (:202-220): advert, then the self-message again 0.01 s later
-            const V2MsgR m = {now + ul, my_seq++, kMsgAdvert, mips, 0};
-            if (out_n == Q) bad = true;
-            else {
-              outq[(out_h + out_n) & qm] = m;
-              if (out_n == 0u) out_hd = m;
-              ++out_n;
+            if (kPhantomAdverts && mips == last_sent && earlier32(ph_tick, ph_seq, now, e_seq)) {
+              // carries the value of the node's previous advert, which the broker already holds
+              ph_tick = now + ul;
+              ph_seq = my_seq++;
+              ph_cnt += ph_tick < stop ? 1u : 0u;
+            } else {
+              const V2MsgR m = {now + ul, my_seq++, kMsgAdvert, mips, 0};
+              last_sent = mips;
+              if (out_n == Q) bad = true;
+              else {
+                outq[(out_h + out_n) & qm] = m;
+                if (out_n == 0u) out_hd = m;
+                ++out_n;
+              }
             }
             t_sched = true;
             t_tick = now + kAdvertPeriod;
@@ -834,6 +892,9 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       O.done_tick[tbase + t] = -1;
     }
   }
+  // unqueued adverts dispatched before the end (after an error: not the one still in flight)
+  if (err != FOGNET_OK && ph_tick < stop && !earlier32(ph_tick, ph_seq, end_tick, end_seq)) ph_cnt -= 1u;
+  c_events += (uint64_t)row_sum_i64<kRowLanes>(own ? (int64_t)ph_cnt : 0);
   const int64_t msum = row_sum_i64<kRowLanes>(own ? (int64_t)mips : 0);
   if (live && li == 0) {
     fognet_v2_stats st = {};
