@@ -51,6 +51,19 @@ constexpr uint8_t kListNone = 0, kListLocal = 1, kListForwarded = 2;
 // replication early un-counts at most that one.  At C1 these are the nodes'
 // 10-ms adverts between two MIPS changes: about half of all FES events.
 constexpr bool kPhantomAdverts = true;
+
+// Batched timer firings (replay_v2_rows_kernel).  A node's firing that releases
+// nothing (ComputeBrokerApp2.cc:222-245 finds no expired reservation, or the
+// self-message is ADVERTISEMIPS) touches only its node: it sends the advert
+// (queued, or left out as above) and re-arms the self-message 0.01 s later,
+// consuming two insertion sequence numbers.  The earliest firings of a row's
+// nodes that precede every other pending event, the first firing that releases
+// something and the arrival of any advert one of them queues are therefore the
+// next events of the FES in their own (tick, sequence) order, and the rest of the
+// simulation cannot observe that they are handled in one step: each takes the
+// two sequence numbers its rank among them gives.  At C1 most events are such
+// firings (five nodes, a 10-ms timer, a publish every 50 ms).
+constexpr bool kBatchFirings = true;
 constexpr int32_t kNoAdvert = INT32_MIN;  // no advert sent yet (the broker's view starts at MIPS 0)
 
 struct V2Msg {  // a message in flight: arrival tick, insertion sequence, payload
@@ -529,6 +542,11 @@ struct V2MsgR {
 static_assert(sizeof(V2MsgR) == sizeof(V2Msg), "same queue slot");
 constexpr uint32_t kSeqLimit = 0xFFFFFF00u;
 
+// s_waitcnt vmcnt(0) (expcnt, lgkmcnt unconstrained) as the builtin, so the
+// compiler's wait insertion knows every load issued so far has landed.
+__device__ __forceinline__ void sync_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+constexpr int kTraceChunk = 64;
+
 __device__ __forceinline__ bool earlier32(int64_t t, uint32_t s, int64_t t2, uint32_t s2) {
   return t < t2 || (t == t2 && s < s2);
 }
@@ -579,8 +597,17 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
     t_tick = fa;
     t_seq = (uint32_t)li;
   }
+  // The node's three FIFOs (broker -> node tasks, node -> broker messages,
+  // reservations) keep their first two entries in registers (hd, nx) and only the
+  // rest in HBM: a push stores only from the third entry on, and a pop loads (and
+  // waits for, sync_vm) only when a third entry moves up.  No load is then left in
+  // flight across loop iterations: the compiler would wait for it at its first use
+  // in a later step with vmcnt(0), which on gfx9 also waits for every store issued
+  // since (the per-task outputs), i.e. an HBM write round trip per step.
   uint32_t in_h = 0u, in_n = 0u, out_h = 0u, out_n = 0u, rs_h = 0u, rs_n = 0u;
   V2MsgR in_hd = {kNever, ~0u, 0, 0, 0}, out_hd = {kNever, ~0u, 0, 0, 0};
+  V2MsgR in_nx = in_hd, out_nx = out_hd;
+  V2Res rs_hd = {0, 0, 0.0}, rs_nx = rs_hd;
   // unqueued adverts (kPhantomAdverts)
   int32_t last_sent = kNoAdvert;
   int64_t ph_tick = INT64_MIN;  // (none in flight)
@@ -594,8 +621,33 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   uint32_t seq = (uint32_t)N + (uint32_t)T;  // the publishes hold N .. N+T-1
   int next = 0, list_h = 0;
   int64_t prev_pub = INT64_MIN;
-  int64_t p_tick = (live && T > 0) ? arrive[0] : kNever;  // the next publish, loaded one publish ahead
-  int32_t p_req = (live && T > 0) ? reqs[0] : 0;
+  // the row's trace, 64 publishes at a time in LDS (loaded and waited for once per
+  // chunk, for the reason above); the next publish in registers
+  __shared__ int64_t s_ptk[kRowsPerWave * kTraceChunk];
+  __shared__ int32_t s_prq[kRowsPerWave * kTraceChunk];
+  int64_t* const ptk = s_ptk + (lane / kRowLanes) * kTraceChunk;
+  int32_t* const prq = s_prq + (lane / kRowLanes) * kTraceChunk;
+  auto stage_chunk = [&](int base) {  // publishes base .. base + 63 (row-uniform call)
+    constexpr int kPer = kTraceChunk / kRowLanes;
+    int64_t tk[kPer];
+    int32_t rq[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {  // every load issued before any is used
+      const int t = base + li + u * kRowLanes;
+      const int tc = t < T ? t : T - 1;
+      tk[u] = arrive[tc];
+      rq[u] = reqs[tc];
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int q = li + u * kRowLanes;
+      ptk[q] = base + q < T ? tk[u] : kNever;
+      prq[q] = base + q < T ? rq[u] : 0;
+    }
+  };
+  if (live && T > 0) stage_chunk(0);
+  int64_t p_tick = (live && T > 0) ? ptk[0] : kNever;
+  int32_t p_req = (live && T > 0) ? prq[0] : 0;
   // per-replication counts (32-bit: each is at most T, except events)
   uint32_t c_tasks = 0, c_local = 0, c_fwd = 0, c_acc = 0, c_rej = 0, c_drop = 0, c_nonodes = 0, c_relb = 0,
            c_infl = 0, c_reln = 0, c_relay = 0;
@@ -608,8 +660,107 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
 
   // (no `continue` inside: every path of a step falls through to its end, so the
   // loop-carried state needs no copies at extra loop exits)
+#ifdef FOGNET_V2_PROF
+  uint32_t pr_iter = 0u, pr_batch = 0u, pr_gen = 0u, pr_fire = 0u;  // profile build only
+#endif
   while (ballot(!fin)) {
+#ifdef FOGNET_V2_PROF
+    ++pr_iter;
+#endif
     if (!fin) {  // (finished rows wait for the others; their lanes stay off)
+    // ---- a batch of simple timer firings (kBatchFirings): the earliest firings of the
+    // row's nodes that come before every other pending event (H), before the first
+    // firing that releases a reservation (K) and before the arrival of any advert a
+    // firing of the batch queues (M), handled at once, each on its node's lane
+    bool batched = false;
+    if (kBatchFirings) {
+      int64_t ht = kNever;
+      uint32_t hs = ~0u;
+      if (in_n) {
+        ht = in_hd.tick;
+        hs = in_hd.seq;
+      }
+      if (out_n && earlier32(out_hd.tick, out_hd.seq, ht, hs)) {
+        ht = out_hd.tick;
+        hs = out_hd.seq;
+      }
+      int64_t H_t = (int64_t)row_min_u64<kRowLanes>((uint64_t)ht);
+      uint32_t H_s = row_min_u32<kRowLanes>(ht == H_t ? hs : ~0u);
+      if (next < T && earlier32(p_tick, (uint32_t)N + (uint32_t)next, H_t, H_s)) {
+        H_t = p_tick;
+        H_s = (uint32_t)N + (uint32_t)next;
+      }
+      if (b_sched && earlier32(b_tick, b_seq, H_t, H_s)) {
+        H_t = b_tick;
+        H_s = b_seq;
+      }
+      const bool cand = t_sched && t_tick < stop && earlier32(t_tick, t_seq, H_t, H_s);
+      const bool rel = cand && t_kind == kKindRelease && rs_n && rs_hd.deadline < dbl(t_tick);
+      const bool phantom = kPhantomAdverts && mips == last_sent && earlier32(ph_tick, ph_seq, t_tick, t_seq);
+      const int64_t K_t = (int64_t)row_min_u64<kRowLanes>((uint64_t)(rel ? t_tick : kNever));
+      const int64_t M_t = (int64_t)row_min_u64<kRowLanes>((uint64_t)(cand && !rel && !phantom ? t_tick + ul : kNever));
+      // (a firing precedes a same-tick queued advert, whose sequence number is new)
+      const bool inb = cand && !rel && t_tick < K_t && t_tick <= M_t;
+      const uint32_t rowb = (uint32_t)(ballot(inb) >> (lane & ~(kRowLanes - 1))) &
+                            (uint32_t)((1ull << kRowLanes) - 1ull);
+      if (rowb && seq >= kSeqLimit) {
+        err = FOGNET_ERR_CAPACITY;  // (32-bit insertion sequence)
+        fin = true;
+        batched = true;
+      } else if (rowb) {
+        batched = true;
+        // the firings' order (tick, then insertion sequence): each consumes two
+        // sequence numbers, its advert's and its next firing's
+        uint32_t rank = 0u;
+        for (uint32_t m = rowb; m; m &= m - 1u) {
+          const int w = (int)__builtin_ctz(m);
+          const int64_t tw = (int64_t)row_bcast_u64<kRowLanes>((uint64_t)t_tick, w);
+          const uint32_t sw = row_bcast_u32<kRowLanes>(t_seq, w);
+          rank += earlier32(tw, sw, t_tick, t_seq) ? 1u : 0u;
+        }
+        const uint32_t tot = (uint32_t)__builtin_popcount(rowb);
+        bool has_last = false;
+        if (inb) {
+          const uint32_t sq = seq + 2u * rank;
+          if (phantom) {  // carries the value of the node's previous advert (kPhantomAdverts)
+            ph_tick = t_tick + ul;
+            ph_seq = sq;
+            ph_cnt += ph_tick < stop ? 1u : 0u;
+          } else {
+            const V2MsgR m = {t_tick + ul, sq, kMsgAdvert, mips, 0};
+            last_sent = mips;
+            if (out_n == Q) bad = true;
+            else {
+              if (out_n == 0u) out_hd = m;
+              else if (out_n == 1u) out_nx = m;
+              else outq[(out_h + out_n) & qm] = m;
+              ++out_n;
+            }
+          }
+          has_last = rank + 1u == tot;  // the batch's last firing (where an error would end the replication)
+          end_tick = t_tick;
+          end_seq = t_seq;
+          t_tick += kAdvertPeriod;
+          t_seq = sq + 1u;
+        }
+        end_tick = (int64_t)row_min_u64<kRowLanes>((uint64_t)(has_last ? end_tick : kNever));
+        end_seq = row_min_u32<kRowLanes>(has_last ? end_seq : ~0u);
+        seq += 2u * tot;
+        c_events += tot;
+#ifdef FOGNET_V2_PROF
+        ++pr_batch;
+        pr_fire += tot;
+#endif
+        if (row_any<kRowLanes>(bad)) {
+          err = FOGNET_ERR_CAPACITY;
+          fin = true;
+        }
+      }
+    }
+    if (!batched) {
+#ifdef FOGNET_V2_PROF
+    ++pr_gen;
+#endif
     // ---- the earliest event: the lanes' own sources, then the broker's
     int64_t ct = kNever;
     uint32_t cs = ~0u;
@@ -671,8 +822,9 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       prev_pub = p_tick;
       const int32_t req = p_req;
       if (next < T) {  // the following publish, in flight while this one is handled
-        p_tick = arrive[next];
-        p_req = reqs[next];
+        if ((next & (kTraceChunk - 1)) == 0) stage_chunk(next);
+        p_tick = ptk[next & (kTraceChunk - 1)];
+        p_req = prq[next & (kTraceChunk - 1)];
       }
       ++c_tasks;
       int32_t k = -1;
@@ -713,8 +865,9 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
             if (in_n == Q) {
               bad = true;
             } else {
-              inq[(in_h + in_n) & qm] = m;
               if (in_n == 0u) in_hd = m;
+              else if (in_n == 1u) in_nx = m;
+              else inq[(in_h + in_n) & qm] = m;
               ++in_n;
             }
           }
@@ -772,7 +925,11 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
         if (li == w) {
           ++out_h;
           --out_n;
-          if (out_n) out_hd = outq[out_h & qm];
+          out_hd = out_nx;
+          if (out_n >= 2u) {
+            out_nx = outq[(out_h + 1u) & qm];
+            sync_vm();
+          }
           if (mk == kMsgAdvert) view = mv;  // setMips (:132)
         }
         if (mk == kMsgAck6) {  // relay and erase the request if it is still listed (:145-153)
@@ -796,18 +953,24 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
             if (t_kind == kKindRelease && rs_n) {
               // ComputeBrokerApp2::releaseResource (:222-245): the first reservation
               // with deadline < now (the oldest: deadlines follow arrival order)
-              const V2Res h = res[rs_h & qm];
+              const V2Res h = rs_hd;
               if (h.deadline < dbl(now)) {
                 mips += h.req;  // :226
                 ++rs_h;
                 --rs_n;
+                rs_hd = rs_nx;
+                if (rs_n >= 2u) {
+                  rs_nx = res[(rs_h + 1u) & qm];
+                  sync_vm();
+                }
                 o_task = h.task;
                 o_what = 1u;
                 const V2MsgR m = {now + ul, my_seq++, kMsgAck6, h.task, 0};  // puback 6 (:231-235)
                 if (out_n == Q) bad = true;
                 else {
-                  outq[(out_h + out_n) & qm] = m;
                   if (out_n == 0u) out_hd = m;
+                  else if (out_n == 1u) out_nx = m;
+                  else outq[(out_h + out_n) & qm] = m;
                   ++out_n;
                 }
               }
@@ -823,8 +986,9 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
               last_sent = mips;
               if (out_n == Q) bad = true;
               else {
-                outq[(out_h + out_n) & qm] = m;
                 if (out_n == 0u) out_hd = m;
+                else if (out_n == 1u) out_nx = m;
+                else outq[(out_h + out_n) & qm] = m;
                 ++out_n;
               }
             }
@@ -837,14 +1001,21 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
             const int32_t req = in_hd.kind;
             ++in_h;
             --in_n;
-            if (in_n) in_hd = inq[in_h & qm];
+            in_hd = in_nx;
+            if (in_n >= 2u) {
+              in_nx = inq[(in_h + 1u) & qm];
+              sync_vm();
+            }
             o_task = t;
             if (req < mips) {  // :269
               mips -= req;     // :272
               o_what = 2u;
               if (rs_n == Q) bad = true;
               else {
-                res[(rs_h + rs_n) & qm] = V2Res{t, req, add_rn(dbl(now), rt)};  // :274
+                const V2Res v = {t, req, add_rn(dbl(now), rt)};  // :274
+                if (rs_n == 0u) rs_hd = v;
+                else if (rs_n == 1u) rs_nx = v;
+                else res[(rs_h + rs_n) & qm] = v;
                 ++rs_n;
               }
               // cancelEvent + RELEASERESOURCE at now + requiredTime (:292-295)
@@ -880,6 +1051,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
         }
       }
     }
+    }  // !batched
   }
   }
 
@@ -909,6 +1081,12 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
     st.n_inflated = c_infl;
     st.n_released_node = c_reln;
     st.n_relayed = c_relay;
+#ifdef FOGNET_V2_PROF
+    st.n_no_nodes = pr_iter;
+    st.n_dropped = pr_batch;
+    st.n_inflated = pr_gen;
+    st.n_rejected = pr_fire;
+#endif
     st.events = (int64_t)c_events;
     st.node_mips_final_sum = msum;
     st.broker_mips_final = pool;
