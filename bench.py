@@ -516,9 +516,12 @@ def bench_c1(args, ctx, dev, dist, world, rank):
                        "R_total": args.R_total, "T_max": T, "N": n_nodes, "model": "BrokerBaseApp2 + ComputeBrokerApp2",
                        "parallelism": f"replications sharded over {world} GPU(s)"},
             "roofline": {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None,
-                         "traffic": None, "kernel": "replay_v2_kernel", "kernel_ms_per_step": kern_ms,
+                         "traffic": None, "kernel": "replay_v2_rows_kernel (N <= 16: four replications per wavefront)",
+                         "kernel_ms_per_step": kern_ms,
                          "events_per_s": events * args.steps / elapsed,
-                         "note": "event-driven (~53 FES events per publish); no HBM roofline applies"},
+                         "note": "event-driven (~53 reference FES events per publish, counted in events_per_s; "
+                                 "no-op adverts are left out of the queues and simple timer firings "
+                                 "batched, DESIGN.md section 9); no HBM roofline applies"},
             "cpu_baseline": cpu, "failed_replications": failed,
             "stats": {"decisions": decisions, "events": events, "local": int(st["n_local"].sum()),
                       "forwarded": int(st["n_forwarded"].sum())},
