@@ -614,6 +614,20 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     return true;
   };
 
+#ifdef FOGNET_WIDE_PROF
+  // profile build only (tools/wide_prof.py): loop counters, written over the statistics
+  uint64_t pf_iter = 0, pf_advit = 0, pf_adv = 0, pf_same = 0, pf_hit = 0, pf_gkey = 0, pf_scan = 0, pf_runs = 0;
+  uint64_t pf_t[7] = {0, 0, 0, 0, 0, 0, 0};  // s_memtime ticks per segment (WTM)
+  uint64_t pf_last = __builtin_amdgcn_s_memtime();
+#define WTM(i)                                          \
+  {                                                     \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+    pf_t[i] += now_ - pf_last;                          \
+    pf_last = now_;                                     \
+  }
+#else
+#define WTM(i)
+#endif
   // the decision is recomputed only after an advert changed the view
   // (adverts are the only view updates, BrokerBaseApp3.cc:123-130)
   bool view_changed = true;
@@ -652,6 +666,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     prev_t = readlane_i64(ca, cnt - 1);
 
     int jp = 0;
+    WTM(6)
     while (jp < cnt) {
       const int64_t t = readlane_i64(ca, jp);
       if constexpr (kHier) {  // escalated tasks that reached their node before t (before any advert of t)
@@ -664,7 +679,14 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       // 1) completion adverts that reached the broker strictly before t
       bool lerr = false, lbroken = false;
       if (ballot(mn < t)) view_changed = true;
+#ifdef FOGNET_WIDE_PROF
+      ++pf_iter;
+#endif
       while (ballot(mn < t)) {
+#ifdef FOGNET_WIDE_PROF
+        ++pf_advit;
+        pf_adv += (uint64_t)__popcll(ballot(mn < t));
+#endif
         if constexpr (kHier) {
           // the regions whose view changes in this round (one advert per due lane): only
           // their cached regional minima are dropped
@@ -700,6 +722,10 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           // the earliest advert: j's was the lane's (so its group's), rescan both levels
           group_scan_nxt(L, lane, g, sl, nxt_j, gx);
           lane_min_nxt(L, lane, mn, mj);
+#ifdef FOGNET_WIDE_PROF
+          pf_same += (mn < t && mj == j) ? 1u : 0u;
+          pf_hit += hit ? 1u : 0u;
+#endif
           if constexpr (!kPerPublish) {
             const int64_t w_j = node_w(h, nxt_j, dl_j);
             V.w[sl] = w_j;
@@ -712,6 +738,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           const uint64_t nk = ((uint64_t)busy_j << 32) | (uint32_t)j;
           const uint64_t gk_new = ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? group_key(V, lane, g)
                                                                                  : (nk < gk_old ? nk : gk_old);
+#ifdef FOGNET_WIDE_PROF
+          pf_gkey += ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? 1u : 0u;
+#endif
           L.g_key[g * kWave + lane] = gk_new;
           if (gk_new < mk) mk = gk_new;
           else if (mk == gk_old && gk_new > gk_old) mk = lane_min_key(L, lane);
@@ -726,6 +755,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         break;
       }
 
+      WTM(1)
       // 2) the decision over the advertised view
       bool escalated = false;
       if constexpr (kExt) {
@@ -785,6 +815,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       }
       const int kl = (int)(k % kWave);
 
+      WTM(2)
       // 3) node k's record and parameters, in its owner lane (cached there)
       cache_node(k);
       uint32_t pend_k = 0u;  // EXT_HIER: k's escalated tasks still pending (decided, not pushed)
@@ -833,6 +864,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       const uint32_t tl_S = readlane_u32(ch.tl_S, kl) & 0x7FFFFFFFu;  // (bit 31: the tail was escalated)
       const int64_t base_done = tl >= 0 ? tl_done : INT64_MIN;  // kNever: the node crashed with work left
 
+      WTM(3)
       // 4) the run: publishes jp .. jq-1 up to the earliest pending advert E
       //    (an advert of any node may change the view) all go to node k; when
       //    k has nothing pending, the run's first task becomes its head and
@@ -867,6 +899,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       }
       const bool in_run = lane >= jp && lane < jq;
       const int Lr = jq - jp;
+#ifdef FOGNET_WIDE_PROF
+      ++pf_runs;
+#endif
 
       // 5) task arrivals at node k (ComputeBrokerApp3.cc:269-320), one lane per
       //    task: FIFO single server, done_m = max(a_m, done_{m-1}) + S_m
@@ -936,6 +971,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         q_status = status;
       }
 
+      WTM(4)
       // 6) node k's record after the run (owner lane)
       const int lz = jq - 1;
       const int64_t a_z = readlane_i64(a, lz), done_z = readlane_i64(done, lz);
@@ -988,8 +1024,10 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         }
       }
       n_done += Lr;
+      WTM(5)
       jp = jq;
     }
+    WTM(0)
     // the chunk's outputs and statistics (also after an error ended it: the tasks pushed so far)
     if (q_on && !A.no_task_out) {  // (statistics-only replays keep no per-task outputs)
       const size_t o = tbase + (size_t)(c0 + lane);
@@ -1022,6 +1060,13 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   if (cj >= 0) nd[cj] = ch;
 
   // ---- per-replication record (the fields replay_kernel + its epilogue write)
+#ifdef FOGNET_WIDE_PROF
+  for (int m = kWave / 2; m > 0; m >>= 1) {
+    pf_same += shfl_xor_u64(pf_same, m);
+    pf_hit += shfl_xor_u64(pf_hit, m);
+    pf_gkey += shfl_xor_u64(pf_gkey, m);
+  }
+#endif
   acc = wave_merge(acc);
   ab = wave_min_abort(ab);
   const uint32_t mp = ~wave_min_u32(~max_pend);
@@ -1036,6 +1081,22 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     // arrival for a task a crash keeps from completing)
     S->events = 2 * (int64_t)N + 4 * (int64_t)n_done - 2 * (int64_t)shorts;
     write_rep_stats(S, acc, ab, A.ref_abort);
+#ifdef FOGNET_WIDE_PROF
+    S->queue_sum_lo = pf_iter;
+    S->queue_sum_hi = pf_advit;
+    S->queue_sq_lo = pf_adv;
+    S->resp_sum_lo = pf_runs;
+    S->resp_sum_hi = pf_same;
+    S->resp_sq_lo = pf_hit;
+    S->resp_sq_hi = pf_gkey;
+    S->queue_min_raw = (int64_t)pf_t[0];  // chunk end: outputs + statistics
+    S->queue_max_raw = (int64_t)pf_t[1];  // adverts (incl. flush of pending escalations)
+    S->resp_min_ticks = (int64_t)pf_t[2]; // decision
+    S->resp_max_ticks = (int64_t)pf_t[3]; // record + parameters (+ EXT_HIER escalation handling)
+    S->last_tick = (int64_t)pf_t[4];      // run horizon + FIFO + entries
+    S->queue_sq_top = pf_t[5];            // record update
+    S->busy_s = (int64_t)pf_t[6];         // chunk start: trace load + preconditions
+#endif
   }
   // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12)
   // with B_j = node j's service seconds (its tail's cumulative sum), summed in node order
