@@ -662,6 +662,15 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   // loop-carried state needs no copies at extra loop exits)
 #ifdef FOGNET_V2_PROF
   uint32_t pr_iter = 0u, pr_batch = 0u, pr_gen = 0u, pr_fire = 0u;  // profile build only
+  uint64_t pr_t[4] = {0, 0, 0, 0}, pr_last = __builtin_amdgcn_s_memtime();
+#define VTM(i)                                          \
+  {                                                     \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+    pr_t[i] += now_ - pr_last;                          \
+    pr_last = now_;                                     \
+  }
+#else
+#define VTM(i)
 #endif
   while (ballot(!fin)) {
 #ifdef FOGNET_V2_PROF
@@ -694,6 +703,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
         H_t = b_tick;
         H_s = b_seq;
       }
+      VTM(0)
       const bool cand = t_sched && t_tick < stop && earlier32(t_tick, t_seq, H_t, H_s);
       const bool rel = cand && t_kind == kKindRelease && rs_n && rs_hd.deadline < dbl(t_tick);
       const bool phantom = kPhantomAdverts && mips == last_sent && earlier32(ph_tick, ph_seq, t_tick, t_seq);
@@ -701,6 +711,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       const int64_t M_t = (int64_t)row_min_u64<kRowLanes>((uint64_t)(cand && !rel && !phantom ? t_tick + ul : kNever));
       // (a firing precedes a same-tick queued advert, whose sequence number is new)
       const bool inb = cand && !rel && t_tick < K_t && t_tick <= M_t;
+      VTM(1)
       const uint32_t rowb = (uint32_t)(ballot(inb) >> (lane & ~(kRowLanes - 1))) &
                             (uint32_t)((1ull << kRowLanes) - 1ull);
       if (rowb && seq >= kSeqLimit) {
@@ -757,6 +768,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
         }
       }
     }
+    VTM(2)
     if (!batched) {
 #ifdef FOGNET_V2_PROF
     ++pr_gen;
@@ -1053,6 +1065,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
     }
     }  // !batched
   }
+  VTM(3)
   }
 
   // ---- tasks not published before the stop (or the error), and the record
@@ -1086,6 +1099,10 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
     st.n_dropped = pr_batch;
     st.n_inflated = pr_gen;
     st.n_rejected = pr_fire;
+    st.n_local = pr_t[0];      // H (non-timer minimum)
+    st.n_forwarded = pr_t[1];  // K, M
+    st.n_accepted = pr_t[2];   // batch execution (rank, adverts)
+    st.n_released_broker = pr_t[3];  // generic step
 #endif
     st.events = (int64_t)c_events;
     st.node_mips_final_sum = msum;

@@ -28,3 +28,6 @@ print("per replication: wave iterations %.0f, batch steps %.0f, generic steps %.
 print("per publish: wave iterations %.2f, batch %.2f, generic %.2f, firings per batch %.2f, events %.2f" % (
     (st["n_no_nodes"] / pubs).mean(), (st["n_dropped"] / pubs).mean(), (st["n_inflated"] / pubs).mean(),
     (st["n_rejected"] / np.maximum(st["n_dropped"], 1)).mean(), (st["events"] / pubs).mean()))
+seg = [("H minimum", "n_local"), ("K, M", "n_forwarded"), ("batch", "n_accepted"), ("generic step", "n_released_broker")]
+tot = sum(st[k].astype(np.float64).sum() for _, k in seg)
+print("time split:", ", ".join("%s %.1f%%" % (n, 100 * st[k].astype(np.float64).sum() / tot) for n, k in seg))
