@@ -683,16 +683,10 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
     // firing of the batch queues (M), handled at once, each on its node's lane
     bool batched = false;
     if (kBatchFirings) {
-      int64_t ht = kNever;
-      uint32_t hs = ~0u;
-      if (in_n) {
-        ht = in_hd.tick;
-        hs = in_hd.seq;
-      }
-      if (out_n && earlier32(out_hd.tick, out_hd.seq, ht, hs)) {
-        ht = out_hd.tick;
-        hs = out_hd.seq;
-      }
+      // H: the earliest event that draws sequence numbers or touches a node's state
+      // (task arrivals, publishes) or the request list (the broker's RELEASERESOURCE)
+      const int64_t ht = in_n ? in_hd.tick : kNever;
+      const uint32_t hs = in_n ? in_hd.seq : ~0u;
       int64_t H_t = (int64_t)row_min_u64<kRowLanes>((uint64_t)ht);
       uint32_t H_s = row_min_u32<kRowLanes>(ht == H_t ? hs : ~0u);
       if (next < T && earlier32(p_tick, (uint32_t)N + (uint32_t)next, H_t, H_s)) {
@@ -708,17 +702,20 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       const bool rel = cand && t_kind == kKindRelease && rs_n && rs_hd.deadline < dbl(t_tick);
       const bool phantom = kPhantomAdverts && mips == last_sent && earlier32(ph_tick, ph_seq, t_tick, t_seq);
       const int64_t K_t = (int64_t)row_min_u64<kRowLanes>((uint64_t)(rel ? t_tick : kNever));
-      const int64_t M_t = (int64_t)row_min_u64<kRowLanes>((uint64_t)(cand && !rel && !phantom ? t_tick + ul : kNever));
-      // (a firing precedes a same-tick queued advert, whose sequence number is new)
-      const bool inb = cand && !rel && t_tick < K_t && t_tick <= M_t;
+      const bool inb = cand && !rel && t_tick < K_t;
+      // messages reaching the broker before H: adverts set the view, status-6 acks
+      // relay and erase their request (BrokerBaseApp2.cc:128-154); they draw no
+      // number and touch neither a node nor what a firing reads
+      const bool arr = out_n && out_hd.tick < stop && earlier32(out_hd.tick, out_hd.seq, H_t, H_s);
       VTM(1)
-      const uint32_t rowb = (uint32_t)(ballot(inb) >> (lane & ~(kRowLanes - 1))) &
-                            (uint32_t)((1ull << kRowLanes) - 1ull);
+      const uint32_t rowm = (uint32_t)((1ull << kRowLanes) - 1ull);
+      const uint32_t rowb = (uint32_t)(ballot(inb) >> (lane & ~(kRowLanes - 1))) & rowm;
+      const bool rowa = ((ballot(arr) >> (lane & ~(kRowLanes - 1))) & rowm) != 0ull;
       if (rowb && seq >= kSeqLimit) {
         err = FOGNET_ERR_CAPACITY;  // (32-bit insertion sequence)
         fin = true;
         batched = true;
-      } else if (rowb) {
+      } else if (rowb || rowa) {
         batched = true;
         // the firings' order (tick, then insertion sequence): each consumes two
         // sequence numbers, its advert's and its next firing's
@@ -754,10 +751,33 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
           t_tick += kAdvertPeriod;
           t_seq = sq + 1u;
         }
-        end_tick = (int64_t)row_min_u64<kRowLanes>((uint64_t)(has_last ? end_tick : kNever));
-        end_seq = row_min_u32<kRowLanes>(has_last ? end_seq : ~0u);
+        if (rowb) {
+          end_tick = (int64_t)row_min_u64<kRowLanes>((uint64_t)(has_last ? end_tick : kNever));
+          end_seq = row_min_u32<kRowLanes>(has_last ? end_seq : ~0u);
+        }
+        // the messages (a queued advert of this batch's firings included: its arrival
+        // commutes with them too)
+        uint32_t n_arr = 0u, n_rl = 0u;
+        while (out_n && out_hd.tick < stop && earlier32(out_hd.tick, out_hd.seq, H_t, H_s)) {
+          if (out_hd.kind == kMsgAdvert) {
+            view = out_hd.val;  // setMips (:132)
+          } else if (list[out_hd.val] == kListForwarded) {  // ack 6: relay, erase if still listed (:145-153)
+            list[out_hd.val] = kListNone;
+            ++n_rl;
+          }
+          ++out_h;
+          --out_n;
+          out_hd = out_nx;
+          if (out_n >= 2u) {
+            out_nx = outq[(out_h + 1u) & qm];
+            sync_vm();
+          }
+          ++n_arr;
+        }
+        const uint32_t na = (uint32_t)row_sum_i64<kRowLanes>((int64_t)n_arr);
         seq += 2u * tot;
-        c_events += tot;
+        c_events += tot + na;
+        c_relay += (uint32_t)row_sum_i64<kRowLanes>((int64_t)n_rl);
 #ifdef FOGNET_V2_PROF
         ++pr_batch;
         pr_fire += tot;
