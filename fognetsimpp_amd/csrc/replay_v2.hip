@@ -699,10 +699,10 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       }
       VTM(0)
       const bool cand = t_sched && t_tick < stop && earlier32(t_tick, t_seq, H_t, H_s);
+      // (a firing that releases a reservation, ComputeBrokerApp2.cc:222-245, also
+      // touches only its node: one more sequence number, its status-6 ack's)
       const bool rel = cand && t_kind == kKindRelease && rs_n && rs_hd.deadline < dbl(t_tick);
-      const bool phantom = kPhantomAdverts && mips == last_sent && earlier32(ph_tick, ph_seq, t_tick, t_seq);
-      const int64_t K_t = (int64_t)row_min_u64<kRowLanes>((uint64_t)(rel ? t_tick : kNever));
-      const bool inb = cand && !rel && t_tick < K_t;
+      const bool inb = cand;
       // messages reaching the broker before H: adverts set the view, status-6 acks
       // relay and erase their request (BrokerBaseApp2.cc:128-154); they draw no
       // number and touch neither a node nor what a firing reads
@@ -717,20 +717,48 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
         batched = true;
       } else if (rowb || rowa) {
         batched = true;
-        // the firings' order (tick, then insertion sequence): each consumes two
-        // sequence numbers, its advert's and its next firing's
-        uint32_t rank = 0u;
+        // the firings' order (tick, then insertion sequence): each draws two
+        // sequence numbers (its advert's, its next firing's), three when it releases
+        // (its ack's first); `off` counts those the firings before it draw
+        uint32_t off = 0u, tot = 0u;
+        const uint32_t hi_rel = (uint32_t)((uint64_t)t_tick >> 32) | (rel ? 0x80000000u : 0u);  // (ticks < 2^53)
         for (uint32_t m = rowb; m; m &= m - 1u) {
           const int w = (int)__builtin_ctz(m);
-          const int64_t tw = (int64_t)row_bcast_u64<kRowLanes>((uint64_t)t_tick, w);
+          const uint32_t hw = row_bcast_u32<kRowLanes>(hi_rel, w);
+          const int64_t tw = (int64_t)(((uint64_t)(hw & 0x7FFFFFFFu) << 32) |
+                                       row_bcast_u32<kRowLanes>((uint32_t)(uint64_t)t_tick, w));
           const uint32_t sw = row_bcast_u32<kRowLanes>(t_seq, w);
-          rank += earlier32(tw, sw, t_tick, t_seq) ? 1u : 0u;
+          const uint32_t dw = (hw >> 31) ? 3u : 2u;
+          off += earlier32(tw, sw, t_tick, t_seq) ? dw : 0u;
+          tot += dw;
         }
-        const uint32_t tot = (uint32_t)__builtin_popcount(rowb);
         bool has_last = false;
+        uint32_t n_rel = 0u;
         if (inb) {
-          const uint32_t sq = seq + 2u * rank;
-          if (phantom) {  // carries the value of the node's previous advert (kPhantomAdverts)
+          uint32_t sq = seq + off;
+          if (rel) {  // releaseResource: the oldest reservation, acked with status 6 (:225-235)
+            const V2Res h = rs_hd;
+            mips += h.req;  // :226
+            ++rs_h;
+            --rs_n;
+            rs_hd = rs_nx;
+            if (rs_n >= 2u) {
+              rs_nx = res[(rs_h + 1u) & qm];
+              sync_vm();
+            }
+            const V2MsgR m = {t_tick + ul, sq++, kMsgAck6, h.task, 0};
+            if (out_n == Q) bad = true;
+            else {
+              if (out_n == 0u) out_hd = m;
+              else if (out_n == 1u) out_nx = m;
+              else outq[(out_h + out_n) & qm] = m;
+              ++out_n;
+            }
+            O.done_tick[tbase + h.task] = t_tick;
+            n_rel = 1u;
+          }
+          if (kPhantomAdverts && mips == last_sent && earlier32(ph_tick, ph_seq, t_tick, t_seq)) {
+            // carries the value of the node's previous advert (kPhantomAdverts)
             ph_tick = t_tick + ul;
             ph_seq = sq;
             ph_cnt += ph_tick < stop ? 1u : 0u;
@@ -745,12 +773,13 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
               ++out_n;
             }
           }
-          has_last = rank + 1u == tot;  // the batch's last firing (where an error would end the replication)
+          has_last = off + (rel ? 3u : 2u) == tot;  // the batch's last firing (where an error would end the replication)
           end_tick = t_tick;
           end_seq = t_seq;
           t_tick += kAdvertPeriod;
           t_seq = sq + 1u;
         }
+        const uint32_t nfire = (uint32_t)__builtin_popcount(rowb);
         if (rowb) {
           end_tick = (int64_t)row_min_u64<kRowLanes>((uint64_t)(has_last ? end_tick : kNever));
           end_seq = row_min_u32<kRowLanes>(has_last ? end_seq : ~0u);
@@ -775,12 +804,13 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
           ++n_arr;
         }
         const uint32_t na = (uint32_t)row_sum_i64<kRowLanes>((int64_t)n_arr);
-        seq += 2u * tot;
-        c_events += tot + na;
+        seq += tot;
+        c_events += nfire + na;
+        c_reln += (uint32_t)row_sum_i64<kRowLanes>((int64_t)n_rel);
         c_relay += (uint32_t)row_sum_i64<kRowLanes>((int64_t)n_rl);
 #ifdef FOGNET_V2_PROF
         ++pr_batch;
-        pr_fire += tot;
+        pr_fire += nfire;
 #endif
         if (row_any<kRowLanes>(bad)) {
           err = FOGNET_ERR_CAPACITY;
