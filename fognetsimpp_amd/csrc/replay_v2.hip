@@ -819,7 +819,10 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       }
     }
     VTM(2)
-    if (!batched) {
+    // then the earliest remaining event, in the same step (rows that batched take
+    // their next event too: the union of the rows' paths is paid either way)
+    (void)batched;
+    {
 #ifdef FOGNET_V2_PROF
     ++pr_gen;
 #endif
