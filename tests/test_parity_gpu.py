@@ -1124,6 +1124,33 @@ def test_v2_random_matches_oracle(ctx, seed, N, R):
     assert_v2_parity(g, o)
 
 
+@pytest.mark.parametrize("seed,N,R", [(21, 16, 8), (22, 5, 9), (23, 3, 4)])
+def test_v2_deep_fifos_and_long_uplinks(ctx, seed, N, R):
+    """Links longer than the 10-ms advert period (ul up to 45 ms, dl up to 60 ms):
+    several adverts of one node in flight, so most cannot be left out of the queue
+    and the FIFOs hold three or more entries (the entries past the two kept in
+    registers live in HBM); N = 16 is the rows kernel's widest row.  Equal to the
+    oracle DES, event counts included."""
+    rng = np.random.default_rng(seed)
+    MS = 10**9
+    T = 1500
+    gaps = rng.choice([0, 1, 3, 10, 20], size=(R, T)) * MS
+    arrive = (rng.integers(0, 30, size=(R, 1)) * MS + np.cumsum(gaps, axis=1)).astype(np.int64)
+    req = rng.integers(0, 900, size=(R, T)).astype(np.int32)
+    tr = dict(arrive=arrive, req=req, mips=rng.choice([600, 1000, 1400], size=(R, N)).astype(np.int32),
+              dl=rng.choice([1, 15, 35, 60], size=(R, N)).astype(np.int64) * MS,
+              ul=rng.choice([1, 10, 25, 45], size=(R, N)).astype(np.int64) * MS,
+              first_adv=rng.integers(0, 25, size=(R, N)).astype(np.int64) * MS)
+    broker = rng.choice([0, 500, 2000], size=R).astype(np.int32)
+    rt = rng.choice([0.01, 0.03, 0.05], size=R)
+    stop = arrive[:, -1] + rng.integers(0, 300, size=R) * MS
+    g = run_v2_gpu(ctx, tr, broker, stop, rt, qcap=4096)
+    o = ol.run_v2(tr["arrive"], tr["req"], broker, tr["mips"], tr["dl"], tr["ul"], tr["first_adv"], stop, rt,
+                  threads=8)
+    assert (o["stats"]["status"] == 0).all()
+    assert_v2_parity(g, o)
+
+
 def test_v2_node_reproduces_general0_recording_gpu(ctx):
     """The device v2 replay on the General-0 recording fixture (see test_oracle)."""
     tr, d = golden_io.general0_v2_node()

@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 from fognetsimpp_amd import _abi  # noqa: E402
 
 MODE = "time" if ("--mode=time" in sys.argv or " ".join(sys.argv).find("--mode time") >= 0) else "count"
-_abi.LIB_PATH = os.path.join(ROOT, "build", "prof2" if MODE == "time" else "prof", "libfognet_hip.so")
+_abi.LIB_PATH = os.environ.get("FOGNET_LIB", os.path.join(ROOT, "build", "prof2" if MODE == "time" else "prof", "libfognet_hip.so"))
 import fognetsimpp_amd as fa  # noqa: E402
 
 FIELDS = [("n_queued", "iterations"), ("n_started", "advert_loop_iters"), ("last_tick", "adverts"),
