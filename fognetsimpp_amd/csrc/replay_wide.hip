@@ -174,6 +174,24 @@ __device__ __forceinline__ uint64_t lane_min_key(const WideLds& L, int lane) {
   return mk;
 }
 
+// The lane's earliest advert and smallest w in one pass over its groups.
+__device__ __forceinline__ void lane_min_nxt_w(const WideLds& L, int lane, int64_t& mn, int& mj, int64_t& mw) {
+  mn = kNever;
+  mj = lane;
+  mw = kNever;
+#pragma unroll 4
+  for (int g = 0; g < L.G; ++g) {
+    const int64_t x = L.g_nxt[g * kWave + lane];
+    const int jj = L.g_j[g * kWave + lane];
+    const int64_t w = L.g_w[g * kWave + lane];
+    if (x < mn) {
+      mn = x;
+      mj = jj;
+    }
+    mw = w < mw ? w : mw;
+  }
+}
+
 __device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn, int& mj, uint64_t& mk) {
   lane_min_nxt(L, lane, mn, mj);
   mk = lane_min_key(L, lane);
@@ -219,15 +237,6 @@ __device__ __forceinline__ int64_t group_min_w(int g, int sl, int64_t sl_w, cons
   return mn;
 }
 
-__device__ __forceinline__ int64_t lane_min_w(const WideLds& L, int lane) {
-  int64_t m = kNever;
-#pragma unroll 4
-  for (int g = 0; g < L.G; ++g) {
-    const int64_t x = L.g_w[g * kWave + lane];
-    m = x < m ? x : m;
-  }
-  return m;
-}
 
 // The advert of node j's head completion reaches the broker (owner lane):
 // the view takes busyTime after releaseResource (ComputeBrokerApp3.cc:232,
@@ -711,8 +720,17 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           WideNode h = hit ? ch : nd[j];
           const int64_t dl_j = hit ? c_dl : P_dl[j];
           bool broken = false;
-          const bool fits =
-              apply_advert(h, e, dl_j, hit ? c_ul : P_ul[j], kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
+          const int64_t ul_j = hit ? c_ul : P_ul[j];
+          bool fits = apply_advert(h, e, dl_j, ul_j, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
+          // node j's later adverts that are due too: adverts of different nodes commute (each
+          // sets only its node's view), so j's are applied now, in their order, and only the
+          // last one's view is stored and rescanned (no store between the dependent entry loads)
+          while (nxt_j < t && !broken) {
+#ifdef FOGNET_WIDE_PROF
+            ++pf_same;
+#endif
+            fits &= apply_advert(h, e, dl_j, ul_j, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
+          }
           if constexpr (kExt) lerr |= !fits;
           lbroken |= broken;
           if (hit) ch = h;
@@ -721,17 +739,17 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           V.busy[sl] = busy_j;
           // the earliest advert: j's was the lane's (so its group's), rescan both levels
           group_scan_nxt(L, lane, g, sl, nxt_j, gx);
-          lane_min_nxt(L, lane, mn, mj);
-#ifdef FOGNET_WIDE_PROF
-          pf_same += (mn < t && mj == j) ? 1u : 0u;
-          pf_hit += hit ? 1u : 0u;
-#endif
           if constexpr (!kPerPublish) {
             const int64_t w_j = node_w(h, nxt_j, dl_j);
             V.w[sl] = w_j;
             L.g_w[g * kWave + lane] = group_min_w(g, sl, w_j, gw);
-            mw = lane_min_w(L, lane);
+            lane_min_nxt_w(L, lane, mn, mj, mw);  // (one LDS pass for both lane minima)
+          } else {
+            lane_min_nxt(L, lane, mn, mj);
           }
+#ifdef FOGNET_WIDE_PROF
+          pf_hit += hit ? 1u : 0u;
+#endif
           // the view key: only j's changed; the group (and lane) minimum needs a rescan only
           // when j held it and its busy time grew
           const uint64_t gk_old = L.g_key[g * kWave + lane];
