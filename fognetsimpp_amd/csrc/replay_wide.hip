@@ -99,6 +99,21 @@ struct WideView {
   int64_t* w;      // [G * kWideGroupSlots] REF_V3: node_w of the slot
 };
 
+// Node j lives in slot j >> 6 of lane (j + (j >> 10)) & 63: within each run of
+// 1,024 nodes (one LDS group row, one EXT_HIER region) the lanes are rotated by
+// the row index, so the rows' first nodes -- the smallest (busy, index) keys
+// when the view is idle, i.e. the regional brokers' usual choices -- belong to
+// different lanes, whose cached records then stay put (with lane j % 64 every
+// region's first node was lane 0's: its one cached record thrashed).
+// (FOGNET_POLICY_EXT_HIER only: the flat policies keep lane j % 64, measured 2 % faster there.)
+template <bool R>
+__host__ __device__ __forceinline__ int wlane(int j) { return R ? (j + (j >> 10)) & (kWave - 1) : j & (kWave - 1); }
+template <bool R>
+__host__ __device__ __forceinline__ int wnode(int s, int lane) {
+  return R ? (s << 6) | ((lane - (s >> 4)) & (kWave - 1)) : (s << 6) | lane;
+}
+static_assert(kWave == 64 && kWideGroupSlots == 16, "wlane/wnode: 64 lanes, 16 slots (1,024 nodes) per group");
+
 __host__ __device__ __forceinline__ int wide_groups(int N) {
   return ((N + kWave - 1) / kWave + kWideGroupSlots - 1) / kWideGroupSlots;
 }
@@ -115,6 +130,7 @@ __device__ __forceinline__ void group_load(const WideView& V, int g, int64_t (&x
 // Earliest advert of group g of this lane from its loaded ticks (slot `sl`
 // replaced by the value just computed: its load was issued before the store).
 // Slots past N hold kNever, so they need no test.
+template <bool R>
 __device__ __forceinline__ void group_scan_nxt(const WideLds& L, int lane, int g, int sl, int64_t sl_nxt,
                                                const int64_t (&x)[kWideGroupSlots]) {
   int64_t mn = kNever;
@@ -125,7 +141,7 @@ __device__ __forceinline__ void group_scan_nxt(const WideLds& L, int lane, int g
     const int64_t xi = s == sl ? sl_nxt : x[i];
     if (xi < mn) {
       mn = xi;
-      mj = s * kWave + lane;
+      mj = wnode<R>(s, lane);
     }
   }
   L.g_nxt[g * kWave + lane] = mn;
@@ -135,6 +151,7 @@ __device__ __forceinline__ void group_scan_nxt(const WideLds& L, int lane, int g
 // Smallest view key (busy << 32 | node) of group g of this lane, from HBM
 // (slot sl's busy just stored by this lane).  Slots past N hold busy
 // 0xFFFFFFFF, above every admissible advertised busy time.
+template <bool R>
 __device__ __forceinline__ uint64_t group_key(const WideView& V, int lane, int g) {
   uint32_t b[kWideGroupSlots];
 #pragma unroll
@@ -142,7 +159,7 @@ __device__ __forceinline__ uint64_t group_key(const WideView& V, int lane, int g
   uint64_t mk = ~0ull;
 #pragma unroll
   for (int i = 0; i < kWideGroupSlots; ++i) {
-    const uint64_t key = ((uint64_t)b[i] << 32) | (uint32_t)((g * kWideGroupSlots + i) * kWave + lane);
+    const uint64_t key = ((uint64_t)b[i] << 32) | (uint32_t)wnode<R>(g * kWideGroupSlots + i, lane);
     mk = key < mk ? key : mk;
   }
   return mk;
@@ -407,7 +424,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   // ---- node parameters + preconditions (fognet_hip.h, fognet_batch_in);
   // every node's first advert {MIPS, busyTime = 0.0} has reached the broker
   bool bad = false;
-  for (int j = lane; j < N; j += kWave) {
+  for (int sj = 0; sj < SP; ++sj) {  // this lane's nodes
+    const int j = wnode<kHier>(sj, lane);
+    if (j >= N) continue;
     int32_t m;
     int64_t d, u, ia;
     if (gen) {
@@ -433,16 +452,16 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   }
   for (int s = 0; s < SP; ++s) {  // slots past N too (group rescans read them): never due, never chosen
     V.nxt[s] = kNever;
-    V.busy[s] = s * kWave + lane < N ? 0u : 0xFFFFFFFFu;
+    V.busy[s] = wnode<kHier>(s, lane) < N ? 0u : 0xFFFFFFFFu;
     if constexpr (!kPerPublish) V.w[s] = kNever;
   }
   for (int h = lane; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kWave) L.hist[h] = 0u;
   L.p_i[lane] = -1;  // EXT_HIER pending slots: free
   for (int g = 0; g < L.G; ++g) {  // the initial view: nothing pending, every busy 0
-    const int j0 = g * kWideGroupSlots * kWave + lane;
+    const int j0 = wnode<kHier>(g * kWideGroupSlots, lane);  // the lane's smallest node of the group
     L.g_nxt[g * kWave + lane] = kNever;
     L.g_w[g * kWave + lane] = kNever;
-    L.g_j[g * kWave + lane] = lane;
+    L.g_j[g * kWave + lane] = j0;
     L.g_key[g * kWave + lane] = j0 < N ? (uint64_t)(uint32_t)j0 : ~0ull;
   }
   __syncthreads();
@@ -472,7 +491,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 
   // record and parameters of node kk into its owner lane's cache
   auto cache_node = [&](uint32_t kk) {
-    if (lane == (int)(kk % kWave) && (int)kk != cj) {
+    if (lane == wlane<kHier>((int)kk) && (int)kk != cj) {
       if (cj >= 0) nd[cj] = ch;  // write back the previous node's record
       cj = (int)kk;
       ch = nd[kk];
@@ -523,7 +542,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   // push escalated task i (publish tick t_i, MIPSRequired req_i) onto node kk; false: past kMaxTick
   auto push_one = [&](int i, int64_t t_i, uint32_t req_i, uint32_t kk) -> bool {
     cache_node(kk);
-    const int kl = (int)(kk % kWave);
+    const int kl = wlane<kHier>((int)kk);
     const UDiv div_k{readlane_u32((uint32_t)c_dv, kl), readlane_u32((uint32_t)(c_dv >> 32), kl)};
     const int64_t dl_k = readlane_i64(c_dl, kl) + A.hier_up;  // (the hop, then the downlink)
     const int64_t ul_k = readlane_i64(c_ul, kl), down_k = readlane_i64(c_down, kl);
@@ -738,7 +757,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           V.nxt[sl] = nxt_j;
           V.busy[sl] = busy_j;
           // the earliest advert: j's was the lane's (so its group's), rescan both levels
-          group_scan_nxt(L, lane, g, sl, nxt_j, gx);
+          group_scan_nxt<kHier>(L, lane, g, sl, nxt_j, gx);
           if constexpr (!kPerPublish) {
             const int64_t w_j = node_w(h, nxt_j, dl_j);
             V.w[sl] = w_j;
@@ -754,7 +773,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           // when j held it and its busy time grew
           const uint64_t gk_old = L.g_key[g * kWave + lane];
           const uint64_t nk = ((uint64_t)busy_j << 32) | (uint32_t)j;
-          const uint64_t gk_new = ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? group_key(V, lane, g)
+          const uint64_t gk_new = ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? group_key<kHier>(V, lane, g)
                                                                                  : (nk < gk_old ? nk : gk_old);
 #ifdef FOGNET_WIDE_PROF
           pf_gkey += ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? 1u : 0u;
@@ -781,9 +800,11 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         const uint32_t rq = readlane_u32((uint32_t)cr, jp);
         uint64_t mc = ~0ull;
         uint32_t mjj = ~0u;
-        for (int j = lane; j < N; j += kWave) {
+        for (int sj = 0; sj < SP; ++sj) {  // this lane's nodes (its view)
+          const int j = wnode<kHier>(sj, lane);
+          if (j >= N) continue;
           const uint32_t S = min(rq / (uint32_t)P_mips[j], kExtSatS);
-          const uint64_t c = (uint64_t)P_dl[j] + ((uint64_t)V.busy[j / kWave] + S) * (uint64_t)kTicksPerSecond;
+          const uint64_t c = (uint64_t)P_dl[j] + ((uint64_t)V.busy[sj] + S) * (uint64_t)kTicksPerSecond;
           if (c < mc) {
             mc = c;
             mjj = (uint32_t)j;
@@ -831,7 +852,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           break;
         }
       }
-      const int kl = (int)(k % kWave);
+      const int kl = wlane<kHier>((int)k);
 
       WTM(2)
       // 3) node k's record and parameters, in its owner lane (cached there)
@@ -1119,7 +1140,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12)
   // with B_j = node j's service seconds (its tail's cumulative sum), summed in node order
   if (A.p_busy && A.out_stats) {
-    // per node j (lane j % 64), then summed in node order 64 at a time
+    __syncthreads();  // (the records written back above by their owner lanes are read by others)
+    // per node j (lane j % 64 here), then summed in node order 64 at a time
     const int64_t H = n_done > 0 ? acc.last : 0;
     double sum = 0.0;
     for (int j0 = 0; j0 < N; j0 += kWave) {
