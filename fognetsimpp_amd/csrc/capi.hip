@@ -754,6 +754,8 @@ void fognet_job_stats_merge(fognet_job_stats* a, const fognet_job_stats* b) {
 void fognet_job_stats_add_rep(fognet_job_stats* a, const fognet_rep_stats* s) {
   if (!a || !s) return;
   a->n_reps += 1;
+  /* counted under FOGNET_FLAG_REF_ABORT too (status FOGNET_REF_ABORTED), like reduce_kernel */
+  if ((s->status == FOGNET_OK || s->status == FOGNET_REF_ABORTED) && s->abort_tick != INT64_MAX) a->n_ref_aborted += 1;
   if (s->status != FOGNET_OK) {
     a->n_failed += 1;
     return;
@@ -769,7 +771,6 @@ void fognet_job_stats_add_rep(fognet_job_stats* a, const fognet_rep_stats* s) {
   b.queue_max_raw = s->queue_max_raw;
   b.n_qtime = s->n_qtime;
   b.n_qtime_overflow = s->n_qtime_overflow;
-  b.n_ref_aborted = s->abort_tick != INT64_MAX ? 1 : 0;
   b.resp_min_ticks = s->resp_min_ticks;
   b.resp_max_ticks = s->resp_max_ticks;
   b.max_pending = s->max_pending;

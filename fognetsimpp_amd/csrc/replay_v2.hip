@@ -644,6 +644,9 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       ptk[q] = base + q < T ? tk[u] : kNever;
       prq[q] = base + q < T ? rq[u] : 0;
     }
+    // the row's lanes read each other's slots next: keep the compiler from
+    // moving those LDS reads above these stores (valid in divergent code)
+    __builtin_amdgcn_wave_barrier();
   };
   if (live && T > 0) stage_chunk(0);
   int64_t p_tick = (live && T > 0) ? ptk[0] : kNever;

@@ -87,9 +87,9 @@ struct WideLds {
   int G;
 };
 
-// EXT_HIER pending escalated tasks: at most one per lane (a replication with more
-// escalated tasks in flight at once, i.e. decided within one hop latency of each
-// other, is refused with FOGNET_ERR_UNSUPPORTED).
+// EXT_HIER pending escalated tasks: one LDS slot per lane; past 64 in flight at
+// once (decided within one hop latency of each other) they spill to an HBM
+// overflow list (WideWs::ov_off, see flush_pending).
 constexpr int kHierPending = kWave;
 
 // This lane's view in HBM: slot s (node s * 64 + lane) at [s].
@@ -319,7 +319,7 @@ __device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, in
 
 // Workspace layout (launch_replay_wide, replay_wide_workspace_bytes).
 struct WideWs {
-  size_t e_off, nd_off, nxt_off, busy_off, w_off, dv_off, gm_off, gd_off, gu_off, bytes;
+  size_t e_off, nd_off, nxt_off, busy_off, w_off, dv_off, gm_off, gd_off, gu_off, ov_off, bytes;
 };
 
 __host__ __device__ __forceinline__ size_t align64(size_t x) { return (x + 63) & ~(size_t)63; }
@@ -338,7 +338,9 @@ __host__ __device__ __forceinline__ WideWs wide_ws(int32_t R, int32_t T, int32_t
   const size_t RN = gen ? (size_t)R * (size_t)N : 0;
   w.gd_off = align64(w.gm_off + RN * sizeof(int32_t));
   w.gu_off = align64(w.gd_off + RN * sizeof(int64_t));
-  w.bytes = align64(w.gu_off + RN * sizeof(int64_t));
+  // EXT_HIER: the pending-escalation overflow list, [R][T] task indices
+  w.ov_off = align64(w.gu_off + RN * sizeof(int64_t));
+  w.bytes = align64(w.ov_off + (size_t)R * (size_t)T * sizeof(int32_t));
   return w;
 }
 
@@ -352,7 +354,8 @@ struct GenNodes {
 
 template <int POL>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
-                                                int64_t* VN, uint32_t* VB, int64_t* VW, GenNodes GN, unsigned char* w_lds);
+                                                int64_t* VN, uint32_t* VB, int64_t* VW, GenNodes GN, int32_t* OV,
+                                                unsigned char* w_lds);
 
 // One replication per workgroup (r = blockIdx.x), or, with A.wide_list set,
 // the replications the register kernel handed over, taken in turn by the
@@ -360,15 +363,15 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 // list (complete before this launch, stream order) is exhausted.
 template <int POL>
 __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry* E, WideNode* ND, int64_t* VN,
-                                                         uint32_t* VB, int64_t* VW, GenNodes GN) {
+                                                         uint32_t* VB, int64_t* VW, GenNodes GN, int32_t* OV) {
   extern __shared__ __align__(16) unsigned char w_lds[];
   if (A.wide_list == nullptr) {
-    replay_wide_rep<POL>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, VW, GN, w_lds);
+    replay_wide_rep<POL>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, VW, GN, OV, w_lds);
     return;
   }
   const int n = *A.wide_count;
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
-    replay_wide_rep<POL>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, VW, GN, w_lds);
+    replay_wide_rep<POL>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, VW, GN, OV, w_lds);
     __syncthreads();  // LDS reuse by the next replication
   }
 }
@@ -376,7 +379,8 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
 // Replication r with workspace slot wr.
 template <int POL>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
-                                                int64_t* VN, uint32_t* VB, int64_t* VW, GenNodes GN, unsigned char* w_lds) {
+                                                int64_t* VN, uint32_t* VB, int64_t* VW, GenNodes GN, int32_t* OV,
+                                                unsigned char* w_lds) {
   constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
   constexpr bool kHier = POL == FOGNET_POLICY_EXT_HIER;
   constexpr bool kPerPublish = kExt || kHier;  // the decision depends on the publish itself
@@ -407,6 +411,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)T;
   WideEntry* const e = E + (size_t)wr * (size_t)T;
+  int32_t* const ov = OV + (size_t)wr * (size_t)T;  // EXT_HIER pending-escalation overflow list
   WideNode* const nd = ND + (size_t)wr * (size_t)N;
   const bool hist = A.hist != nullptr;
   // generated mode (ReplayArgs::gen_on): the node parameters are computed
@@ -513,7 +518,18 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   // precede), and at the end.  Each chain stays in arrival order, so the FIFO
   // recurrence and the advert scans hold as for direct tasks.  A pushed pending
   // task's statistics and outputs are recorded at once (uniform code).
-  int n_pend = 0;  // occupied pending slots (wave-uniform)
+  // Overflow (ComputeBrokerApp3.cc:305-309: a node's FIFO takes any number of
+  // tasks, so any number may be in flight): while all 64 slots are taken, or
+  // the overflow list is not empty, an escalated task i goes to the HBM list
+  // ov[ov_head .. ov_tail) (decision order, -1: pushed already) with its
+  // pending fields in its own entry e[i] (written for real when it is pushed:
+  // {a, done := publish tick, S := MIPSRequired, prev := node, pad = 2}).
+  // Every slot's task was decided before every listed one, so pushing the
+  // slots' selected tasks first and then the list's in list order keeps each
+  // node's arrival order (per node decision order: the same dl and hop).
+  int n_pend = 0;  // pending escalated tasks, slots and overflow list (wave-uniform)
+  int n_ovf = 0;   // of which in the overflow list (wave-uniform)
+  int ov_head = 0, ov_tail = 0;
   int n_sq = 0;    // staged statistics of pushed pending tasks (wave-uniform)
   // accumulate the staged statistics, one task per lane (the chunk end's code)
   auto drain_stats = [&]() {
@@ -537,7 +553,14 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     n_sq = 0;
   };
   auto pend_count = [&](uint32_t kk) -> uint32_t {
-    return n_pend ? (uint32_t)__popcll(ballot(L.p_i[lane] >= 0 && (uint32_t)L.p_k[lane] == kk)) : 0u;
+    if (!n_pend) return 0u;
+    uint32_t c = (uint32_t)__popcll(ballot(L.p_i[lane] >= 0 && (uint32_t)L.p_k[lane] == kk));
+    for (int w0 = n_ovf ? ov_head : ov_tail; w0 < ov_tail; w0 += kWave) {
+      const int pos = w0 + lane;
+      const int32_t oi = pos < ov_tail ? ov[pos] : -1;
+      c += (uint32_t)__popcll(ballot(oi >= 0 && (uint32_t)e[oi].prev == kk));
+    }
+    return c;
   };
   // push escalated task i (publish tick t_i, MIPSRequired req_i) onto node kk; false: past kMaxTick
   auto push_one = [&](int i, int64_t t_i, uint32_t req_i, uint32_t kk) -> bool {
@@ -625,7 +648,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   // push the pending tasks of node kk arriving at or before lim (by_node), or of any
   // node arriving before lim, in decision order (per node also arrival order)
   auto flush_pending = [&](bool by_node, uint32_t kk, int64_t lim) -> bool {
-    while (n_pend > 0) {
+    while (n_pend - n_ovf > 0) {  // the slots
       const int32_t pi = L.p_i[lane];
       const int64_t pa = L.p_a[lane];
       const bool sel = pi >= 0 && (by_node ? ((uint32_t)L.p_k[lane] == kk && pa <= lim) : pa < lim);
@@ -638,6 +661,40 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       if (lane == sl) L.p_i[lane] = -1;
       --n_pend;
       if (!push_one((int)mi, t_i, r_i, k_i)) return false;
+    }
+    if (!n_ovf) return true;
+    // the overflow list, 64 entries at a time, in list (= decision) order
+    for (int w0 = ov_head; w0 < ov_tail && n_ovf; w0 += kWave) {
+      const int pos = w0 + lane;
+      const int32_t oi = pos < ov_tail ? ov[pos] : -1;
+      WideEntry x{};
+      if (oi >= 0) x = e[oi];
+      uint64_t sm = ballot(oi >= 0 && (by_node ? ((uint32_t)x.prev == kk && x.a <= lim) : x.a < lim));
+      while (sm) {
+        const int sl = (int)__builtin_ctzll(sm);
+        sm &= sm - 1ull;
+        const int32_t i = (int32_t)readlane_u32((uint32_t)oi, sl);
+        const int64_t t_i = readlane_i64(x.done, sl);
+        const uint32_t k_i = readlane_u32((uint32_t)x.prev, sl);
+        const uint32_t r_i = readlane_u32(x.S, sl);
+        if (lane == sl) ov[pos] = -1;
+        --n_ovf;
+        --n_pend;
+        if (!push_one((int)i, t_i, r_i, k_i)) return false;
+      }
+    }
+    if (!n_ovf) {
+      ov_head = ov_tail = 0;
+    } else {  // drop the pushed entries at the head
+      for (;;) {
+        const int pos = ov_head + lane;
+        const uint64_t live = ballot(pos < ov_tail && ov[pos] >= 0);
+        if (live) {
+          ov_head += (int)__builtin_ctzll(live);
+          break;
+        }
+        ov_head += kWave;
+      }
     }
     return true;
   };
@@ -860,19 +917,25 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       uint32_t pend_k = 0u;  // EXT_HIER: k's escalated tasks still pending (decided, not pushed)
       if constexpr (kHier) {
         if (escalated) {  // wait in a pending slot until the tasks that reach k before it are pushed
-          const uint64_t fr = ballot(L.p_i[lane] < 0);
-          if (!fr) {
-            err = FOGNET_ERR_UNSUPPORTED;  // more than 64 escalated tasks in flight at once
-            break;
-          }
-          const int sl = (int)__builtin_ctzll(fr);
+          const uint64_t fr = n_ovf ? 0ull : ballot(L.p_i[lane] < 0);
           const int64_t a_esc = t + readlane_i64(c_dl, kl) + A.hier_up;
-          if (lane == sl) {
-            L.p_i[lane] = c0 + jp;
-            L.p_t[lane] = t;
-            L.p_a[lane] = a_esc;
-            L.p_k[lane] = (int32_t)k;
-            L.p_r[lane] = readlane_u32((uint32_t)cr, jp);
+          const uint32_t rq = readlane_u32((uint32_t)cr, jp);
+          if (fr) {
+            const int sl = (int)__builtin_ctzll(fr);
+            if (lane == sl) {
+              L.p_i[lane] = c0 + jp;
+              L.p_t[lane] = t;
+              L.p_a[lane] = a_esc;
+              L.p_k[lane] = (int32_t)k;
+              L.p_r[lane] = rq;
+            }
+          } else {  // all slots taken (or the list in use): the overflow list in HBM
+            if (lane == 0) {
+              e[c0 + jp] = WideEntry{a_esc, t, 0u, rq, (int32_t)k, -1, 2};
+              ov[ov_tail] = c0 + jp;
+            }
+            ++ov_tail;
+            ++n_ovf;
           }
           ++n_pend;
           const uint32_t tot = (uint32_t)readlane_u32((uint32_t)ch.npend, kl) + pend_count(k);
@@ -1168,11 +1231,11 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 
 template <int POL>
 void launch_wide_pol(const ReplayArgs& a, int32_t slots, WideEntry* e, WideNode* nd, int64_t* vn, uint32_t* vb,
-                     int64_t* vw, GenNodes gn, size_t lds, hipStream_t s) {
+                     int64_t* vw, GenNodes gn, int32_t* ov, size_t lds, hipStream_t s) {
   if (lds > 65536)  // above the default dynamic-LDS limit (N > ~51,000 nodes; gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&replay_wide_kernel<POL>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb, vw, gn);
+  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb, vw, gn, ov);
 }
 
 }  // namespace
@@ -1196,13 +1259,14 @@ hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slot
   int64_t* const vw = reinterpret_cast<int64_t*>(base + w.w_off);
   const GenNodes gn{reinterpret_cast<int32_t*>(base + w.gm_off), reinterpret_cast<int64_t*>(base + w.gd_off),
                     reinterpret_cast<int64_t*>(base + w.gu_off), reinterpret_cast<uint64_t*>(base + w.dv_off)};
+  int32_t* const ov = reinterpret_cast<int32_t*>(base + w.ov_off);
   const size_t lds = replay_wide_lds_bytes(a.N);
   if (a.policy == FOGNET_POLICY_EXT_LAT)
-    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, slots, e, nd, vn, vb, vw, gn, lds, s);
+    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, slots, e, nd, vn, vb, vw, gn, ov, lds, s);
   else if (a.policy == FOGNET_POLICY_EXT_HIER)
-    launch_wide_pol<FOGNET_POLICY_EXT_HIER>(a, slots, e, nd, vn, vb, vw, gn, lds, s);
+    launch_wide_pol<FOGNET_POLICY_EXT_HIER>(a, slots, e, nd, vn, vb, vw, gn, ov, lds, s);
   else
-    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, slots, e, nd, vn, vb, vw, gn, lds, s);
+    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, slots, e, nd, vn, vb, vw, gn, ov, lds, s);
   return hipGetLastError();
 }
 

@@ -140,6 +140,9 @@ __global__ __launch_bounds__(kRedThreads) void reduce_kernel(const fognet_rep_st
   for (int r = r0 + threadIdx.x; r < r1; r += kRedThreads) {
     const fognet_rep_stats& s = st[r];
     a.n_reps += 1;
+    // the reference's abort point counts under FOGNET_FLAG_REF_ABORT too, where such a replication's
+    // status is FOGNET_REF_ABORTED (failed: it contributes nothing else)
+    if (s.status == FOGNET_OK || s.status == FOGNET_REF_ABORTED) a.n_ref_aborted += s.abort_tick != INT64_MAX ? 1 : 0;
     if (s.status != FOGNET_OK) {
       a.n_failed += 1;
       continue;
@@ -153,7 +156,6 @@ __global__ __launch_bounds__(kRedThreads) void reduce_kernel(const fognet_rep_st
     a.queue_max_raw = max(a.queue_max_raw, s.queue_max_raw);
     a.n_qtime += s.n_qtime;
     a.n_qtime_overflow += s.n_qtime_overflow;
-    a.n_ref_aborted += s.abort_tick != INT64_MAX ? 1 : 0;
     a.resp_min_ticks = min(a.resp_min_ticks, s.resp_min_ticks);
     a.resp_max_ticks = max(a.resp_max_ticks, s.resp_max_ticks);
     a.max_pending = max(a.max_pending, (int64_t)s.max_pending);

@@ -71,7 +71,7 @@ typedef enum fognet_status {
     FOGNET_ERR_CAPACITY = 7,    /* v2 queue_capacity exceeded; a decision whose smallest advertised busy
                                    time is 2^32 - 1 s or more (the view keeps 32 bits, saturated: larger
                                    values only lose); EXT_LAT: an advertised busy time of 2^24 s or more */
-    FOGNET_ERR_UNSUPPORTED = 8, /* configuration not implemented (e.g. N > 256, unknown policy)        */
+    FOGNET_ERR_UNSUPPORTED = 8, /* configuration not implemented (e.g. N > 65,536, unknown policy)     */
     FOGNET_REF_ABORTED = 9,     /* replication status under FOGNET_FLAG_REF_ABORT: the reference run ends
                                    at a queueTime emission that overflows (ComputeBrokerApp3.cc:238; see
                                    "Reference signal values"); outputs are still written in full     */
@@ -108,9 +108,11 @@ typedef enum fognet_policy {
                                    reach every broker with the node's uplink latency.  A direct
                                    task can reach a node before an escalated task decided earlier
                                    (it overtakes it inside the hop): the node serves in arrival
-                                   order.  More than 64 escalated tasks in flight at once
-                                   (decided within one hop of each other) are not modelled: that
-                                   replication's status is FOGNET_ERR_UNSUPPORTED.            */
+                                   order; any number of escalated tasks may be in flight at once
+                                   (the node FIFO takes any length, ComputeBrokerApp3.cc:305-309).
+                                   A replication that fails (status != OK) leaves the per-task
+                                   outputs of escalated tasks still in flight at the error
+                                   unwritten, like every task after the error.                */
 } fognet_policy;
 
 /* Region size of FOGNET_POLICY_EXT_HIER (node r * 1024 .. r * 1024 + 1023 form region r). */
@@ -211,7 +213,8 @@ typedef struct fognet_job_stats {
                                  order across GPUs; differs from another sharding's sum by
                                  rounding only (within 1e-9 relative)                            */
     int64_t n_qtime, n_qtime_overflow;
-    int64_t n_ref_aborted;    /* replications the reference would have aborted (abort_tick set)  */
+    int64_t n_ref_aborted;    /* replications the reference would have aborted (abort_tick set),
+                                 status OK or FOGNET_REF_ABORTED (the latter also in n_failed) */
 } fognet_job_stats;
 
 /* R trace replays of T tasks over N fog nodes, SoA, row-major [R][T] / [R|1][N]. */

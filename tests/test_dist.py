@@ -31,7 +31,8 @@ def job_from_rep_stats(st):
     rec["queue_max_raw"] = int(ok["queue_max_raw"].max()) if len(ok) else big.min
     rec["n_qtime"] = int(ok["n_qtime"].sum())
     rec["n_qtime_overflow"] = int(ok["n_qtime_overflow"].sum())
-    rec["n_ref_aborted"] = int((ok["abort_tick"] != np.iinfo(np.int64).max).sum())
+    ab = st[(st["status"] == 0) | (st["status"] == _abi.FOGNET_REF_ABORTED)]  # counted under the flag too
+    rec["n_ref_aborted"] = int((ab["abort_tick"] != np.iinfo(np.int64).max).sum())
     rec["resp_max_ticks"] = int(ok["resp_max_ticks"].max()) if len(ok) else big.min
     rec["max_pending"] = int(ok["max_pending"].max()) if len(ok) else 0
     for name, lo, hi in (("queue_sum", "queue_sum_lo", "queue_sum_hi"), ("queue_sq", "queue_sq_lo", "queue_sq_hi"),

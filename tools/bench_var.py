@@ -1,4 +1,4 @@
-"""bench.py against a variant build (tools/build_variant.sh): FOGNET_LIB=build/var/X/libfognet_hip.so
+"""bench.py against a variant build (tools/build_variant.sh): FOGNET_LIB=build/ab/X/libfognet_hip.so
 python tools/bench_var.py <bench args>.  Diagnostics only; the product bench loads the in-tree library."""
 import os
 import runpy

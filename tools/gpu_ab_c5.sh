@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 for rep in 1 2; do
   for v in ${VARIANTS:-base new}; do
     for pol in EXT_HIER REF_V3; do
-      FOGNET_LIB=build/var/$v/libfognet_hip.so timeout -k 10 300 python tools/bench_var.py --workload c5 --policy $pol --steps 5 --warmup 1 --no-cpu > gpurun_out/ab_c5_$v.log 2>&1 || { tail gpurun_out/ab_c5_$v.log; exit 1; }
+      FOGNET_LIB=build/ab/$v/libfognet_hip.so timeout -k 10 300 python tools/bench_var.py --workload c5 --policy $pol --steps 5 --warmup 1 --no-cpu > gpurun_out/ab_c5_$v.log 2>&1 || { tail gpurun_out/ab_c5_$v.log; exit 1; }
       echo "$v $pol $(grep '^{' gpurun_out/ab_c5_$v.log | python -c 'import json,sys; print(round(json.loads(sys.stdin.read())["ms_per_step"],2))')"
     done
   done

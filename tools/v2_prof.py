@@ -4,7 +4,7 @@ import os, sys
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fognetsimpp_amd import _abi
-_abi.LIB_PATH = os.environ.get("FOGNET_LIB", "build/var/v2prof/libfognet_hip.so")
+_abi.LIB_PATH = os.environ.get("FOGNET_LIB", "build/ab/v2prof/libfognet_hip.so")
 import fognetsimpp_amd as fa
 from fognetsimpp_amd import formats
 MS = 10**9

@@ -6,7 +6,7 @@ import os, sys
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fognetsimpp_amd import _abi
-_abi.LIB_PATH = os.environ.get("FOGNET_LIB", "build/var/wideprof/libfognet_hip.so")
+_abi.LIB_PATH = os.environ.get("FOGNET_LIB", "build/ab/wideprof/libfognet_hip.so")
 import fognetsimpp_amd as fa
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 T, N = 10_000, 10_000
