@@ -675,7 +675,8 @@ int fognet_user_stats_dev(fognet_ctx* c, const fognet_batch_in* in, const fognet
 int fognet_run_v2_dev(fognet_ctx* c, const fognet_v2_in* in, fognet_v2_out* out, void* stream) {
   if (!c || !in || !out) return FOGNET_ERR_ARG;
   if (in->R < 0 || in->T < 0 || in->N < 0) return fail(c, FOGNET_ERR_ARG, "negative R/T/N");
-  if (in->N > FOGNET_V2_MAX_NODES) return fail(c, FOGNET_ERR_UNSUPPORTED, "the v2 replay keeps node j on lane j: N <= 64");
+  if (in->N > FOGNET_V2_MAX_NODES)
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "the v2 replay keeps at most 16 nodes per lane: N <= 1024");
   if (in->node_stride != 0 && in->node_stride != in->N) return fail(c, FOGNET_ERR_ARG, "node_stride must be 0 or N");
   const int q = in->queue_capacity ? in->queue_capacity : 256;
   if (q < 2 || (q & (q - 1)) != 0 || q > (1 << 16)) return fail(c, FOGNET_ERR_ARG, "queue_capacity must be a power of two in [2, 2^16]");
@@ -689,7 +690,7 @@ int fognet_run_v2_dev(fognet_ctx* c, const fognet_v2_in* in, fognet_v2_out* out,
     return fail(c, FOGNET_ERR_ARG, "null output array");
   int rc = set_device(c);
   if (rc) return rc;
-  rc = ensure(c, (void**)&c->ring, &c->ring_bytes, fognet::replay_v2_workspace_bytes(in->R, in->T, qlog),
+  rc = ensure(c, (void**)&c->ring, &c->ring_bytes, fognet::replay_v2_workspace_bytes(in->R, in->T, in->N, qlog),
               "v2 replay workspace");
   if (rc) return rc;
   hipError_t e = fognet::launch_replay_v2(*in, *out, c->ring, qlog, (hipStream_t)stream);

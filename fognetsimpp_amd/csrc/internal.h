@@ -351,7 +351,7 @@ hipError_t launch_decide_v2(int64_t m, int32_t n, const int32_t* mips, const int
 hipError_t launch_user_stats(const ReplayArgs& a, const int64_t* user_ul, const int64_t* user_dl, int32_t per_task,
                              fognet_user_stats* out, hipStream_t s);
 // v2 model replay (replay_v2.hip)
-size_t replay_v2_workspace_bytes(int32_t R, int32_t T, int32_t q_log2);
+size_t replay_v2_workspace_bytes(int32_t R, int32_t T, int32_t N, int32_t q_log2);
 hipError_t launch_replay_v2(const fognet_v2_in& in, const fognet_v2_out& out, void* workspace, int32_t q_log2,
                             hipStream_t s);
 hipError_t launch_gen_trace(const fognet_gen_params& p, int64_t r0, int32_t R, int32_t T, int32_t N,

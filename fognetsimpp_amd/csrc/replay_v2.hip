@@ -106,20 +106,40 @@ struct V2Args {
   int32_t q_log2;
 };
 
+// Per-node state of replay_v2_kernel (node j = slot * 64 + lane).
+struct V2Node {
+  int32_t mips, view;  // remaining MIPS; the broker's view of it (starts at MIPS 0, BrokerBaseApp2.cc:105)
+  int64_t dl, ul;
+  bool t_sched;        // selfMsg->isScheduled()
+  int64_t t_tick;
+  uint64_t t_seq;
+  uint32_t t_kind;
+  uint32_t in_h, in_n, out_h, out_n, rs_h, rs_n;
+  V2Msg in_hd, out_hd;
+  // adverts that change nothing at the broker (kPhantomAdverts): the MIPS of the
+  // node's last advert sent, its one unqueued advert in flight and the count of those
+  int32_t last_sent;
+  int64_t ph_tick;  // (INT64_MIN: none in flight)
+  uint64_t ph_seq;
+  uint32_t ph_cnt;
+};
+
+// NPL nodes per lane (N <= 64 * NPL): node j on lane j % 64, slot j / 64, like
+// the v3 register kernel.  The slot is a compile-time index everywhere (static
+// loops select it), so the state stays in registers.
+template <int NPL>
 __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
+  constexpr int kPad = NPL * kWave;  // queue rows per replication
   const fognet_v2_in& A = P.in;
   const fognet_v2_out& O = P.out;
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
   const int N = A.N, T = A.T;
-  const bool own = lane < N;
   const uint32_t Q = 1u << P.q_log2, qm = Q - 1u;
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)T;
-  const size_t qbase = ((size_t)r * (size_t)FOGNET_V2_MAX_NODES + (size_t)lane) << P.q_log2;
-  V2Msg* const inq = P.inq + qbase;
-  V2Msg* const outq = P.outq + qbase;
-  V2Res* const res = P.res + qbase;
+  // queue row of slot s of this lane (node s * 64 + lane)
+  auto qrow = [&](int s) -> size_t { return ((size_t)r * (size_t)kPad + (size_t)(s * kWave + lane)) << P.q_log2; };
   uint8_t* const list = P.list + tbase;
   const int64_t* const arrive = A.arrive_tick + tbase;
   const int32_t* const reqs = A.req_mips + tbase;
@@ -129,32 +149,37 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
   const int64_t rt_ticks = (int64_t)add_rn(rtx, rtx >= 0.0 ? 0.5 : -0.5);
   const int64_t stop = A.stop_tick[r];
 
-  // ---- node j on lane j
-  int32_t mips = 0, view = 0;  // the broker's Broker record starts at MIPS 0 (BrokerBaseApp2.cc:105)
-  int64_t dl = 0, ul = 0;
-  bool t_sched = false;  // selfMsg->isScheduled()
-  int64_t t_tick = kNever;
-  uint64_t t_seq = ~0ull;
-  uint32_t t_kind = kKindAdvertise;
+  V2Node nd[NPL];
   bool bad = !(stop <= kMaxV2Tick) || !(rtx >= 0.0) || rt_ticks > kMaxV2Tick;
-  if (own) {
-    mips = A.mips[nbase + lane];
-    dl = A.dl_tick[nbase + lane];
-    ul = A.ul_tick[nbase + lane];
-    const int64_t fa = A.first_adv_tick[nbase + lane];
-    bad |= dl < 0 || ul < 0 || fa < 0 || dl > kMaxV2Tick || ul > kMaxV2Tick || fa > kMaxV2Tick;
-    t_sched = true;  // the first ADVERTISEMIPS firing, pre-inserted in node order
-    t_tick = fa;
-    t_seq = (uint64_t)lane;
+#pragma unroll
+  for (int s = 0; s < NPL; ++s) {
+    const int j = s * kWave + lane;
+    V2Node& x = nd[s];
+    x.mips = 0;
+    x.view = 0;
+    x.dl = x.ul = 0;
+    x.t_sched = false;
+    x.t_tick = kNever;
+    x.t_seq = ~0ull;
+    x.t_kind = kKindAdvertise;
+    x.in_h = x.in_n = x.out_h = x.out_n = x.rs_h = x.rs_n = 0u;
+    x.in_hd = V2Msg{kNever, ~0ull, 0, 0};
+    x.out_hd = V2Msg{kNever, ~0ull, 0, 0};
+    x.last_sent = kNoAdvert;
+    x.ph_tick = INT64_MIN;
+    x.ph_seq = 0ull;
+    x.ph_cnt = 0u;
+    if (j < N) {
+      x.mips = A.mips[nbase + j];
+      x.dl = A.dl_tick[nbase + j];
+      x.ul = A.ul_tick[nbase + j];
+      const int64_t fa = A.first_adv_tick[nbase + j];
+      bad |= x.dl < 0 || x.ul < 0 || fa < 0 || x.dl > kMaxV2Tick || x.ul > kMaxV2Tick || fa > kMaxV2Tick;
+      x.t_sched = true;  // the first ADVERTISEMIPS firing, pre-inserted in node order
+      x.t_tick = fa;
+      x.t_seq = (uint64_t)j;
+    }
   }
-  uint32_t in_h = 0u, in_n = 0u, out_h = 0u, out_n = 0u, rs_h = 0u, rs_n = 0u;
-  V2Msg in_hd = {kNever, ~0ull, 0, 0}, out_hd = {kNever, ~0ull, 0, 0};
-  // adverts that change nothing at the broker (kPhantomAdverts): the MIPS of the
-  // node's last advert sent, its one unqueued advert in flight and the count of those
-  int32_t last_sent = kNoAdvert;
-  int64_t ph_tick = INT64_MIN;  // (none in flight)
-  uint64_t ph_seq = 0ull;
-  uint32_t ph_cnt = 0u;
 
   // ---- broker (wave-uniform)
   int32_t pool = A.broker_mips[r];
@@ -174,30 +199,40 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
   uint64_t end_seq = ~0ull;
 
   while (err == FOGNET_OK) {
-    // ---- the earliest event: the lanes' own sources, then the broker's
+    // ---- the earliest event: the lanes' own sources (over their slots), then the broker's
     int64_t ct = kNever;
     uint64_t cs = ~0ull;
     int src = 0;  // 1 self-message, 2 task arrival, 3 message at the broker
-    if (t_sched) {
-      ct = t_tick;
-      cs = t_seq;
-      src = 1;
+    int csl = 0;  // its slot
+#pragma unroll
+    for (int s = 0; s < NPL; ++s) {
+      const V2Node& x = nd[s];
+      if (x.t_sched && earlier(x.t_tick, x.t_seq, ct, cs)) {
+        ct = x.t_tick;
+        cs = x.t_seq;
+        src = 1;
+        csl = s;
+      }
+      if (x.in_n && earlier(x.in_hd.tick, x.in_hd.seq, ct, cs)) {
+        ct = x.in_hd.tick;
+        cs = x.in_hd.seq;
+        src = 2;
+        csl = s;
+      }
+      if (x.out_n && earlier(x.out_hd.tick, x.out_hd.seq, ct, cs)) {
+        ct = x.out_hd.tick;
+        cs = x.out_hd.seq;
+        src = 3;
+        csl = s;
+      }
     }
-    if (in_n && earlier(in_hd.tick, in_hd.seq, ct, cs)) {
-      ct = in_hd.tick;
-      cs = in_hd.seq;
-      src = 2;
-    }
-    if (out_n && earlier(out_hd.tick, out_hd.seq, ct, cs)) {
-      ct = out_hd.tick;
-      cs = out_hd.seq;
-      src = 3;
-    }
-    const int64_t m_tick = (int64_t)(N <= 16 ? row0_min_u64((uint64_t)ct) : wave_min_u64((uint64_t)ct));
+    const int64_t m_tick =
+        (int64_t)((NPL == 1 && N <= 16) ? row0_min_u64((uint64_t)ct) : wave_min_u64((uint64_t)ct));
     const uint64_t tied = ballot(src != 0 && ct == m_tick);
     uint64_t m_seq = ~0ull, wmask = tied;
-    if (__popcll(tied) > 1) {  // same-tick events on several nodes: insertion order decides
-      m_seq = N <= 16 ? row0_min_u64(ct == m_tick ? cs : ~0ull) : wave_min_u64(ct == m_tick ? cs : ~0ull);
+    if (__popcll(tied) > 1) {  // same-tick events on several lanes: insertion order decides
+      m_seq = (NPL == 1 && N <= 16) ? row0_min_u64(ct == m_tick ? cs : ~0ull)
+                                    : wave_min_u64(ct == m_tick ? cs : ~0ull);
       wmask = ballot(src != 0 && ct == m_tick && cs == m_seq);
     } else if (tied) {
       m_seq = ((uint64_t)readlane_u32((uint32_t)(cs >> 32), __builtin_ctzll(tied)) << 32) |
@@ -264,21 +299,37 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
         }
       } else {
         // the LAST node whose advertised MIPS exceeds node 0's (:241-248), else node 0
-        const int32_t v0 = (int32_t)readlane_u32((uint32_t)view, 0);
-        k = (int32_t)~wave_min_u32(~((own && lane >= 1 && view > v0) ? (uint32_t)lane : 0u));
-        const int32_t vk = (int32_t)readlane_u32((uint32_t)view, k);
+        const int32_t v0 = (int32_t)readlane_u32((uint32_t)nd[0].view, 0);
+        uint32_t last = 0u;
+#pragma unroll
+        for (int s = 0; s < NPL; ++s) {
+          const int j = s * kWave + lane;
+          if (j < N && j >= 1 && nd[s].view > v0) last = (uint32_t)j;
+        }
+        k = (int32_t)~wave_min_u32(~last);
+        const int kl = k & (kWave - 1), ks = k / kWave;
+        int32_t vk = 0;
+#pragma unroll
+        for (int s = 0; s < NPL; ++s)
+          if (s == ks) vk = (int32_t)readlane_u32((uint32_t)nd[s].view, kl);
         lmark = kListForwarded;  // :255-260, before the MIPS check
         if (req < vk) {          // :262-270: FognetMsgTask to node k
           status = FOGNET_V2_ST_FORWARDED;
           ++st.n_forwarded;
-          if (lane == k) {
-            const V2Msg m = {now + dl, seq, req, t};
-            if (in_n == Q) {
-              bad = true;
-            } else {
-              inq[(in_h + in_n) & qm] = m;
-              if (in_n == 0u) in_hd = m;
-              ++in_n;
+          if (lane == kl) {
+#pragma unroll
+            for (int s = 0; s < NPL; ++s) {
+              if (s == ks) {
+                V2Node& x = nd[s];
+                const V2Msg m = {now + x.dl, seq, req, t};
+                if (x.in_n == Q) {
+                  bad = true;
+                } else {
+                  P.inq[qrow(s) + ((x.in_h + x.in_n) & qm)] = m;
+                  if (x.in_n == 0u) x.in_hd = m;
+                  ++x.in_n;
+                }
+              }
             }
           }
           ++seq;
@@ -323,17 +374,25 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
         if (mark == kListForwarded) ++st.n_inflated;
       }
     } else {
-      // ---- an event of node w
+      // ---- an event of node ws * 64 + w
       const int wsrc = (int)readlane_u32((uint32_t)src, w);
+      const int ws = (int)readlane_u32((uint32_t)csl, w);
       if (wsrc == 3) {
         // a node -> broker message reaches the broker (BrokerBaseApp2.cc:128-154)
-        const int32_t mk = (int32_t)readlane_u32((uint32_t)out_hd.kind, w);
-        const int32_t mv = (int32_t)readlane_u32((uint32_t)out_hd.val, w);
-        if (lane == w) {
-          ++out_h;
-          --out_n;
-          if (out_n) out_hd = outq[out_h & qm];
-          if (mk == kMsgAdvert) view = mv;  // setMips (:132)
+        int32_t mk = 0, mv = 0;
+#pragma unroll
+        for (int s = 0; s < NPL; ++s) {
+          if (s == ws) {
+            mk = (int32_t)readlane_u32((uint32_t)nd[s].out_hd.kind, w);
+            mv = (int32_t)readlane_u32((uint32_t)nd[s].out_hd.val, w);
+            if (lane == w) {
+              V2Node& x = nd[s];
+              ++x.out_h;
+              --x.out_n;
+              if (x.out_n) x.out_hd = P.outq[qrow(s) + (x.out_h & qm)];
+              if (mk == kMsgAdvert) x.view = mv;  // setMips (:132)
+            }
+          }
         }
         if (mk == kMsgAck6) {  // relay and erase the request if it is still listed (:145-153)
           bool relayed = false;
@@ -347,75 +406,79 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
         // the node's own events: its self-message or a task arrival.  The owner
         // lane runs the handler; sequence numbers and per-task results are
         // broadcast afterwards (lane 0 writes the outputs).
-        int32_t o_task = -1;        // task whose result changed
-        uint32_t o_what = 0u;       // 1 released, 2 accepted, 3 rejected
-        bool released = false;
+        int32_t o_task = -1;   // task whose result changed
+        uint32_t o_what = 0u;  // 1 released, 2 accepted, 3 rejected
         uint64_t my_seq = seq;
         if (lane == w) {
-          if (wsrc == 1) {
-            t_sched = false;
-            if (t_kind == kKindRelease && rs_n) {
-              // ComputeBrokerApp2::releaseResource (:222-245): the first reservation
-              // with deadline < now (the oldest: deadlines follow arrival order)
-              const V2Res h = res[rs_h & qm];
-              if (h.deadline < dbl(now)) {
-                mips += h.req;  // :226
-                ++rs_h;
-                --rs_n;
-                released = true;
-                o_task = h.task;
-                o_what = 1u;
-                const V2Msg m = {now + ul, my_seq++, kMsgAck6, h.task};  // puback 6 (:231-235)
-                if (out_n == Q) bad = true;
-                else {
-                  outq[(out_h + out_n) & qm] = m;
-                  if (out_n == 0u) out_hd = m;
-                  ++out_n;
+#pragma unroll
+          for (int s = 0; s < NPL; ++s) {
+            if (s != ws) continue;
+            V2Node& x = nd[s];
+            V2Msg* const outq = P.outq + qrow(s);
+            if (wsrc == 1) {
+              x.t_sched = false;
+              if (x.t_kind == kKindRelease && x.rs_n) {
+                // ComputeBrokerApp2::releaseResource (:222-245): the first reservation
+                // with deadline < now (the oldest: deadlines follow arrival order)
+                const V2Res h = P.res[qrow(s) + (x.rs_h & qm)];
+                if (h.deadline < dbl(now)) {
+                  x.mips += h.req;  // :226
+                  ++x.rs_h;
+                  --x.rs_n;
+                  o_task = h.task;
+                  o_what = 1u;
+                  const V2Msg m = {now + x.ul, my_seq++, kMsgAck6, h.task};  // puback 6 (:231-235)
+                  if (x.out_n == Q) bad = true;
+                  else {
+                    outq[(x.out_h + x.out_n) & qm] = m;
+                    if (x.out_n == 0u) x.out_hd = m;
+                    ++x.out_n;
+                  }
                 }
               }
-            }
-            // advertiseMIPS (:202-220): advert, then the self-message again 0.01 s later
-            if (kPhantomAdverts && mips == last_sent && earlier(ph_tick, ph_seq, now, e_seq)) {
-              // carries the value of the node's previous advert, which the broker already holds
-              ph_tick = now + ul;
-              ph_seq = my_seq++;
-              ph_cnt += ph_tick < stop ? 1u : 0u;
-            } else {
-              const V2Msg m = {now + ul, my_seq++, kMsgAdvert, mips};
-              last_sent = mips;
-              if (out_n == Q) bad = true;
-              else {
-                outq[(out_h + out_n) & qm] = m;
-                if (out_n == 0u) out_hd = m;
-                ++out_n;
+              // advertiseMIPS (:202-220): advert, then the self-message again 0.01 s later
+              if (kPhantomAdverts && x.mips == x.last_sent && earlier(x.ph_tick, x.ph_seq, now, e_seq)) {
+                // carries the value of the node's previous advert, which the broker already holds
+                x.ph_tick = now + x.ul;
+                x.ph_seq = my_seq++;
+                x.ph_cnt += x.ph_tick < stop ? 1u : 0u;
+              } else {
+                const V2Msg m = {now + x.ul, my_seq++, kMsgAdvert, x.mips};
+                x.last_sent = x.mips;
+                if (x.out_n == Q) bad = true;
+                else {
+                  outq[(x.out_h + x.out_n) & qm] = m;
+                  if (x.out_n == 0u) x.out_hd = m;
+                  ++x.out_n;
+                }
               }
-            }
-            t_sched = true;
-            t_tick = now + kAdvertPeriod;
-            t_seq = my_seq++;
-          } else {
-            // ComputeBrokerApp2::processPacket, FognetMsgTask (:258-318)
-            const int32_t t = in_hd.val;
-            const int32_t req = in_hd.kind;
-            ++in_h;
-            --in_n;
-            if (in_n) in_hd = inq[in_h & qm];
-            o_task = t;
-            if (req < mips) {  // :269
-              mips -= req;     // :272
-              o_what = 2u;
-              if (rs_n == Q) bad = true;
-              else {
-                res[(rs_h + rs_n) & qm] = V2Res{t, req, add_rn(dbl(now), rt)};  // :274
-                ++rs_n;
-              }
-              // cancelEvent + RELEASERESOURCE at now + requiredTime (:292-295)
-              t_kind = kKindRelease;
-              t_sched = true;
-              t_tick = now + rt_ticks;
-              t_seq = my_seq++;
+              x.t_sched = true;
+              x.t_tick = now + kAdvertPeriod;
+              x.t_seq = my_seq++;
             } else {
-              o_what = 3u;  // TaskAck(false) (:299-306)
+              // ComputeBrokerApp2::processPacket, FognetMsgTask (:258-318)
+              const int32_t t = x.in_hd.val;
+              const int32_t req = x.in_hd.kind;
+              ++x.in_h;
+              --x.in_n;
+              if (x.in_n) x.in_hd = P.inq[qrow(s) + (x.in_h & qm)];
+              o_task = t;
+              if (req < x.mips) {  // :269
+                x.mips -= req;     // :272
+                o_what = 2u;
+                if (x.rs_n == Q) bad = true;
+                else {
+                  P.res[qrow(s) + ((x.rs_h + x.rs_n) & qm)] = V2Res{t, req, add_rn(dbl(now), rt)};  // :274
+                  ++x.rs_n;
+                }
+                // cancelEvent + RELEASERESOURCE at now + requiredTime (:292-295)
+                x.t_kind = kKindRelease;
+                x.t_sched = true;
+                x.t_tick = now + rt_ticks;
+                x.t_seq = my_seq++;
+              } else {
+                o_what = 3u;  // TaskAck(false) (:299-306)
+              }
             }
           }
         }
@@ -439,15 +502,20 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
           ++st.n_rejected;
           if (lane == 0) O.status[tbase + o_task] = FOGNET_V2_ST_REJECTED;
         }
-        (void)released;
       }
     }
   }
 
   // ---- unqueued adverts dispatched before the end (an error ends the replication at
   // event end_*: the one still in flight after it is not)
-  if (err != FOGNET_OK && ph_tick < stop && !earlier(ph_tick, ph_seq, end_tick, end_seq)) ph_cnt -= 1u;
-  int64_t ph_sum = (int64_t)ph_cnt;
+  int64_t ph_sum = 0, msum = 0;
+#pragma unroll
+  for (int s = 0; s < NPL; ++s) {
+    V2Node& x = nd[s];
+    if (err != FOGNET_OK && x.ph_tick < stop && !earlier(x.ph_tick, x.ph_seq, end_tick, end_seq)) x.ph_cnt -= 1u;
+    ph_sum += (int64_t)x.ph_cnt;
+    msum += s * kWave + lane < N ? (int64_t)x.mips : 0;
+  }
   for (int m = kWave / 2; m > 0; m >>= 1) ph_sum += (int64_t)shfl_xor_u64((uint64_t)ph_sum, m);
   st.events += ph_sum;
   // ---- tasks not published before the stop (or the error), and the record
@@ -457,7 +525,6 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
     O.start_tick[tbase + t] = -1;
     O.done_tick[tbase + t] = -1;
   }
-  int64_t msum = own ? (int64_t)mips : 0;
   for (int m = kWave / 2; m > 0; m >>= 1) msum += (int64_t)shfl_xor_u64((uint64_t)msum, m);
   if (lane == 0) {
     st.node_mips_final_sum = msum;
@@ -566,7 +633,7 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   const uint32_t Q = 1u << P.q_log2, qm = Q - 1u;
   const size_t nbase = (size_t)rr * (size_t)A.node_stride;
   const size_t tbase = (size_t)rr * (size_t)T;
-  const size_t qbase = ((size_t)rr * (size_t)FOGNET_V2_MAX_NODES + (size_t)li) << P.q_log2;
+  const size_t qbase = ((size_t)rr * (size_t)kWave + (size_t)li) << P.q_log2;
   V2MsgR* const inq = reinterpret_cast<V2MsgR*>(P.inq) + qbase;
   V2MsgR* const outq = reinterpret_cast<V2MsgR*>(P.outq) + qbase;
   V2Res* const res = P.res + qbase;
@@ -1170,8 +1237,14 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
 
 }  // namespace
 
-size_t replay_v2_workspace_bytes(int32_t R, int32_t T, int32_t q_log2) {
-  const size_t q = (size_t)R * FOGNET_V2_MAX_NODES << q_log2;
+// queue rows per replication: 64 * the kernel's nodes per lane (the rows kernels use the first 64)
+static size_t v2_rows(int32_t N) {
+  const size_t npl = N <= kWave ? 1 : (size_t)1 << (32 - __builtin_clz((unsigned)((N + kWave - 1) / kWave - 1)));
+  return npl * kWave;
+}
+
+size_t replay_v2_workspace_bytes(int32_t R, int32_t T, int32_t N, int32_t q_log2) {
+  const size_t q = (size_t)R * v2_rows(N) << q_log2;
   return q * (2 * sizeof(V2Msg) + sizeof(V2Res)) + (size_t)R * (size_t)T;
 }
 
@@ -1182,7 +1255,7 @@ hipError_t launch_replay_v2(const fognet_v2_in& in, const fognet_v2_out& out, vo
   a.in = in;
   a.out = out;
   a.q_log2 = q_log2;
-  const size_t q = (size_t)in.R * FOGNET_V2_MAX_NODES << q_log2;
+  const size_t q = (size_t)in.R * v2_rows(in.N) << q_log2;
   a.inq = reinterpret_cast<V2Msg*>(ws);
   a.outq = a.inq + q;
   a.res = reinterpret_cast<V2Res*>(a.outq + q);
@@ -1194,8 +1267,16 @@ hipError_t launch_replay_v2(const fognet_v2_in& in, const fognet_v2_out& out, vo
     hipLaunchKernelGGL(replay_v2_rows_kernel<16>, dim3((in.R + 3) / 4), dim3(kWave), 0, s, a);
   else if (in.N <= 32)
     hipLaunchKernelGGL(replay_v2_rows_kernel<32>, dim3((in.R + 1) / 2), dim3(kWave), 0, s, a);
+  else if (in.N <= 64)
+    hipLaunchKernelGGL(replay_v2_kernel<1>, dim3(in.R), dim3(kWave), 0, s, a);
+  else if (in.N <= 128)
+    hipLaunchKernelGGL(replay_v2_kernel<2>, dim3(in.R), dim3(kWave), 0, s, a);
+  else if (in.N <= 256)
+    hipLaunchKernelGGL(replay_v2_kernel<4>, dim3(in.R), dim3(kWave), 0, s, a);
+  else if (in.N <= 512)
+    hipLaunchKernelGGL(replay_v2_kernel<8>, dim3(in.R), dim3(kWave), 0, s, a);
   else
-    hipLaunchKernelGGL(replay_v2_kernel, dim3(in.R), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL(replay_v2_kernel<16>, dim3(in.R), dim3(kWave), 0, s, a);
   return hipGetLastError();
 }
 

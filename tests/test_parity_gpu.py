@@ -1113,14 +1113,31 @@ def v2_random(seed, R, N, T):
 
 
 @pytest.mark.parametrize("seed,N,R", [(0, 1, 16), (1, 2, 16), (2, 5, 16), (3, 13, 16), (4, 64, 16), (5, 5, 16),
-                                      (6, 16, 7), (7, 17, 5), (8, 3, 1), (9, 5, 13)])
+                                      (6, 16, 7), (7, 17, 5), (8, 3, 1), (9, 5, 13), (10, 65, 5), (11, 200, 4),
+                                      (12, 129, 3), (13, 300, 2), (14, 1024, 2)])
 def test_v2_random_matches_oracle(ctx, seed, N, R):
-    """N <= 16: replay_v2_rows_kernel (four replications per wavefront, R not a
-    multiple of four included); N > 16: replay_v2_kernel."""
-    tr, broker, stop, rt = v2_random(seed, R, N, 3000)
+    """N <= 16: replay_v2_rows_kernel<16> (four replications per wavefront, R not
+    a multiple of four included); 17 <= N <= 32: replay_v2_rows_kernel<32> (two);
+    N > 32: replay_v2_kernel<NPL> with node j on lane j % 64, slot j / 64 (NPL = 1,
+    2, 4, 8, 16: N <= 1024; the reference's loop takes any brokers.size(),
+    BrokerBaseApp2.cc:241-248)."""
+    tr, broker, stop, rt = v2_random(seed, R, N, 3000 if N <= 256 else 1500)
     g = run_v2_gpu(ctx, tr, broker, stop, rt, qcap=4096)
     o = ol.run_v2(tr["arrive"], tr["req"], broker, tr["mips"], tr["dl"], tr["ul"], tr["first_adv"], stop, rt,
                   threads=8)
+    assert (o["stats"]["status"] == 0).all()
+    assert_v2_parity(g, o)
+
+
+@pytest.mark.parametrize("N", [5, 16])
+def test_v2_two_rows_per_wave_at_small_n(ctx, monkeypatch, N):
+    """FOGNET_V2_ROW=32 forces replay_v2_rows_kernel<32> (two replications per
+    wavefront) where N <= 16 would take the four-row kernel: same outputs."""
+    monkeypatch.setenv("FOGNET_V2_ROW", "32")
+    tr, broker, stop, rt = v2_random(40 + N, 7, N, 3000)
+    g = run_v2_gpu(ctx, tr, broker, stop, rt, qcap=4096)
+    o = ol.run_v2(tr["arrive"], tr["req"], broker, tr["mips"], tr["dl"], tr["ul"], tr["first_adv"], stop, rt,
+                  threads=7)
     assert (o["stats"]["status"] == 0).all()
     assert_v2_parity(g, o)
 
