@@ -3,7 +3,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 SRC_DIR := fognetsimpp_amd/csrc
-SRCS := $(SRC_DIR)/capi.hip $(SRC_DIR)/replay.hip $(SRC_DIR)/replay_wide.hip $(SRC_DIR)/replay_v2.hip $(SRC_DIR)/decide.hip $(SRC_DIR)/tracegen.hip $(SRC_DIR)/user_stats.hip
+SRCS := $(SRC_DIR)/capi.hip $(SRC_DIR)/replay.hip $(SRC_DIR)/replay_wide.hip $(SRC_DIR)/replay_v2.hip $(SRC_DIR)/replay_region.hip $(SRC_DIR)/decide.hip $(SRC_DIR)/tracegen.hip $(SRC_DIR)/user_stats.hip
 HDRS := include/fognet_hip.h include/fognet_io.h $(SRC_DIR)/internal.h $(SRC_DIR)/replay_common.h
 OBJDIR := build/obj
 OBJS := $(patsubst $(SRC_DIR)/%.hip,$(OBJDIR)/%.o,$(SRCS)) $(OBJDIR)/io.o

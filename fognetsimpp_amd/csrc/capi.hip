@@ -159,6 +159,19 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a, boo
 // are identical (the parity tests run both).  Not the default: at C3 (4,096
 // replications, all resident at 4 waves/SIMD) it measured 20.9 ms/launch
 // against 14.1 ms, the fourth wave per SIMD being worth more than the re-read.
+// FOGNET_HIER_REGIONS=0: EXT_HIER replays run on the sequential wide kernel
+// only; =only: the region pass without the sequential hand-over (a replication
+// it cannot finish keeps an internal status) -- the parity tests use both to
+// check that each path ran.
+bool use_regions() {
+  const char* f = getenv("FOGNET_HIER_REGIONS");
+  return f == nullptr || strcmp(f, "0") != 0;
+}
+bool regions_only() {
+  const char* f = getenv("FOGNET_HIER_REGIONS");
+  return f != nullptr && strcmp(f, "only") == 0;
+}
+
 bool use_inloop() {
   const char* f = getenv("FOGNET_REPLAY_STATS");
   return f != nullptr && strcmp(f, "inloop") == 0;
@@ -418,6 +431,36 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     // statistics-only stage has nothing left to do
     if (!(which & 1)) return FOGNET_OK;
     a.no_task_out = stats_only ? 1 : 0;
+    const int32_t B = (a.N + FOGNET_HIER_REGION_NODES - 1) / FOGNET_HIER_REGION_NODES;
+    if (a.policy == FOGNET_POLICY_EXT_HIER && !a.down && !stats_only && a.T > 0 && B >= 2 && use_regions()) {
+      // one wavefront per (replication, region) while no region escalates (replay_region.hip), the
+      // statistics pass, then the sequential wide kernel for the replications some region handed back.
+      // workspace: [hand-over counter | list [R] | region records [R][B] | entries [R][T] | node records
+      // [R][N]]; the hand-over launch reuses the space from the entries on (stream order: after the
+      // statistics pass has read the node records)
+      const size_t o_rec = align256(256 + (size_t)a.R * sizeof(int32_t));
+      const size_t o_e = o_rec + align256((size_t)a.R * (size_t)B * sizeof(fognet::RegionRec));
+      const size_t o_nd = o_e + align256((size_t)a.R * (size_t)a.T * sizeof(fognet::WideEntry));
+      const size_t body = o_nd - o_e + (size_t)a.R * (size_t)a.N * sizeof(fognet::WideNode);
+      const int32_t slots = fallback_slots(a.R, a.T, a.N, body, false);
+      const size_t fb = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
+      rc = ensure(c, (void**)&c->ring, &c->ring_bytes, o_e + (body > fb ? body : fb), "region replay workspace");
+      if (rc) return rc;
+      unsigned char* const base = reinterpret_cast<unsigned char*>(c->ring);
+      a.wide_count = reinterpret_cast<int32_t*>(base);
+      a.wide_list = reinterpret_cast<int32_t*>(base + 256);
+      e = hipMemsetAsync(a.wide_count, 0, sizeof(int32_t), (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(c, e, "hand-over counter");
+      const fognet::RegionWs w{reinterpret_cast<fognet::WideEntry*>(base + o_e),
+                               reinterpret_cast<fognet::WideNode*>(base + o_nd),
+                               reinterpret_cast<fognet::RegionRec*>(base + o_rec), B};
+      if (regions_only()) a.wide_list = nullptr;
+      e = fognet::launch_replay_region(a, w, (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(c, e, "region replay launch");
+      if (regions_only()) return FOGNET_OK;
+      e = fognet::launch_replay_wide(a, base + o_e, slots, (hipStream_t)stream);
+      return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "wide hand-over launch");
+    }
     const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N);
     rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ws, "wide replay workspace");
     if (rc) return rc;

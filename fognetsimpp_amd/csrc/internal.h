@@ -328,6 +328,21 @@ size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen = f
 // listed replications in turn (slots <= R bounds the workspace).
 hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slots, hipStream_t s);
 
+// FOGNET_POLICY_EXT_HIER by region (replay_region.hip): one wavefront per
+// (replication, region) over the region's publishes while no escalation occurs;
+// then per replication the regions' records merged and the statistics pass, or
+// the replication appended to a.wide_list for the sequential wide kernel.
+struct RegionRec {
+  int32_t n_done, max_pend, status, pad;
+};
+struct RegionWs {
+  WideEntry* e;    // [R][T]
+  WideNode* nd;    // [R][N]
+  RegionRec* rec;  // [R][B]
+  int32_t B;       // regions: ceil(N / FOGNET_HIER_REGION_NODES)
+};
+hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s);
+
 hipError_t launch_replay(const ReplayArgs& a, hipStream_t s);
 hipError_t launch_rep_stats(const ReplayArgs& a, hipStream_t s);
 // Job reduction: one block up to kReduceChunk records, else blocks of

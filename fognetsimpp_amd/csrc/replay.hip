@@ -577,67 +577,6 @@ __device__ __forceinline__ int64_t scan_max_level(int64_t v, int64_t& tmp) {
   return tmp > v ? tmp : v;
 }
 
-// ---------------------------------------------------------------- statistics
-// The statistics pass over the replay outputs (Acc: replay_common.h).
-
-// Accumulate tasks i = i0, i0 + stride, ... < n of one replication into `a`
-// (plus the per-node service seconds s_busy and the histogram s_hist in LDS
-// when those statistics are on).  The loads of UNROLL tasks are issued
-// before any is used.  dl_of(k): node k's downlink latency.
-// kPerTask = false: busy seconds, per-node service and `last` are not
-// accumulated per task (the fused epilogue takes them from the node tails).
-// ab_tick/ab_task (LDS, one slot per thread, indexed by i0): the abort point
-// (replay_common.h AbortPt) is kept there, a read-modify-write only on an
-// overflow, which is rare, instead of in registers (the fused epilogue has
-// none to spare).
-template <int UNROLL, bool kPerTask = true, class DlOf>
-__device__ __forceinline__ void stats_accumulate(const ReplayArgs& A, size_t tbase, int n, int i0, int stride, Acc& a,
-                                                 unsigned long long* s_busy, uint32_t* s_hist, DlOf dl_of,
-                                                 int64_t* ab_tick, int32_t* ab_task) {
-  const bool energy = kPerTask && A.p_busy != nullptr;
-  const bool hist = A.hist != nullptr;
-  for (int ib = i0; ib < n; ib += stride * UNROLL) {
-    int64_t t[UNROLL], st0[UNROLL], dn[UNROLL];
-    int32_t kk[UNROLL];
-    uint32_t stt[UNROLL];
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int i = ib + u * stride;
-      const size_t o = tbase + (size_t)(i < n ? i : ib);  // past the end: reload task ib (in bounds, unused)
-      t[u] = A.arrive[o];
-      kk[u] = A.out_node[o];
-      stt[u] = A.out_status[o];
-      st0[u] = A.out_start[o];
-      dn[u] = A.out_done[o];
-    }
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      if (ib + u * stride < n) {
-        const int32_t k = kk[u];
-        const int64_t resp = dn[u] - t[u];
-        if constexpr (kPerTask) {
-          const uint64_t svc = (uint64_t)(dn[u] - st0[u]) / (uint64_t)kTicksPerSecond;  // whole seconds
-          a.busy += svc;
-          if (energy) atomicAdd(&s_busy[k], (unsigned long long)svc);
-          a.last = max(a.last, dn[u]);
-        }
-        add_moment(a.rs_lo, a.rs_hi, a.rq_lo, a.rq_hi, (uint64_t)resp);
-        a.rmin = min(a.rmin, resp);
-        a.rmax = max(a.rmax, resp);
-        if (hist) atomicAdd(&s_hist[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
-        if (stt[u] == 4u) {  // queueTime emission (ComputeBrokerApp3.cc:238), enqueued at its arrival
-          a.n4 += 1u;
-          if (!acc_qtime(a.qs_lo, a.qs_hi, a.qq_lo, a.qq_hi, a.qq_top, a.qmin, a.qmax, a.nqt, a.nqo, st0[u],
-                         t[u] + dl_of(k), hist ? s_hist : nullptr))
-            abort_min(ab_tick[i0], ab_task[i0], st0[u], ib + u * stride);
-        } else {
-          a.n5 += 1u;
-        }
-      }
-    }
-  }
-}
-
 // Builder-defined statistics of the north star, after the accumulation (and a
 // barrier): histogram counts added into the job histogram, and node energy
 // E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12) with IEEE-rounded

@@ -386,4 +386,133 @@ __device__ __forceinline__ void write_rep_stats(fognet_rep_stats* S, const Acc& 
   S->n_qtime_overflow = (int64_t)b.nqo;
 }
 
+// ---------------------------------------------------------------- statistics pass
+// The statistics pass over the replay outputs (replay.hip's fused epilogue and
+// rep_stats_kernel, replay_region.hip's finish kernel).
+
+// Accumulate tasks i = i0, i0 + stride, ... < n of one replication into `a`
+// (plus the per-node service seconds s_busy and the histogram s_hist in LDS
+// when those statistics are on).  The loads of UNROLL tasks are issued
+// before any is used.  dl_of(k): node k's downlink latency.
+// kPerTask = false: busy seconds, per-node service and `last` are not
+// accumulated per task (the fused epilogue takes them from the node tails).
+// ab_tick/ab_task (LDS, one slot per thread, indexed by i0): the abort point
+// (replay_common.h AbortPt) is kept there, a read-modify-write only on an
+// overflow, which is rare, instead of in registers (the fused epilogue has
+// none to spare).
+template <int UNROLL, bool kPerTask = true, class DlOf>
+__device__ __forceinline__ void stats_accumulate(const ReplayArgs& A, size_t tbase, int n, int i0, int stride, Acc& a,
+                                                 unsigned long long* s_busy, uint32_t* s_hist, DlOf dl_of,
+                                                 int64_t* ab_tick, int32_t* ab_task) {
+  const bool energy = kPerTask && A.p_busy != nullptr;
+  const bool hist = A.hist != nullptr;
+  for (int ib = i0; ib < n; ib += stride * UNROLL) {
+    int64_t t[UNROLL], st0[UNROLL], dn[UNROLL];
+    int32_t kk[UNROLL];
+    uint32_t stt[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int i = ib + u * stride;
+      const size_t o = tbase + (size_t)(i < n ? i : ib);  // past the end: reload task ib (in bounds, unused)
+      t[u] = A.arrive[o];
+      kk[u] = A.out_node[o];
+      stt[u] = A.out_status[o];
+      st0[u] = A.out_start[o];
+      dn[u] = A.out_done[o];
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (ib + u * stride < n) {
+        const int32_t k = kk[u];
+        const int64_t resp = dn[u] - t[u];
+        if constexpr (kPerTask) {
+          const uint64_t svc = (uint64_t)(dn[u] - st0[u]) / (uint64_t)kTicksPerSecond;  // whole seconds
+          a.busy += svc;
+          if (energy) atomicAdd(&s_busy[k], (unsigned long long)svc);
+          a.last = max(a.last, dn[u]);
+        }
+        add_moment(a.rs_lo, a.rs_hi, a.rq_lo, a.rq_hi, (uint64_t)resp);
+        a.rmin = min(a.rmin, resp);
+        a.rmax = max(a.rmax, resp);
+        if (hist) atomicAdd(&s_hist[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
+        if (stt[u] == 4u) {  // queueTime emission (ComputeBrokerApp3.cc:238), enqueued at its arrival
+          a.n4 += 1u;
+          if (!acc_qtime(a.qs_lo, a.qs_hi, a.qq_lo, a.qq_hi, a.qq_top, a.qmin, a.qmax, a.nqt, a.nqo, st0[u],
+                         t[u] + dl_of(k), hist ? s_hist : nullptr))
+            abort_min(ab_tick[i0], ab_task[i0], st0[u], ib + u * stride);
+        } else {
+          a.n5 += 1u;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- wide-record advert
+// (replay_wide.hip, replay_region.hip) Saturated advertised busy time in the
+// 32-bit view of the wide kernels.
+constexpr uint32_t kViewBusySat = 0xFFFFFFFFu;
+
+// The advert of node j's head completion reaches the broker (owner lane):
+// the view takes busyTime after releaseResource (ComputeBrokerApp3.cc:232,
+// :254) = the service of the tasks that reached j before that completion and
+// are not done yet, a difference of cumulative sums; the head advances.
+// Returns false when the advertised busy time is 2^24 s or more (only the
+// EXT_LAT cost cares: its uint64 tick arithmetic needs busy < 2^24).
+// h: node j's record (loaded from HBM or the lane's cached copy), updated in place.
+// up: FOGNET_POLICY_EXT_HIER's extra hop, which an escalated task (entry pad
+// != 0, bit 31 of the record's tl_S for the tail) took before its downlink:
+// the same-tick rule compares the arrival's own insertion tick.
+// broken: the chain invariant failed (see below; a library bug, never an input).
+__device__ __forceinline__ bool apply_wide_advert(WideNode& h, const WideEntry* e, int64_t dl, int64_t ul, int64_t up,
+                                             int64_t& nxt_j, uint32_t& busy_j, bool& broken) {
+  // the entry after the head, loaded first: for the lane's cached node h is in
+  // registers, so this load issues together with the group's view loads
+  WideEntry nx{};
+  if (h.npend >= 2) {
+    nx = e[h.hd_next];
+    // Chain invariant, checked at every applied advert: with two or more tasks
+    // pending, the record's hd_next names the entry whose prev is the head and
+    // whose cumulative service is the head's plus its own.  hd_next changes on
+    // three paths -- this advert, a push onto a node with exactly one pending
+    // task (hd_next := the pushed task) and a multi-task run onto an idle node
+    // (hd_next := its second task) -- so any copy of it elsewhere (the round-2
+    // experiment kept one in the HBM view, refreshed only where the view is
+    // written: here and on a push onto an idle node) goes stale on the second
+    // path, and the next advert then advances the head to a wrong entry.
+    broken = nx.prev != h.hd || nx.C != h.hd_C + nx.S;
+  }
+  uint64_t c_arrived = h.hd_C;  // only the completing task itself ...
+  if (arrives_before(h.tl_a, h.hd_done, dl + ((h.tl_S >> 31) ? up : 0), h.hd_S)) {
+    c_arrived = h.tl_C;  // ... or everything up to the newest task (the common case)
+  } else {
+    for (int32_t x = e[h.tl].prev; x != h.hd;) {  // newest first
+      const WideEntry ex = e[x];
+      if (arrives_before(ex.a, h.hd_done, dl + (ex.pad ? up : 0), h.hd_S)) {
+        c_arrived = ex.C;
+        break;
+      }
+      x = ex.prev;
+    }
+  }
+  const uint64_t busy = c_arrived - h.hd_C;
+  // the view keeps 32 bits, saturated: a saturated node can only be chosen when the
+  // decision's minimum itself is saturated, which the decision refuses (kViewBusySat)
+  busy_j = busy < (uint64_t)kViewBusySat ? (uint32_t)busy : kViewBusySat;
+  h.npend -= 1;
+  if (h.npend == 0) {
+    nxt_j = kNever;
+  } else {
+    // FIFO: the next task started at max(arrival, this completion); its
+    // done tick was fixed when it was pushed
+    h.hd = h.hd_next;
+    h.hd_done = nx.done;
+    h.hd_C = nx.C;
+    h.hd_S = nx.S;
+    h.hd_next = nx.next;  // valid while npend >= 2
+    nxt_j = nx.done == kNever ? kNever : nx.done + ul;  // never: crashed before it completes
+  }
+  return busy < ((uint64_t)1 << 24);  // FOGNET_POLICY_EXT_LAT's cost needs busy < 2^24
+}
+
 }  // namespace fognet

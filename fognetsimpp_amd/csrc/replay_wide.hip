@@ -56,7 +56,7 @@ namespace {
 constexpr uint32_t kWideSCap = 1u << 22;
 // Saturated advertised busy time in the 32-bit view (also the busy value of the
 // view's slots past N, which never win: their index is larger).
-constexpr uint32_t kBusySat = 0xFFFFFFFFu;
+constexpr uint32_t kBusySat = kViewBusySat;
 // A start or completion tick at or past base + 2^22 s (beyond kMaxTick).
 constexpr int64_t kPastRange = kMaxTick + 1;
 
@@ -254,68 +254,6 @@ __device__ __forceinline__ int64_t group_min_w(int g, int sl, int64_t sl_w, cons
   return mn;
 }
 
-
-// The advert of node j's head completion reaches the broker (owner lane):
-// the view takes busyTime after releaseResource (ComputeBrokerApp3.cc:232,
-// :254) = the service of the tasks that reached j before that completion and
-// are not done yet, a difference of cumulative sums; the head advances.
-// Returns false when the advertised busy time is 2^24 s or more (only the
-// EXT_LAT cost cares: its uint64 tick arithmetic needs busy < 2^24).
-// h: node j's record (loaded from HBM or the lane's cached copy), updated in place.
-// up: FOGNET_POLICY_EXT_HIER's extra hop, which an escalated task (entry pad
-// != 0, bit 31 of the record's tl_S for the tail) took before its downlink:
-// the same-tick rule compares the arrival's own insertion tick.
-// broken: the chain invariant failed (see below; a library bug, never an input).
-__device__ __forceinline__ bool apply_advert(WideNode& h, const WideEntry* e, int64_t dl, int64_t ul, int64_t up,
-                                             int64_t& nxt_j, uint32_t& busy_j, bool& broken) {
-  // the entry after the head, loaded first: for the lane's cached node h is in
-  // registers, so this load issues together with the group's view loads
-  WideEntry nx{};
-  if (h.npend >= 2) {
-    nx = e[h.hd_next];
-    // Chain invariant, checked at every applied advert: with two or more tasks
-    // pending, the record's hd_next names the entry whose prev is the head and
-    // whose cumulative service is the head's plus its own.  hd_next changes on
-    // three paths -- this advert, a push onto a node with exactly one pending
-    // task (hd_next := the pushed task) and a multi-task run onto an idle node
-    // (hd_next := its second task) -- so any copy of it elsewhere (the round-2
-    // experiment kept one in the HBM view, refreshed only where the view is
-    // written: here and on a push onto an idle node) goes stale on the second
-    // path, and the next advert then advances the head to a wrong entry.
-    broken = nx.prev != h.hd || nx.C != h.hd_C + nx.S;
-  }
-  uint64_t c_arrived = h.hd_C;  // only the completing task itself ...
-  if (arrives_before(h.tl_a, h.hd_done, dl + ((h.tl_S >> 31) ? up : 0), h.hd_S)) {
-    c_arrived = h.tl_C;  // ... or everything up to the newest task (the common case)
-  } else {
-    for (int32_t x = e[h.tl].prev; x != h.hd;) {  // newest first
-      const WideEntry ex = e[x];
-      if (arrives_before(ex.a, h.hd_done, dl + (ex.pad ? up : 0), h.hd_S)) {
-        c_arrived = ex.C;
-        break;
-      }
-      x = ex.prev;
-    }
-  }
-  const uint64_t busy = c_arrived - h.hd_C;
-  // the view keeps 32 bits, saturated: a saturated node can only be chosen when the
-  // decision's minimum itself is saturated, which the decision refuses (kBusySat)
-  busy_j = busy < (uint64_t)kBusySat ? (uint32_t)busy : kBusySat;
-  h.npend -= 1;
-  if (h.npend == 0) {
-    nxt_j = kNever;
-  } else {
-    // FIFO: the next task started at max(arrival, this completion); its
-    // done tick was fixed when it was pushed
-    h.hd = h.hd_next;
-    h.hd_done = nx.done;
-    h.hd_C = nx.C;
-    h.hd_S = nx.S;
-    h.hd_next = nx.next;  // valid while npend >= 2
-    nxt_j = nx.done == kNever ? kNever : nx.done + ul;  // never: crashed before it completes
-  }
-  return busy < ((uint64_t)1 << 24);  // FOGNET_POLICY_EXT_LAT's cost needs busy < 2^24
-}
 
 // Workspace layout (launch_replay_wide, replay_wide_workspace_bytes).
 struct WideWs {
@@ -797,7 +735,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           const int64_t dl_j = hit ? c_dl : P_dl[j];
           bool broken = false;
           const int64_t ul_j = hit ? c_ul : P_ul[j];
-          bool fits = apply_advert(h, e, dl_j, ul_j, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
+          bool fits = apply_wide_advert(h, e, dl_j, ul_j, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
           // node j's later adverts that are due too: adverts of different nodes commute (each
           // sets only its node's view), so j's are applied now, in their order, and only the
           // last one's view is stored and rescanned (no store between the dependent entry loads)
@@ -805,7 +743,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 #ifdef FOGNET_WIDE_PROF
             ++pf_same;
 #endif
-            fits &= apply_advert(h, e, dl_j, ul_j, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
+            fits &= apply_wide_advert(h, e, dl_j, ul_j, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
           }
           if constexpr (kExt) lerr |= !fits;
           lbroken |= broken;

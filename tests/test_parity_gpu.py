@@ -1364,6 +1364,47 @@ def test_hier_matches_oracle(ctx, kind):
     np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
 
 
+def test_hier_region_pass_and_handover(ctx, monkeypatch):
+    """EXT_HIER by region (replay_region.hip: one wavefront per regional broker
+    while no region escalates) with the sequential hand-over: of six
+    replications five never escalate (two regions, one of 6 nodes) and one does
+    (297 escalated publishes in the oracle).  FOGNET_HIER_REGIONS=only shows the
+    region pass finishing exactly the five; the default (region pass + hand-over
+    of the sixth) and FOGNET_HIER_REGIONS=0 (sequential only) both equal the
+    oracle, records and job histogram included."""
+    tr = tg.make_batch(21, 6, 1030, 4000, rho=0.9)
+    reg = np.zeros_like(tr["req"])
+    reg[1::2, 1::2] = 1
+    reg[0, 5::7] = 1
+    tr = dict(tr, region=reg)
+    kw = dict(policy="EXT_HIER", hier_threshold_s=0, hier_up_tick=10**12, hist=True)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=6, hist=True,
+                     policy=ol.POLICY_EXT_HIER, region=reg, hier_threshold_s=0, hier_up_tick=10**12)
+    esc = (o["node"] // _abi.HIER_REGION_NODES != reg).sum(axis=1)
+    assert list(esc > 0) == [False] * 5 + [True]
+    dev = torch.device("cuda", ctx.device)
+    d = fa.as_device_trace(tr, dev)
+    monkeypatch.setenv("FOGNET_HIER_REGIONS", "only")
+    out = fa.run_batch(ctx, d, **kw)
+    torch.cuda.synchronize()
+    st = out.rep_stats()
+    assert list(st["status"][:5]) == [0] * 5 and st["status"][5] not in (0, _abi.FOGNET_ERR_ARG)
+    for k, gk in (("node", out.node), ("status", out.status), ("start", out.start_tick), ("done", out.done_tick)):
+        np.testing.assert_array_equal(gk.cpu().numpy()[:5], o[k][:5], err_msg=k)
+    assert st[:5].tobytes() == o["stats"][:5].tobytes()
+    np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"][:5].sum(axis=0))
+    for mode in ("1", "0"):
+        monkeypatch.setenv("FOGNET_HIER_REGIONS", mode)
+        out = fa.run_batch(ctx, d, **kw)
+        torch.cuda.synchronize()
+        g = dict(node=out.node.cpu().numpy(), status=out.status.cpu().numpy(), start=out.start_tick.cpu().numpy(),
+                 done=out.done_tick.cpu().numpy(), stats=out.rep_stats())
+        assert (g["stats"]["status"] == 0).all()
+        assert_parity(tr, g, o)
+        assert out.rep_stats().tobytes() == o["stats"].tobytes()
+        np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
+
+
 @pytest.mark.parametrize("thr,up_s", [(0, 1), (3, 2), (0, 40), (2, 300)])
 def test_hier_overtaken_escalation_matches_oracle(ctx, thr, up_s):
     """EXT_HIER: publishes alternating between a saturated 6-node region and a
@@ -1437,7 +1478,8 @@ def test_hier_pending_escalations_spill_to_hbm(ctx, up_s):
     np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
 
 
-def test_c5_ext_hier_as_named(ctx):
+@pytest.mark.parametrize("mode", ["only", "0"])
+def test_c5_ext_hier_as_named(ctx, monkeypatch, mode):
     """Config C5 as BASELINE.json configs[4] names it, in the bench's settings:
     N = 10,000 fog nodes in 10 regional brokers (every rotated-lane row of the
     wide kernel), fa.mobility_regions handoffs, T = 10,000 device-generated
@@ -1448,7 +1490,10 @@ def test_c5_ext_hier_as_named(ctx):
     advertises only after a completion, and the stale view herds a region's
     publishes onto one node until that node's first advert, so ~1,000 publishes
     per region touch a few dozen nodes; escalations, overtaking and the overflow
-    list are covered at smaller regions (test_hier_*)."""
+    list are covered at smaller regions (test_hier_*).  mode "only": the region
+    pass alone (one wavefront per regional broker, replay_region.hip, no
+    sequential hand-over); "0": the sequential wide kernel alone."""
+    monkeypatch.setenv("FOGNET_HIER_REGIONS", mode)
     R, T, N = 4, 10_000, 10_000
     mg, sc = fa.c5_params(np.arange(R), N)
     d = fa.generate_trace(ctx, 0x5EED0005, R, T, N, mg, sc)
