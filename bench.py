@@ -245,9 +245,9 @@ def main():
                     pj.get("policy", "REF_V3" if args.workload == "c3" else "EXT_HIER") == args.policy:
                 traffic = pj.get("replay_hbm_bytes_per_launch") or pj.get("hbm_bytes_per_launch")
                 if pj.get("valu_busy") is not None:
-                    # the resource the replay is bound by (SQ_ACTIVE_INST_VALU x 4 cycles / SIMD / active
-                    # cycles): the issue-side roofline beside the byte-count one
-                    valu = {"busy": pj["valu_busy"], "peak": 1.0, "unit": "VALU busy fraction",
+                    # the issue-side figure beside the byte-count roofline: VALU pipe occupancy on gfx950
+                    # (SQ_INSTS_VALU x 2 cycles / SIMD / active cycles, tools/pmc_summary.py)
+                    valu = {"busy": pj["valu_busy"], "peak": 1.0, "unit": "VALU pipe busy fraction",
                             "valu_per_decision": pj.get("SQ_INSTS_VALU_per_decision"),
                             "salu_per_decision": pj.get("SQ_INSTS_SALU_per_decision"),
                             "hbm_bytes_per_decision": (traffic / (R * T) if traffic else None),
@@ -439,9 +439,9 @@ def bench_c4(args, ctx, dev, dist, world, rank):
                          "kernel": "replay_gen_kernel (trace generated per 64-publish chunk, statistics in "
                                    "registers, no per-task stores)",
                          "kernel_ms_per_step": replay_ms,
-                         "note": "SURVEY.md §8(d): C4 has no per-task HBM traffic, so VALU utilisation "
-                                 "(PMC: SQ_ACTIVE_INST_VALU*4/SIMDs/GRBM_GUI_ACTIVE per XCD, "
-                                 "profiles/pmc_valu_c4.json) replaces the HBM fraction"},
+                         "note": "SURVEY.md §8(d): C4 has no per-task HBM traffic, so VALU pipe occupancy "
+                                 "(PMC: SQ_INSTS_VALU*2/SIMDs/GRBM_GUI_ACTIVE per XCD, gfx950's 2-cycle "
+                                 "wave64 issue; profiles/pmc_valu_c4.json) replaces the HBM fraction"},
             "cpu_baseline": cpu,
             "failed_replications": summary["failed"],
             "reference_abort": {"ref_aborted_replications": summary["ref_aborted"], "replications": args.R_total,
