@@ -1206,8 +1206,9 @@ def test_v2_errors(ctx):
               first_adv=np.zeros(0, np.int64))
     g = run_v2_gpu(ctx, tr, 100, 100 * MS)
     assert int(g["stats"]["status"][0]) == _abi.FOGNET_ERR_STATE
-    big = dict(arrive=np.array([[10 * MS]]), req=np.array([[1]], np.int32), mips=np.full(65, 1000, np.int32),
-               dl=np.ones(65, np.int64), ul=np.ones(65, np.int64), first_adv=np.ones(65, np.int64))
+    n = _abi.V2_MAX_NODES + 1  # (16 nodes per lane)
+    big = dict(arrive=np.array([[10 * MS]]), req=np.array([[1]], np.int32), mips=np.full(n, 1000, np.int32),
+               dl=np.ones(n, np.int64), ul=np.ones(n, np.int64), first_adv=np.ones(n, np.int64))
     with pytest.raises(fa.FognetError) as e:
         run_v2_gpu(ctx, big, 100, 100 * MS)
     assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED

@@ -25,3 +25,11 @@ for pol in ${C5POL:-REF_V3 EXT_HIER}; do
   done
 done
 step done
+if [ "${HN:-1}" = 1 ]; then
+  # round-3 hd_next experiment: the first code shape (A) against the hoisted one (B)
+  for v in A B; do
+    step hn_$v
+    FOGNET_LIB=build/hn/$v/out/libfognet_hip.so timeout -k 10 120 python tools/dbg_hier.py > $O/hn_$v.log 2>&1 || { tail $O/hn_$v.log; exit 1; }
+    cat $O/hn_$v.log
+  done
+fi
