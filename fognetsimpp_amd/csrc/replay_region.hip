@@ -216,6 +216,9 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
       if (lane == kl) {
         e[i] = WideEntry{a, done, C, S, tl, -1, 0};
         WideNode h = ch;
+        // (no three-way branch on npend: that shape, with a store in the middle arm, was
+        // miscompiled on gfx950 -- DESIGN.md §3.6 "The hd_next miscompile"; hd_next is set
+        // after the two-way branch instead)
         if (h.npend == 0) {  // the task is the node's head: its advert is the node's next one
           h.hd = i;
           h.hd_done = done;
@@ -228,11 +231,10 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
             mn = x;
             ms = sk;
           }
-        } else if (h.npend == 1) {
-          h.hd_next = i;
-        } else {
+        } else if (h.npend >= 2) {
           e[h.tl].next = i;
         }
+        if (h.npend == 1) h.hd_next = i;  // the tail is the head
         h.tl = i;
         h.tl_a = a;
         h.tl_done = done;

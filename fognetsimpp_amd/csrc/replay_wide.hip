@@ -550,11 +550,10 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           mn = x;
           mj = (int)kk;
         }
-      } else if (h.npend == 1) {
-        h.hd_next = i;
-      } else {
+      } else if (h.npend >= 2) {
         e[h.tl].next = i;
       }
+      if (h.npend == 1) h.hd_next = i;  // the tail is the head (hoisted: DESIGN.md §3.6 "The hd_next miscompile")
       h.tl = i;
       h.tl_a = a;
       h.tl_done = done;
@@ -1039,12 +1038,13 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
             mn = x;
             mj = (int)k;
           }
-          if (Lr > 1) h.hd_next = i0 + 1;
-        } else if (h.npend == 1) {
-          h.hd_next = i0;  // the tail is the head
-        } else {
+        } else if (h.npend >= 2) {
           e[h.tl].next = i0;
         }
+        // hd_next after the two-way branch, not in a third arm (DESIGN.md §3.6 "The hd_next
+        // miscompile"): the run's second task on an idle node, its first on a node whose one
+        // pending task is the tail
+        if (h.npend == 1 || (h.npend == 0 && Lr > 1)) h.hd_next = h.npend == 1 ? i0 : i0 + 1;
         h.tl = iz;
         h.tl_a = a_z;
         h.tl_done = done_z;
