@@ -77,10 +77,11 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
   int64_t mn = kNever;
   int ms = 0;
   uint64_t mk = lane < nb ? (uint64_t)(uint32_t)(base + lane) : ~0ull;
+  // (partially unrolled: a full unroll issues all 16 LDS loads at once and holds 32 VGPRs)
   auto rescan_nxt = [&]() {
     mn = kNever;
     ms = 0;
-#pragma unroll
+#pragma unroll 4
     for (int s = 0; s < kRegionSlots; ++s) {
       const int64_t x = vnxt[s * kWave];
       if (x < mn) {
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
   };
   auto rescan_key = [&]() {
     mk = ~0ull;
-#pragma unroll
+#pragma unroll 4
     for (int s = 0; s < kRegionSlots; ++s) {
       const uint64_t key = ((uint64_t)vbusy[s * kWave] << 32) | (uint32_t)(base + s * kWave + lane);
       mk = key < mk ? key : mk;

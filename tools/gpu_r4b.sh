@@ -20,3 +20,10 @@ for rep in 1 2; do
   done
 done
 step done
+if [ "${PROF:-1}" = 1 ]; then
+  step prof_c3
+  timeout -k 10 300 python tools/replay_counters.py --mode time --R 1024 --out $O/c3_time_R1024.json > /dev/null 2> $O/prof_time.err || { tail $O/prof_time.err; exit 1; }
+  timeout -k 10 300 python tools/replay_counters.py --mode count --R 1024 --out $O/c3_count_R1024.json > /dev/null 2> $O/prof_count.err || { tail $O/prof_count.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/c3_time_R1024.json')); print(json.dumps(d['all'])); print(json.dumps(d['per_rep_total_cycles']))"
+  python3 -c "import json; d=json.load(open('$O/c3_count_R1024.json')); print(json.dumps(d['all']))"
+fi
