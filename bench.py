@@ -12,8 +12,12 @@ RCCL all-reduce of histograms + energy.  Replications are sharded over ranks
 
 ``--workload c5`` runs config C5 (large topology, BASELINE.json configs[4]):
 1024 replications in total x T = 10,000 x N = 10,000 fog nodes, sharded over
-the ranks (strong scaling), on the wide replay kernel (replay_wide.hip), with
-the builder-defined light-load recipe of ``fognetsimpp_amd.c5_params``.
+the ranks (strong scaling), with the builder-defined light-load recipe of
+``fognetsimpp_amd.c5_params``: the default EXT_HIER policy (hierarchical
+brokers + mobility handoff) on the region kernel (replay_region.hip: one
+wavefront per regional broker while no region escalates, the sequential wide
+kernel for a replication that does), ``--policy REF_V3`` on the wide replay
+kernel (replay_wide.hip).
 
 ``--workload c1`` runs config C1 (the reference's example General run,
 BASELINE.json configs[0]) with the modules its ini names (BrokerBaseApp2 +
@@ -297,7 +301,9 @@ def main():
                        "parallelism": f"replications sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": ("replay_wide_kernel (statistics inline)" if N > 256
+                         "kernel": ("replay_region_kernel (one wavefront per regional broker) + region_finish_kernel "
+                                    "(statistics pass)" if args.policy == "EXT_HIER" and N > _abi.HIER_REGION_NODES
+                                    else "replay_wide_kernel (statistics inline)" if N > 256
                                     else "replay_kernel (statistics pass fused)"), "kernel_avg_ms": replay_avg_s * 1e3,
                          "bytes_per_decision": bpd, "bytes_per_decision_source": "SURVEY.md §8(d)",
                          "valu_issue": valu},
