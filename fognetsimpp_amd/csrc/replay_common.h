@@ -515,4 +515,38 @@ __device__ __forceinline__ bool apply_wide_advert(WideNode& h, const WideEntry* 
   return busy < ((uint64_t)1 << 24);  // FOGNET_POLICY_EXT_LAT's cost needs busy < 2^24
 }
 
+// ---------------------------------------------------------------- a11 energy over node records
+// E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12) with B_j = node j's service seconds
+// (its tail's cumulative sum, nd[j].tl_C), each operation separately rounded, summed in node
+// order (0, 1, ..., N-1) by one wavefront (all 64 lanes active; the sum is returned in every
+// lane).  kDepth chunks of 64 nodes have their loads issued before the first of them is summed:
+// the sum is one dependent chain, so the record and power loads must not each wait in it.
+template <int kDepth = 8>
+__device__ __forceinline__ double energy_sum_wave(const WideNode* nd, const double* p_busy, const double* p_idle,
+                                                  int N, int64_t H, double* out_row, int lane) {
+  double sum = 0.0;
+  for (int c0 = 0; c0 < N; c0 += kDepth * kWave) {
+    double en[kDepth];
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u) {
+      const int j = c0 + u * kWave + lane;
+      en[u] = 0.0;
+      if (j < N) {
+        const int64_t B = (int64_t)nd[j].tl_C;
+        const double eb = mul_rn(p_busy[j], (double)B);
+        const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
+        en[u] = add_rn(eb, mul_rn(p_idle[j], idle));
+        if (out_row) out_row[j] = en[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u) {
+      const int j0 = c0 + u * kWave;
+      const int m = min(kWave, N - j0);
+      for (int l = 0; l < m; ++l) sum = add_rn(sum, __longlong_as_double(readlane_i64(__double_as_longlong(en[u]), l)));
+    }
+  }
+  return sum;
+}
+
 }  // namespace fognet

@@ -347,23 +347,10 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   }
   // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12), summed in node
   // order by the first wave (replay_wide.hip's order: 64 nodes at a time, then lane by lane)
-  if (A.p_busy && tid < kWave) {
+  if (A.p_busy && tid < kWave) {  // (an unused node's record has tl_C = 0)
     const int64_t H = n > 0 ? s_acc[0].last : 0;
-    double sum = 0.0;
-    for (int j0 = 0; j0 < N; j0 += kWave) {
-      const int j = j0 + tid;
-      double en = 0.0;
-      if (j < N) {
-        const WideNode x = nd[j];
-        const int64_t Bj = x.tl >= 0 ? (int64_t)x.tl_C : 0;
-        const double eb = mul_rn(A.p_busy[nbase + j], (double)Bj);
-        const double idle = __ddiv_rn((double)(H - Bj * kTicksPerSecond), 1e12);
-        en = add_rn(eb, mul_rn(A.p_idle[nbase + j], idle));
-        if (A.out_energy) A.out_energy[(size_t)r * (size_t)N + j] = en;
-      }
-      const int m = min(kWave, N - j0);
-      for (int l = 0; l < m; ++l) sum = add_rn(sum, __longlong_as_double(readlane_i64(__double_as_longlong(en), l)));
-    }
+    const double sum = energy_sum_wave(nd, A.p_busy + nbase, A.p_idle + nbase, N, H,
+                                       A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, tid);
     if (tid == 0) S->energy_j = sum;
   }
 }

@@ -1144,20 +1144,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     __syncthreads();  // (the records written back above by their owner lanes are read by others)
     // per node j (lane j % 64 here), then summed in node order 64 at a time
     const int64_t H = n_done > 0 ? acc.last : 0;
-    double sum = 0.0;
-    for (int j0 = 0; j0 < N; j0 += kWave) {
-      const int j = j0 + lane;
-      double en = 0.0;
-      if (j < N) {
-        const int64_t B = (int64_t)nd[j].tl_C;
-        const double eb = mul_rn(A.p_busy[nbase + j], (double)B);
-        const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
-        en = add_rn(eb, mul_rn(A.p_idle[nbase + j], idle));
-        if (A.out_energy) A.out_energy[(size_t)r * (size_t)N + j] = en;
-      }
-      const int m = min(kWave, N - j0);
-      for (int l = 0; l < m; ++l) sum = add_rn(sum, __longlong_as_double(readlane_i64(__double_as_longlong(en), l)));
-    }
+    const double sum = energy_sum_wave(nd, A.p_busy + nbase, A.p_idle + nbase, N, H,
+                                       A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, lane);
     if (lane == 0) S->energy_j = sum;
   }
   if (hist) {
