@@ -92,6 +92,15 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return min(min(r0, r1), min(r2, r3));
 }
 
+// Sum over the 64 lanes (all active), every lane gets it.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += dpp_u32<0xB1>(v);
+  v += dpp_u32<0x4E>(v);
+  v += dpp_u32<0x141>(v);
+  v += dpp_u32<0x140>(v);
+  return readlane_u32(v, 0) + readlane_u32(v, 16) + readlane_u32(v, 32) + readlane_u32(v, 48);
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 
 struct U4 {

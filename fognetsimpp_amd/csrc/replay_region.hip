@@ -280,22 +280,24 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   const int r = blockIdx.x;
   const int tid = threadIdx.x;
   const int B = W.B, N = A.N;
-  __shared__ Acc s_acc[kFinThreads];
+  constexpr int kFinWaves = kFinThreads / kWave;
+  // (per-wave partial records: 4 x 152 B of LDS, so many blocks fit per CU)
+  __shared__ Acc s_acc[kFinWaves];
   __shared__ int64_t s_abt[kFinThreads];
   __shared__ int32_t s_abk[kFinThreads];
   __shared__ uint32_t s_hist[FOGNET_HIST_METRICS * FOGNET_HIST_BINS];
   __shared__ int s_ok, s_done, s_mp;
-  if (tid == 0) {
-    int ok = 1, done = 0, mp = 0;
-    for (int b = 0; b < B; ++b) {
-      const RegionRec x = W.rec[(size_t)r * B + b];
-      ok &= x.status == FOGNET_OK;
-      done += x.n_done;
-      mp = max(mp, x.max_pend);
+  if (tid < kWave) {  // the regions' records, one per lane (B <= 64: N <= 65,536)
+    RegionRec x{0, 0, FOGNET_OK, 0};
+    if (tid < B) x = W.rec[(size_t)r * B + tid];
+    const bool ok = ballot(x.status != FOGNET_OK) == 0ull;
+    const int done = (int)wave_sum_u32((uint32_t)x.n_done);
+    const int mp = (int)~wave_min_u32(~(uint32_t)x.max_pend);
+    if (tid == 0) {
+      s_ok = ok;
+      s_done = done;
+      s_mp = mp;
     }
-    s_ok = ok;
-    s_done = done;
-    s_mp = mp;
   }
   __syncthreads();
   if (!s_ok) {  // (the sequential replay overwrites the record; FOGNET_HIER_REGIONS=only leaves this status)
@@ -317,30 +319,45 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   Acc a = acc_identity();
   stats_accumulate<2, false>(A, tbase, n, tid, kFinThreads, a, nullptr, s_hist,
                              [&](int k) { return A.dl[nbase + k]; }, s_abt, s_abk);
-  // busy seconds and the last completion from the node tails
-  for (int j = tid; j < N; j += kFinThreads) {
-    const WideNode x = nd[j];
-    if (x.tl >= 0) {
-      a.busy += x.tl_C;
-      a.last = max(a.last, x.tl_done);
+  // busy seconds and the last completion from the node tails (2 records in flight per thread)
+  for (int j0 = tid; j0 < N; j0 += 2 * kFinThreads) {
+    WideNode x[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = j0 + u * kFinThreads;
+      x[u] = j < N ? nd[j] : WideNode{-1, -1, 0, -1, 0, 0u, 0, 0, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (x[u].tl >= 0) {
+        a.busy += x[u].tl_C;
+        a.last = max(a.last, x[u].tl_done);
+      }
     }
   }
-  s_acc[tid] = a;
+  a = wave_merge(a);
+  const AbortPt ab_w = wave_min_abort(AbortPt{s_abt[tid], s_abk[tid]});  // (each thread's own slot)
+  if ((tid & (kWave - 1)) == 0) {
+    s_acc[tid / kWave] = a;
+    s_abt[tid] = ab_w.tick;
+    s_abk[tid] = ab_w.task;
+  }
   __syncthreads();
-  for (int w = kFinThreads / 2; w > 0; w >>= 1) {
-    if (tid < w) {
-      acc_merge(s_acc[tid], s_acc[tid + w]);
-      abort_min(s_abt[tid], s_abk[tid], s_abt[tid + w], s_abk[tid + w]);
-    }
-    __syncthreads();
-  }
   if (tid == 0) {
+    Acc t = s_acc[0];
+    AbortPt ab = AbortPt{s_abt[0], s_abk[0]};
+    for (int w = 1; w < kFinWaves; ++w) {
+      acc_merge(t, s_acc[w]);
+      abort_min(ab.tick, ab.task, s_abt[w * kWave], s_abk[w * kWave]);
+    }
+    s_acc[0] = t;
     S->n_tasks = n;
     S->max_pending = s_mp;
     S->status = FOGNET_OK;
     S->events = 2 * (int64_t)N + 4 * (int64_t)n;  // initial adverts + publish, arrival, release, advert per task
-    write_rep_stats(S, s_acc[0], AbortPt{s_abt[0], s_abk[0]}, A.ref_abort);
+    write_rep_stats(S, t, ab, A.ref_abort);
   }
+  __syncthreads();  // (s_acc[0].last: the energy's horizon)
   if (A.hist) {
     for (int h = tid; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kFinThreads)
       if (s_hist[h]) atomicAdd((unsigned long long*)&A.hist[h], (unsigned long long)s_hist[h]);
