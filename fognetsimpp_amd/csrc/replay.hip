@@ -1144,6 +1144,7 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
         if (lane == 0) abort_min(s_ab_tick[0], s_ab_task[0], m.tick, m.task);
       }
     }
+    TMARK(7)  // (profile builds: the chunk's output flush and statistics)
   }
   // drain the inline-asm prefetches before the wave retires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

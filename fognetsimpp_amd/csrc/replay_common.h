@@ -25,6 +25,13 @@ __device__ __forceinline__ int64_t ticks_of(uint32_t s) {
   return (int64_t)(((uint64_t)s * 244140625u) << 12);
 }
 
+// s_waitcnt vmcnt(0) (expcnt, lgkmcnt unconstrained) as the builtin, so the
+// compiler's wait insertion knows every load issued so far has landed.  Placed
+// inside the arm of a branch that loads, it keeps the wait off the other arm: the
+// compiler would otherwise wait at the merge (vmcnt(0), which on gfx9 also waits
+// for every store issued before), on every path.
+__device__ __forceinline__ void sync_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // arrival at tick `a` happens before the completion at `done` of a task with
 // service S on a node with downlink latency dl (FES insertion-order rule,
 // DESIGN.md §3.3).
@@ -471,6 +478,7 @@ __device__ __forceinline__ bool apply_wide_advert(WideNode& h, const WideEntry* 
   WideEntry nx{};
   if (h.npend >= 2) {
     nx = e[h.hd_next];
+    sync_vm();  // (in this arm: see sync_vm)
     // Chain invariant, checked at every applied advert: with two or more tasks
     // pending, the record's hd_next names the entry whose prev is the head and
     // whose cumulative service is the head's plus its own.  hd_next changes on
@@ -494,6 +502,7 @@ __device__ __forceinline__ bool apply_wide_advert(WideNode& h, const WideEntry* 
       }
       x = ex.prev;
     }
+    sync_vm();
   }
   const uint64_t busy = c_arrived - h.hd_C;
   // the view keeps 32 bits, saturated: a saturated node can only be chosen when the

@@ -60,11 +60,16 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
   int64_t* const vnxt = s_nxt + lane;    // vnxt[s * kWave]: slot s of this lane
   uint32_t* const vbusy = s_busy + lane;
   bool bad = false;
+  // slots with an advert pending (view tick not kNever) and slots whose advertised busy
+  // time is not 0, as bit masks: the rescans below visit only the first kind, and a
+  // lane with a zero-busy slot has its smallest key without reading the view
+  uint32_t act = 0u, nzb = 0u;
 #pragma unroll
   for (int s = 0; s < kRegionSlots; ++s) {
     const int l = s * kWave + lane;
     vnxt[s * kWave] = kNever;
     vbusy[s * kWave] = l < nb ? 0u : kRegBusySat;  // (past the region: never the minimum)
+    nzb |= l < nb ? 0u : 1u << s;
     if (l < nb) {
       const int j = base + l;
       const int32_t m = A.mips[nbase + j];
@@ -77,20 +82,27 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
   int64_t mn = kNever;
   int ms = 0;
   uint64_t mk = lane < nb ? (uint64_t)(uint32_t)(base + lane) : ~0ull;
-  // (partially unrolled: a full unroll issues all 16 LDS loads at once and holds 32 VGPRs)
-  auto rescan_nxt = [&]() {
-    mn = kNever;
-    ms = 0;
-#pragma unroll 4
-    for (int s = 0; s < kRegionSlots; ++s) {
+  // after slot sl's view tick became xs: the earliest over the pending slots (ties: the
+  // smallest slot)
+  auto rescan_nxt = [&](int sl, int64_t xs) {
+    mn = xs;
+    ms = sl;
+    for (uint32_t m = act & ~(1u << sl); m; m &= m - 1u) {
+      const int s = __builtin_ctz(m);
       const int64_t x = vnxt[s * kWave];
-      if (x < mn) {
+      if (x < mn || (x == mn && s < ms)) {
         mn = x;
         ms = s;
       }
     }
   };
+  // (partially unrolled: a full unroll issues all 16 LDS loads at once and holds 32 VGPRs)
   auto rescan_key = [&]() {
+    const uint32_t z = ~nzb & ((1u << kRegionSlots) - 1u);
+    if (z) {  // a zero-busy slot: the smallest one holds the smallest key
+      mk = (uint32_t)(base + __builtin_ctz(z) * kWave + lane);
+      return;
+    }
     mk = ~0ull;
 #pragma unroll 4
     for (int s = 0; s < kRegionSlots; ++s) {
@@ -113,15 +125,27 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
   auto cache_node = [&](uint32_t kk, int kl) {
     if (lane == kl && (int)kk != cj) {
       if (cj >= 0) nd[cj] = ch;
+
+
       cj = (int)kk;
       ch = nd[kk];
       c_dv = udiv_magic((uint32_t)A.mips[nbase + kk]);
       c_dl = A.dl[nbase + kk];
       c_ul = A.ul[nbase + kk];
+      sync_vm();  // (here: a hit then waits for nothing)
     }
   };
   bool view_changed = true;
   uint64_t key = 0ull;  // the regional broker's choice: its smallest view key
+#ifdef FOGNET_REGION_PROF
+  uint64_t pr[16] = {};
+  uint64_t pt0 = clock64(), pt = 0;
+#define PRC(i, v) pr[i] += (v)
+#define PRT(i) { const uint64_t _n = clock64(); pr[i] += _n - pt; pt = _n; }
+#else
+#define PRC(i, v)
+#define PRT(i)
+#endif
 
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
@@ -138,6 +162,9 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
     prev_t = readlane_i64(ca, cnt - 1);
     // this chunk's publishes of region b; each member lane keeps its task's outputs until the chunk ends
     uint64_t mem = ballot(live && cg == b);
+#ifdef FOGNET_REGION_PROF
+    pt = clock64();
+#endif
     bool q_on = false;
     uint32_t q_k = 0u, q_status = 0u;
     int64_t q_start = 0, q_done = 0;
@@ -149,14 +176,28 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
       // 1) completion adverts that reached the broker strictly before t, lane-parallel
       bool lbroken = false;
       if (ballot(mn < t)) view_changed = true;
+      PRC(0, 1);
       while (ballot(mn < t)) {
+        PRC(1, 1);
+        PRC(2, __builtin_popcountll(ballot(mn < t)));
+        PRC(3, __builtin_popcountll(ballot(mn < t && base + ms * kWave + lane == cj)));
+        PRC(4, __builtin_popcountll(ballot(mn < t && base + ms * kWave + lane == cj && ch.npend >= 2)));
         if (mn < t) {
           const int sl = ms;
           const int j = base + sl * kWave + lane;
           const bool hit = j == cj;
-          WideNode h = hit ? ch : nd[j];
-          const int64_t dl_j = hit ? c_dl : A.dl[nbase + j];
-          const int64_t ul_j = hit ? c_ul : A.ul[nbase + j];
+          WideNode h;
+          int64_t dl_j, ul_j;
+          if (hit) {
+            h = ch;
+            dl_j = c_dl;
+            ul_j = c_ul;
+          } else {  // (waited for here, not where the arms meet: sync_vm)
+            h = nd[j];
+            dl_j = A.dl[nbase + j];
+            ul_j = A.ul[nbase + j];
+            sync_vm();
+          }
           int64_t nxt_j;
           uint32_t busy_j;
           bool broken = false;
@@ -167,9 +208,12 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
           else nd[j] = h;
           vnxt[sl * kWave] = nxt_j;
           vbusy[sl * kWave] = busy_j;
-          rescan_nxt();
+          act = nxt_j != kNever ? act | (1u << sl) : act & ~(1u << sl);
+          nzb = busy_j != 0u ? nzb | (1u << sl) : nzb & ~(1u << sl);
+          rescan_nxt(sl, nxt_j);
           // the key: only j's changed; a rescan only when j held the minimum and grew
           const uint64_t nk = ((uint64_t)busy_j << 32) | (uint32_t)j;
+          PRC(6, __builtin_popcountll(ballot((uint32_t)mk == (uint32_t)j && nk > mk)));
           if ((uint32_t)mk == (uint32_t)j && nk > mk) rescan_key();
           else mk = nk < mk ? nk : mk;
         }
@@ -178,7 +222,9 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
         err = FOGNET_ERR_INTERNAL;
         break;
       }
+      PRT(8)
       // 2) the regional broker's decision; above the threshold it would escalate
+      PRC(7, view_changed ? 1 : 0);
       if (view_changed) {
         key = wave_min_u64(mk);
         view_changed = false;
@@ -191,6 +237,9 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
       const int kl = ((int)k - base) & (kWave - 1);
 
       // 3) the task reaches node k (ComputeBrokerApp3.cc:269-320): FIFO single server
+      PRC(5, ballot(lane == kl && (int)k != cj) ? 1 : 0);
+      PRC(12, (k - base) / kWave);
+      PRT(9)
       cache_node(k, kl);
       const UDiv div_k{readlane_u32(c_dv.m, kl), readlane_u32(c_dv.sh, kl)};
       const int64_t dl_k = readlane_i64(c_dl, kl), ul_k = readlane_i64(c_ul, kl);
@@ -228,6 +277,7 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
           const int sk = ((int)k - base) / kWave;
           const int64_t x = done + ul_k;
           vnxt[sk * kWave] = x;
+          act |= 1u << sk;
           if (x < mn) {
             mn = x;
             ms = sk;
@@ -253,6 +303,7 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
         q_done = done;
       }
       n_done += 1;
+      PRT(10)
     }
     // the chunk's outputs (member lanes, coalesced)
     if (q_on) {
@@ -264,6 +315,12 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
     }
   }
   if (cj >= 0) nd[cj] = ch;
+#ifdef FOGNET_REGION_PROF
+  pr[11] = clock64() - pt0;
+  if (lane == 0 && (blockIdx.x < 3 || blockIdx.x % 1000 == 7))
+    printf("RPROF blk %d pubs %lu rounds %lu advl %lu hit %lu hit_e %lu cmiss %lu krescan %lu dec %lu cyc_adv %lu cyc_dec %lu cyc_push %lu cyc_tot %lu slotsum %lu\n",
+           (int)blockIdx.x, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[8], pr[9], pr[10], pr[11], pr[12]);
+#endif
   const uint32_t mp = ~wave_min_u32(~max_pend);
   if (lane == 0) W.rec[blockIdx.x] = RegionRec{n_done, (int32_t)mp, (int32_t)err, 0};
 }

@@ -609,9 +609,6 @@ struct V2MsgR {
 static_assert(sizeof(V2MsgR) == sizeof(V2Msg), "same queue slot");
 constexpr uint32_t kSeqLimit = 0xFFFFFF00u;
 
-// s_waitcnt vmcnt(0) (expcnt, lgkmcnt unconstrained) as the builtin, so the
-// compiler's wait insertion knows every load issued so far has landed.
-__device__ __forceinline__ void sync_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 constexpr int kTraceChunk = 64;
 
 __device__ __forceinline__ bool earlier32(int64_t t, uint32_t s, int64_t t2, uint32_t s2) {

@@ -29,7 +29,7 @@ FIELDS = [("n_queued", "iterations"), ("n_started", "advert_loop_iters"), ("last
 TIME_FIELDS = [("n_queued", "cyc_chunk"), ("n_started", "cyc_adverts"), ("last_tick", "cyc_argmin"),
                ("queue_min_raw", "cyc_horizon"), ("queue_max_raw", "cyc_run_scan"),
                ("resp_min_ticks", "cyc_stores"), ("resp_max_ticks", "cyc_node_update"),
-               ("queue_sum_lo", "cyc_tail"), ("queue_sum_hi", "cyc_total"), ("queue_sq_lo", "cyc_advert_nh_wait"),
+               ("queue_sum_lo", "cyc_chunk_flush_stats"), ("queue_sum_hi", "cyc_total"), ("queue_sq_lo", "cyc_advert_nh_wait"),
                ("queue_sq_hi", "cyc_horizon_nh_wait")]
 
 
