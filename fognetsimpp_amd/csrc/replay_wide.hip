@@ -43,6 +43,10 @@
 // max_pending) follows the reference's `brokers` bookkeeping.
 #include "replay_common.h"
 
+#ifndef FOGNET_WIDE_MASK
+#define FOGNET_WIDE_MASK 1
+#endif
+
 namespace fognet {
 
 namespace {
@@ -84,6 +88,11 @@ struct WideLds {
   int64_t* q_dn;    // [64] completion (kNever: never)
   int32_t* q_i;     // [64] task index
   uint32_t* q_sS;   // [64] service seconds << 3 | status (4, 5, 9 -> 4, 5, 1)
+  // [G][64] per group of the lane: bit i (0-15) slot i has an advert pending (view tick
+  // not kNever), bit 16 + i its advertised busy time is not 0 (past N: saturated).  An
+  // advert rescans only the group's pending slots, and a key rescan of a group with a
+  // zero-busy slot needs no view read (its smallest such slot holds the smallest key).
+  uint32_t* g_msk;
   int G;
 };
 
@@ -163,6 +172,15 @@ __device__ __forceinline__ uint64_t group_key(const WideView& V, int lane, int g
     mk = key < mk ? key : mk;
   }
   return mk;
+}
+
+// group_key with the group's busy mask (WideLds::g_msk): a zero-busy slot holds
+// the group's smallest key (nodes grow with the slot), else the full scan.
+template <bool R>
+__device__ __forceinline__ uint64_t group_key_m(const WideView& V, const WideLds& L, int lane, int g) {
+  const uint32_t z = ~(L.g_msk[g * kWave + lane] >> 16) & 0xFFFFu;
+  if (z) return (uint64_t)(uint32_t)wnode<R>(g * kWideGroupSlots + __builtin_ctz(z), lane);
+  return group_key<R>(V, lane, g);
 }
 
 // The lane's earliest advert over its groups (first group on ties).
@@ -343,6 +361,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   L.q_dn = L.q_st + kWave;
   L.q_i = reinterpret_cast<int32_t*>(L.q_dn + kWave);
   L.q_sS = reinterpret_cast<uint32_t*>(L.q_i + kWave);
+  L.g_msk = L.q_sS + kWave;
   const int SP = L.G * kWideGroupSlots;
   const WideView V{VN + ((size_t)wr * kWave + lane) * SP, VB + ((size_t)wr * kWave + lane) * SP,
                    VW + ((size_t)wr * kWave + lane) * SP};
@@ -406,6 +425,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     L.g_w[g * kWave + lane] = kNever;
     L.g_j[g * kWave + lane] = j0;
     L.g_key[g * kWave + lane] = j0 < N ? (uint64_t)(uint32_t)j0 : ~0ull;
+    uint32_t nz = 0u;  // slots past N: busy saturated
+    for (int i = 0; i < kWideGroupSlots; ++i) nz |= wnode<kHier>(g * kWideGroupSlots + i, lane) < N ? 0u : 1u << i;
+    L.g_msk[g * kWave + lane] = nz << 16;
   }
   __syncthreads();
   uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
@@ -542,6 +564,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         const int64_t x = done == kNever ? kNever : done + ul_k;
         const int g = ((int)kk / kWave) / kWideGroupSlots;
         V.nxt[kk / kWave] = x;
+        if (x != kNever) L.g_msk[g * kWave + lane] |= 1u << ((kk / kWave) % kWideGroupSlots);
         if (x < L.g_nxt[g * kWave + lane]) {
           L.g_nxt[g * kWave + lane] = x;
           L.g_j[g * kWave + lane] = (int)kk;
@@ -727,13 +750,29 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           uint32_t busy_j;
           const bool hit = j == cj;
           const int g = sl / kWideGroupSlots;
+#if FOGNET_WIDE_MASK
+          const int si = sl % kWideGroupSlots;
+          WideNode h;
+          int64_t dl_j, ul_j;
+          if (hit) {
+            h = ch;
+            dl_j = c_dl;
+            ul_j = c_ul;
+          } else {  // (waited for in this arm: sync_vm)
+            h = nd[j];
+            dl_j = P_dl[j];
+            ul_j = P_ul[j];
+            sync_vm();
+          }
+#else
           int64_t gx[kWideGroupSlots], gw[kWideGroupSlots];
           group_load(V, g, gx);
           if constexpr (!kPerPublish) group_load_w(V, g, gw);
           WideNode h = hit ? ch : nd[j];
           const int64_t dl_j = hit ? c_dl : P_dl[j];
-          bool broken = false;
           const int64_t ul_j = hit ? c_ul : P_ul[j];
+#endif
+          bool broken = false;
           bool fits = apply_wide_advert(h, e, dl_j, ul_j, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
           // node j's later adverts that are due too: adverts of different nodes commute (each
           // sets only its node's view), so j's are applied now, in their order, and only the
@@ -750,6 +789,38 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           else nd[j] = h;
           V.nxt[sl] = nxt_j;
           V.busy[sl] = busy_j;
+#if FOGNET_WIDE_MASK
+          // the earliest advert: j's was the lane's (so its group's), rescan both levels, the
+          // group over its other pending slots only (ties: the smallest slot)
+          const uint32_t gm0 = L.g_msk[g * kWave + lane];
+          const uint32_t bit = 1u << si;
+          uint32_t gm = nxt_j != kNever ? gm0 | bit : gm0 & ~bit;
+          gm = busy_j != 0u ? gm | (bit << 16) : gm & ~(bit << 16);
+          L.g_msk[g * kWave + lane] = gm;
+          int64_t gmn = nxt_j, gmw = kNever;
+          int gsi = si;
+          if constexpr (!kPerPublish) gmw = node_w(h, nxt_j, dl_j);
+          if constexpr (!kPerPublish) V.w[sl] = gmw;
+          for (uint32_t m = gm0 & 0xFFFFu & ~bit; m; m &= m - 1u) {
+            const int i = __builtin_ctz(m);
+            const int64_t x = V.nxt[g * kWideGroupSlots + i];
+            int64_t w = kNever;
+            if constexpr (!kPerPublish) w = V.w[g * kWideGroupSlots + i];
+            if (x < gmn || (x == gmn && i < gsi)) {
+              gmn = x;
+              gsi = i;
+            }
+            gmw = w < gmw ? w : gmw;
+          }
+          L.g_nxt[g * kWave + lane] = gmn;
+          L.g_j[g * kWave + lane] = gmn == kNever ? lane : wnode<kHier>(g * kWideGroupSlots + gsi, lane);
+          if constexpr (!kPerPublish) {
+            L.g_w[g * kWave + lane] = gmw;
+            lane_min_nxt_w(L, lane, mn, mj, mw);  // (one LDS pass for both lane minima)
+          } else {
+            lane_min_nxt(L, lane, mn, mj);
+          }
+#else
           // the earliest advert: j's was the lane's (so its group's), rescan both levels
           group_scan_nxt<kHier>(L, lane, g, sl, nxt_j, gx);
           if constexpr (!kPerPublish) {
@@ -760,6 +831,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           } else {
             lane_min_nxt(L, lane, mn, mj);
           }
+#endif
 #ifdef FOGNET_WIDE_PROF
           pf_hit += hit ? 1u : 0u;
 #endif
@@ -767,8 +839,13 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           // when j held it and its busy time grew
           const uint64_t gk_old = L.g_key[g * kWave + lane];
           const uint64_t nk = ((uint64_t)busy_j << 32) | (uint32_t)j;
+#if FOGNET_WIDE_MASK
+          const uint64_t gk_new = ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? group_key_m<kHier>(V, L, lane, g)
+                                                                                 : (nk < gk_old ? nk : gk_old);
+#else
           const uint64_t gk_new = ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? group_key<kHier>(V, lane, g)
                                                                                  : (nk < gk_old ? nk : gk_old);
+#endif
 #ifdef FOGNET_WIDE_PROF
           pf_gkey += ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? 1u : 0u;
 #endif
@@ -1030,6 +1107,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           const int64_t x = done_f == kNever ? kNever : done_f + ul_k;
           const int g = ((int)k / kWave) / kWideGroupSlots;
           V.nxt[k / kWave] = x;
+          if (x != kNever) L.g_msk[g * kWave + lane] |= 1u << ((k / kWave) % kWideGroupSlots);
           if (x < L.g_nxt[g * kWave + lane]) {
             L.g_nxt[g * kWave + lane] = x;
             L.g_j[g * kWave + lane] = (int)k;
@@ -1170,7 +1248,8 @@ size_t replay_wide_lds_bytes(int32_t N) {
   const size_t G = (size_t)wide_groups(N);
   return G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int64_t) + sizeof(int32_t)) +
          FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t) + G * sizeof(uint64_t) +
-         kHierPending * (2 * sizeof(int64_t) + 3 * sizeof(int32_t)) + kWave * (4 * sizeof(int64_t) + 2 * sizeof(int32_t));
+         kHierPending * (2 * sizeof(int64_t) + 3 * sizeof(int32_t)) + kWave * (4 * sizeof(int64_t) + 2 * sizeof(int32_t)) +
+         G * kWave * sizeof(uint32_t);
 }
 
 size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen) { return wide_ws(R, T, N, gen).bytes; }
