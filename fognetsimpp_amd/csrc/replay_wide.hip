@@ -227,6 +227,39 @@ __device__ __forceinline__ void lane_min_nxt_w(const WideLds& L, int lane, int64
   }
 }
 
+// The same over the groups with a pending advert only (bit g of ga; G <= 64): the
+// other groups hold kNever in both minima.
+__device__ __forceinline__ void lane_min_nxt_w_m(const WideLds& L, int lane, uint64_t ga, int64_t& mn, int& mj,
+                                                 int64_t& mw) {
+  mn = kNever;
+  mj = lane;
+  mw = kNever;
+  for (uint64_t m = ga; m; m &= m - 1ull) {
+    const int g = (int)__builtin_ctzll(m);
+    const int64_t x = L.g_nxt[g * kWave + lane];
+    const int jj = L.g_j[g * kWave + lane];
+    const int64_t w = L.g_w[g * kWave + lane];
+    if (x < mn) {
+      mn = x;
+      mj = jj;
+    }
+    mw = w < mw ? w : mw;
+  }
+}
+__device__ __forceinline__ void lane_min_nxt_m(const WideLds& L, int lane, uint64_t ga, int64_t& mn, int& mj) {
+  mn = kNever;
+  mj = lane;
+  for (uint64_t m = ga; m; m &= m - 1ull) {
+    const int g = (int)__builtin_ctzll(m);
+    const int64_t x = L.g_nxt[g * kWave + lane];
+    const int jj = L.g_j[g * kWave + lane];
+    if (x < mn) {
+      mn = x;
+      mj = jj;
+    }
+  }
+}
+
 __device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn, int& mj, uint64_t& mk) {
   lane_min_nxt(L, lane, mn, mj);
   mk = lane_min_key(L, lane);
@@ -437,6 +470,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   int mj;
   uint64_t mk;
   lane_min(L, lane, mn, mj, mk);
+  uint64_t gact = 0ull;  // the lane's groups with a pending advert (FOGNET_WIDE_MASK)
   int64_t mw = kNever;  // REF_V3 run horizon: this lane's smallest node_w
   Acc acc = acc_identity();
   AbortPt ab = abort_none();  // the reference's abort point (replay_common.h)
@@ -564,7 +598,10 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         const int64_t x = done == kNever ? kNever : done + ul_k;
         const int g = ((int)kk / kWave) / kWideGroupSlots;
         V.nxt[kk / kWave] = x;
-        if (x != kNever) L.g_msk[g * kWave + lane] |= 1u << ((kk / kWave) % kWideGroupSlots);
+        if (x != kNever) {
+          L.g_msk[g * kWave + lane] |= 1u << ((kk / kWave) % kWideGroupSlots);
+          gact |= 1ull << g;
+        }
         if (x < L.g_nxt[g * kWave + lane]) {
           L.g_nxt[g * kWave + lane] = x;
           L.g_j[g * kWave + lane] = (int)kk;
@@ -814,11 +851,12 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           }
           L.g_nxt[g * kWave + lane] = gmn;
           L.g_j[g * kWave + lane] = gmn == kNever ? lane : wnode<kHier>(g * kWideGroupSlots + gsi, lane);
+          gact = (gm & 0xFFFFu) != 0u ? gact | (1ull << g) : gact & ~(1ull << g);
           if constexpr (!kPerPublish) {
             L.g_w[g * kWave + lane] = gmw;
-            lane_min_nxt_w(L, lane, mn, mj, mw);  // (one LDS pass for both lane minima)
+            lane_min_nxt_w_m(L, lane, gact, mn, mj, mw);  // (one LDS pass for both lane minima)
           } else {
-            lane_min_nxt(L, lane, mn, mj);
+            lane_min_nxt_m(L, lane, gact, mn, mj);
           }
 #else
           // the earliest advert: j's was the lane's (so its group's), rescan both levels
@@ -1107,7 +1145,10 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           const int64_t x = done_f == kNever ? kNever : done_f + ul_k;
           const int g = ((int)k / kWave) / kWideGroupSlots;
           V.nxt[k / kWave] = x;
-          if (x != kNever) L.g_msk[g * kWave + lane] |= 1u << ((k / kWave) % kWideGroupSlots);
+          if (x != kNever) {
+            L.g_msk[g * kWave + lane] |= 1u << ((k / kWave) % kWideGroupSlots);
+            gact |= 1ull << g;
+          }
           if (x < L.g_nxt[g * kWave + lane]) {
             L.g_nxt[g * kWave + lane] = x;
             L.g_j[g * kWave + lane] = (int)k;
