@@ -186,26 +186,22 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
           const int sl = ms;
           const int j = base + sl * kWave + lane;
           const bool hit = j == cj;
-          WideNode h;
-          int64_t dl_j, ul_j;
-          if (hit) {
-            h = ch;
-            dl_j = c_dl;
-            ul_j = c_ul;
-          } else {  // (waited for here, not where the arms meet: sync_vm)
-            h = nd[j];
-            dl_j = A.dl[nbase + j];
-            ul_j = A.ul[nbase + j];
-            sync_vm();
-          }
           int64_t nxt_j;
           uint32_t busy_j;
           bool broken = false;
-          (void)apply_wide_advert(h, e, dl_j, ul_j, 0, nxt_j, busy_j, broken);
-          while (nxt_j < t && !broken) (void)apply_wide_advert(h, e, dl_j, ul_j, 0, nxt_j, busy_j, broken);
+          // the cached record is updated in place (no copy of it through a merged value)
+          if (hit) {
+            (void)apply_wide_advert(ch, e, c_dl, c_ul, 0, nxt_j, busy_j, broken);
+            while (nxt_j < t && !broken) (void)apply_wide_advert(ch, e, c_dl, c_ul, 0, nxt_j, busy_j, broken);
+          } else {  // (waited for here, not where the arms meet: sync_vm)
+            WideNode h = nd[j];
+            const int64_t dl_j = A.dl[nbase + j], ul_j = A.ul[nbase + j];
+            sync_vm();
+            (void)apply_wide_advert(h, e, dl_j, ul_j, 0, nxt_j, busy_j, broken);
+            while (nxt_j < t && !broken) (void)apply_wide_advert(h, e, dl_j, ul_j, 0, nxt_j, busy_j, broken);
+            nd[j] = h;
+          }
           lbroken |= broken;
-          if (hit) ch = h;
-          else nd[j] = h;
           vnxt[sl * kWave] = nxt_j;
           vbusy[sl * kWave] = busy_j;
           act = nxt_j != kNever ? act | (1u << sl) : act & ~(1u << sl);

@@ -43,10 +43,6 @@
 // max_pending) follows the reference's `brokers` bookkeeping.
 #include "replay_common.h"
 
-#ifndef FOGNET_WIDE_MASK
-#define FOGNET_WIDE_MASK 1
-#endif
-
 namespace fognet {
 
 namespace {
@@ -127,36 +123,6 @@ __host__ __device__ __forceinline__ int wide_groups(int N) {
   return ((N + kWave - 1) / kWave + kWideGroupSlots - 1) / kWideGroupSlots;
 }
 
-// Load the next-advert ticks of group g of this lane's view (issued before
-// the advert that changes one of its slots, so these loads overlap the
-// node-record load instead of queueing behind the advert's stores: gfx9's
-// vmcnt counts both).
-__device__ __forceinline__ void group_load(const WideView& V, int g, int64_t (&x)[kWideGroupSlots]) {
-#pragma unroll
-  for (int i = 0; i < kWideGroupSlots; ++i) x[i] = V.nxt[g * kWideGroupSlots + i];
-}
-
-// Earliest advert of group g of this lane from its loaded ticks (slot `sl`
-// replaced by the value just computed: its load was issued before the store).
-// Slots past N hold kNever, so they need no test.
-template <bool R>
-__device__ __forceinline__ void group_scan_nxt(const WideLds& L, int lane, int g, int sl, int64_t sl_nxt,
-                                               const int64_t (&x)[kWideGroupSlots]) {
-  int64_t mn = kNever;
-  int mj = lane;
-#pragma unroll
-  for (int i = 0; i < kWideGroupSlots; ++i) {
-    const int s = g * kWideGroupSlots + i;
-    const int64_t xi = s == sl ? sl_nxt : x[i];
-    if (xi < mn) {
-      mn = xi;
-      mj = wnode<R>(s, lane);
-    }
-  }
-  L.g_nxt[g * kWave + lane] = mn;
-  L.g_j[g * kWave + lane] = mj;
-}
-
 // Smallest view key (busy << 32 | node) of group g of this lane, from HBM
 // (slot sl's busy just stored by this lane).  Slots past N hold busy
 // 0xFFFFFFFF, above every admissible advertised busy time.
@@ -207,24 +173,6 @@ __device__ __forceinline__ uint64_t lane_min_key(const WideLds& L, int lane) {
     mk = key < mk ? key : mk;
   }
   return mk;
-}
-
-// The lane's earliest advert and smallest w in one pass over its groups.
-__device__ __forceinline__ void lane_min_nxt_w(const WideLds& L, int lane, int64_t& mn, int& mj, int64_t& mw) {
-  mn = kNever;
-  mj = lane;
-  mw = kNever;
-#pragma unroll 4
-  for (int g = 0; g < L.G; ++g) {
-    const int64_t x = L.g_nxt[g * kWave + lane];
-    const int jj = L.g_j[g * kWave + lane];
-    const int64_t w = L.g_w[g * kWave + lane];
-    if (x < mn) {
-      mn = x;
-      mj = jj;
-    }
-    mw = w < mw ? w : mw;
-  }
 }
 
 // The same over the groups with a pending advert only (bit g of ga; G <= 64): the
@@ -289,21 +237,6 @@ __device__ __forceinline__ int64_t node_w(const WideNode& h, int64_t nxt, int64_
   return nxt + ticks_of((uint32_t)(v1 < ((uint64_t)1 << 21) ? v1 : ((uint64_t)1 << 21)));
 }
 
-__device__ __forceinline__ void group_load_w(const WideView& V, int g, int64_t (&x)[kWideGroupSlots]) {
-#pragma unroll
-  for (int i = 0; i < kWideGroupSlots; ++i) x[i] = V.w[g * kWideGroupSlots + i];
-}
-
-// Group g's smallest w (slot sl replaced by the value just computed).
-__device__ __forceinline__ int64_t group_min_w(int g, int sl, int64_t sl_w, const int64_t (&x)[kWideGroupSlots]) {
-  int64_t mn = kNever;
-#pragma unroll
-  for (int i = 0; i < kWideGroupSlots; ++i) {
-    const int64_t xi = g * kWideGroupSlots + i == sl ? sl_w : x[i];
-    mn = xi < mn ? xi : mn;
-  }
-  return mn;
-}
 
 
 // Workspace layout (launch_replay_wide, replay_wide_workspace_bytes).
@@ -470,7 +403,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   int mj;
   uint64_t mk;
   lane_min(L, lane, mn, mj, mk);
-  uint64_t gact = 0ull;  // the lane's groups with a pending advert (FOGNET_WIDE_MASK)
+  uint64_t gact = 0ull;  // the lane's groups with a pending advert (lane minima visit only these)
   int64_t mw = kNever;  // REF_V3 run horizon: this lane's smallest node_w
   Acc acc = acc_identity();
   AbortPt ab = abort_none();  // the reference's abort point (replay_common.h)
@@ -787,46 +720,36 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           uint32_t busy_j;
           const bool hit = j == cj;
           const int g = sl / kWideGroupSlots;
-#if FOGNET_WIDE_MASK
           const int si = sl % kWideGroupSlots;
-          WideNode h;
-          int64_t dl_j, ul_j;
-          if (hit) {
-            h = ch;
-            dl_j = c_dl;
-            ul_j = c_ul;
-          } else {  // (waited for in this arm: sync_vm)
-            h = nd[j];
-            dl_j = P_dl[j];
-            ul_j = P_ul[j];
-            sync_vm();
-          }
-#else
-          int64_t gx[kWideGroupSlots], gw[kWideGroupSlots];
-          group_load(V, g, gx);
-          if constexpr (!kPerPublish) group_load_w(V, g, gw);
-          WideNode h = hit ? ch : nd[j];
-          const int64_t dl_j = hit ? c_dl : P_dl[j];
-          const int64_t ul_j = hit ? c_ul : P_ul[j];
-#endif
-          bool broken = false;
-          bool fits = apply_wide_advert(h, e, dl_j, ul_j, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
-          // node j's later adverts that are due too: adverts of different nodes commute (each
-          // sets only its node's view), so j's are applied now, in their order, and only the
-          // last one's view is stored and rescanned (no store between the dependent entry loads)
-          while (nxt_j < t && !broken) {
+          // node j's adverts that are due: adverts of different nodes commute (each sets only
+          // its node's view), so j's later due ones are applied now, in their order, and only
+          // the last one's view is stored and rescanned (no store between the dependent entry
+          // loads).  The cached record is updated in place (no copy through a merged value).
+          bool broken = false, fits = true;
+          int64_t w_j = kNever;
+          auto apply_due = [&](WideNode& hh, int64_t dl, int64_t ul) {
+            fits = apply_wide_advert(hh, e, dl, ul, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
+            while (nxt_j < t && !broken) {
 #ifdef FOGNET_WIDE_PROF
-            ++pf_same;
+              ++pf_same;
 #endif
-            fits &= apply_wide_advert(h, e, dl_j, ul_j, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
+              fits &= apply_wide_advert(hh, e, dl, ul, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
+            }
+            if constexpr (!kPerPublish) w_j = node_w(hh, nxt_j, dl);
+          };
+          if (hit) {
+            apply_due(ch, c_dl, c_ul);
+          } else {  // (waited for in this arm: sync_vm)
+            WideNode h = nd[j];
+            const int64_t dl_j = P_dl[j], ul_j = P_ul[j];
+            sync_vm();
+            apply_due(h, dl_j, ul_j);
+            nd[j] = h;
           }
           if constexpr (kExt) lerr |= !fits;
           lbroken |= broken;
-          if (hit) ch = h;
-          else nd[j] = h;
           V.nxt[sl] = nxt_j;
           V.busy[sl] = busy_j;
-#if FOGNET_WIDE_MASK
           // the earliest advert: j's was the lane's (so its group's), rescan both levels, the
           // group over its other pending slots only (ties: the smallest slot)
           const uint32_t gm0 = L.g_msk[g * kWave + lane];
@@ -834,10 +757,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           uint32_t gm = nxt_j != kNever ? gm0 | bit : gm0 & ~bit;
           gm = busy_j != 0u ? gm | (bit << 16) : gm & ~(bit << 16);
           L.g_msk[g * kWave + lane] = gm;
-          int64_t gmn = nxt_j, gmw = kNever;
+          int64_t gmn = nxt_j, gmw = w_j;
           int gsi = si;
-          if constexpr (!kPerPublish) gmw = node_w(h, nxt_j, dl_j);
-          if constexpr (!kPerPublish) V.w[sl] = gmw;
+          if constexpr (!kPerPublish) V.w[sl] = w_j;
           for (uint32_t m = gm0 & 0xFFFFu & ~bit; m; m &= m - 1u) {
             const int i = __builtin_ctz(m);
             const int64_t x = V.nxt[g * kWideGroupSlots + i];
@@ -858,18 +780,6 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           } else {
             lane_min_nxt_m(L, lane, gact, mn, mj);
           }
-#else
-          // the earliest advert: j's was the lane's (so its group's), rescan both levels
-          group_scan_nxt<kHier>(L, lane, g, sl, nxt_j, gx);
-          if constexpr (!kPerPublish) {
-            const int64_t w_j = node_w(h, nxt_j, dl_j);
-            V.w[sl] = w_j;
-            L.g_w[g * kWave + lane] = group_min_w(g, sl, w_j, gw);
-            lane_min_nxt_w(L, lane, mn, mj, mw);  // (one LDS pass for both lane minima)
-          } else {
-            lane_min_nxt(L, lane, mn, mj);
-          }
-#endif
 #ifdef FOGNET_WIDE_PROF
           pf_hit += hit ? 1u : 0u;
 #endif
@@ -877,13 +787,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           // when j held it and its busy time grew
           const uint64_t gk_old = L.g_key[g * kWave + lane];
           const uint64_t nk = ((uint64_t)busy_j << 32) | (uint32_t)j;
-#if FOGNET_WIDE_MASK
           const uint64_t gk_new = ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? group_key_m<kHier>(V, L, lane, g)
                                                                                  : (nk < gk_old ? nk : gk_old);
-#else
-          const uint64_t gk_new = ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? group_key<kHier>(V, lane, g)
-                                                                                 : (nk < gk_old ? nk : gk_old);
-#endif
 #ifdef FOGNET_WIDE_PROF
           pf_gkey += ((uint32_t)gk_old == (uint32_t)j && nk > gk_old) ? 1u : 0u;
 #endif
