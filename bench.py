@@ -559,7 +559,7 @@ def bench_c1(args, ctx, dev, dist, world, rank):
                        "R_total": args.R_total, "T_max": T, "N": n_nodes, "model": "BrokerBaseApp2 + ComputeBrokerApp2",
                        "parallelism": f"replications sharded over {world} GPU(s)"},
             "roofline": {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None,
-                         "traffic": None, "kernel": "replay_v2_rows_kernel (N <= 16: four replications per wavefront)",
+                         "traffic": None, "kernel": "replay_v2_rows_kernel<16, 2> (N <= 16: two replications per wavefront, two wavefronts per SIMD)",
                          "kernel_ms_per_step": kern_ms,
                          "events_per_s": events * args.steps / elapsed,
                          "note": "event-driven (~53 reference FES events per publish, counted in events_per_s; "

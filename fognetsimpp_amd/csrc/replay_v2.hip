@@ -615,15 +615,17 @@ __device__ __forceinline__ bool earlier32(int64_t t, uint32_t s, int64_t t2, uin
   return t < t2 || (t == t2 && s < s2);
 }
 
-template <int kRowLanes>
+template <int kRowLanes, int kActive = kWave / kRowLanes>
 __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
   constexpr int kRowsPerWave = kWave / kRowLanes;
   const fognet_v2_in& A = P.in;
   const fognet_v2_out& O = P.out;
   const int lane = threadIdx.x;
   const int li = lane & (kRowLanes - 1);
-  const int r = blockIdx.x * kRowsPerWave + lane / kRowLanes;
-  const bool live = r < A.R;  // rows past R idle from the start
+  // (kActive < kRowsPerWave: only the first kActive rows replay, the others idle -- more
+  // wavefronts, each issuing the union of fewer rows' paths)
+  const int r = blockIdx.x * kActive + lane / kRowLanes;
+  const bool live = lane / kRowLanes < kActive && r < A.R;  // rows past R idle from the start
   const int rr = live ? r : 0;  // (their addresses stay in bounds)
   const int N = A.N, T = A.T;
   const bool own = live && li < N;
@@ -1257,11 +1259,18 @@ hipError_t launch_replay_v2(const fognet_v2_in& in, const fognet_v2_out& out, vo
   a.outq = a.inq + q;
   a.res = reinterpret_cast<V2Res*>(a.outq + q);
   a.list = reinterpret_cast<uint8_t*>(a.res + q);
-  // rows of 16 lanes (four replications per wavefront) unless FOGNET_V2_ROW=32 (two) or N > 16
+  // rows of 16 lanes unless FOGNET_V2_ROW=32 (two replications per wavefront) or N > 16
   const char* rw = getenv("FOGNET_V2_ROW");
   const int row = (in.N > 16 || (rw && strcmp(rw, "32") == 0)) ? 32 : 16;
-  if (in.N <= 16 && row == 16)
+  // N <= 16: two replications per wavefront in rows 0-1 (rows 2-3 idle), i.e. two wavefronts
+  // per SIMD at the C1 size: 375 -> 360 ms against all four rows of one wavefront busy
+  // (FOGNET_V2_ACTIVE=4; one row per wavefront needs three generations of wavefronts at 164
+  // VGPRs, 546 ms)
+  const char* act = getenv("FOGNET_V2_ACTIVE");
+  if (in.N <= 16 && row == 16 && act && strcmp(act, "4") == 0)
     hipLaunchKernelGGL(replay_v2_rows_kernel<16>, dim3((in.R + 3) / 4), dim3(kWave), 0, s, a);
+  else if (in.N <= 16 && row == 16)
+    hipLaunchKernelGGL((replay_v2_rows_kernel<16, 2>), dim3((in.R + 1) / 2), dim3(kWave), 0, s, a);
   else if (in.N <= 32)
     hipLaunchKernelGGL(replay_v2_rows_kernel<32>, dim3((in.R + 1) / 2), dim3(kWave), 0, s, a);
   else if (in.N <= 64)

@@ -1129,11 +1129,14 @@ def test_v2_random_matches_oracle(ctx, seed, N, R):
     assert_v2_parity(g, o)
 
 
+@pytest.mark.parametrize("env", [("FOGNET_V2_ROW", "32"), ("FOGNET_V2_ACTIVE", "4")])
 @pytest.mark.parametrize("N", [5, 16])
-def test_v2_two_rows_per_wave_at_small_n(ctx, monkeypatch, N):
-    """FOGNET_V2_ROW=32 forces replay_v2_rows_kernel<32> (two replications per
-    wavefront) where N <= 16 would take the four-row kernel: same outputs."""
-    monkeypatch.setenv("FOGNET_V2_ROW", "32")
+def test_v2_two_rows_per_wave_at_small_n(ctx, monkeypatch, N, env):
+    """Where N <= 16 takes replay_v2_rows_kernel<16, 2> (16-lane rows, two of the
+    four busy), FOGNET_V2_ROW=32 forces replay_v2_rows_kernel<32> (two 32-lane
+    rows per wavefront) and FOGNET_V2_ACTIVE=4 all four 16-lane rows: same outputs
+    (R = 7: a wavefront with a row past R in every variant)."""
+    monkeypatch.setenv(*env)
     tr, broker, stop, rt = v2_random(40 + N, 7, N, 3000)
     g = run_v2_gpu(ctx, tr, broker, stop, rt, qcap=4096)
     o = ol.run_v2(tr["arrive"], tr["req"], broker, tr["mips"], tr["dl"], tr["ul"], tr["first_adv"], stop, rt,
