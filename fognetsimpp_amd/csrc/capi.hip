@@ -436,12 +436,13 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       // one wavefront per (replication, region) while no region escalates (replay_region.hip), the
       // statistics pass, then the sequential wide kernel for the replications some region handed back.
       // workspace: [hand-over counter | list [R] | region records [R][B] | entries [R][T] | node records
-      // [R][N]]; the hand-over launch reuses the space from the entries on (stream order: after the
-      // statistics pass has read the node records)
+      // [R][N] | busy view [R][B][1024]]; the hand-over launch reuses the space from the entries on
+      // (stream order: after the statistics pass has read the node records)
       const size_t o_rec = align256(256 + (size_t)a.R * sizeof(int32_t));
       const size_t o_e = o_rec + align256((size_t)a.R * (size_t)B * sizeof(fognet::RegionRec));
       const size_t o_nd = o_e + align256((size_t)a.R * (size_t)a.T * sizeof(fognet::WideEntry));
-      const size_t body = o_nd - o_e + (size_t)a.R * (size_t)a.N * sizeof(fognet::WideNode);
+      const size_t o_vb = o_nd + align256((size_t)a.R * (size_t)a.N * sizeof(fognet::WideNode));
+      const size_t body = o_vb - o_e + (size_t)a.R * (size_t)B * FOGNET_HIER_REGION_NODES * sizeof(uint32_t);
       const int32_t slots = fallback_slots(a.R, a.T, a.N, body, false);
       const size_t fb = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
       rc = ensure(c, (void**)&c->ring, &c->ring_bytes, o_e + (body > fb ? body : fb), "region replay workspace");
@@ -453,7 +454,8 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       if (e != hipSuccess) return hip_fail(c, e, "hand-over counter");
       const fognet::RegionWs w{reinterpret_cast<fognet::WideEntry*>(base + o_e),
                                reinterpret_cast<fognet::WideNode*>(base + o_nd),
-                               reinterpret_cast<fognet::RegionRec*>(base + o_rec), B};
+                               reinterpret_cast<fognet::RegionRec*>(base + o_rec),
+                               reinterpret_cast<uint32_t*>(base + o_vb), B};
       if (regions_only()) a.wide_list = nullptr;
       e = fognet::launch_replay_region(a, w, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(c, e, "region replay launch");

@@ -348,6 +348,7 @@ struct RegionWs {
   WideEntry* e;    // [R][T]
   WideNode* nd;    // [R][N]
   RegionRec* rec;  // [R][B]
+  uint32_t* vb;    // [R][B][16][64] advertised busy times (the region kernel's view, [slot][lane])
   int32_t B;       // regions: ceil(N / FOGNET_HIER_REGION_NODES)
 };
 hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s);

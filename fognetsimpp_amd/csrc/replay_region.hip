@@ -39,8 +39,8 @@ constexpr uint32_t kRegSCap = 1u << 22;  // the wide kernel's kWideSCap: past it
 // (fognet_hip.h never returns it; tests see it under FOGNET_HIER_REGIONS=only).
 constexpr int32_t kRegionSeq = 0x53455121;
 
-// 3 waves per SIMD: 12 KiB of LDS each (the region's view), <= 168 VGPRs.
-__global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, RegionWs W) {
+// 4 waves per SIMD: 8 KiB of LDS each (the view's ticks), <= 128 VGPRs.
+__global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, RegionWs W) {
   const int B = W.B;
   const int r = blockIdx.x / B, b = blockIdx.x - (blockIdx.x / B) * B;
   const int lane = threadIdx.x;
@@ -53,12 +53,13 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
   WideNode* const nd = W.nd + (size_t)r * (size_t)N;
   const int64_t arrive0 = T > 0 ? A.arrive[tbase] : kNever;
 
-  // ---- this lane's nodes (local l = s * 64 + lane) and their view in LDS ([slot][lane]: each lane
-  // touches only its own column, conflict-free)
+  // ---- this lane's nodes (local l = s * 64 + lane) and their view ([slot][lane]: each lane
+  // touches only its own column): next advert ticks in LDS (conflict-free); advertised busy
+  // times in HBM (RegionWs::vb; read back only by a key rescan of a lane without a zero-busy
+  // slot), so the LDS of a wavefront is 8 KiB: 20 fit per CU, and 4 per SIMD by VGPRs
   __shared__ int64_t s_nxt[kRegionSlots * kWave];
-  __shared__ uint32_t s_busy[kRegionSlots * kWave];
-  int64_t* const vnxt = s_nxt + lane;    // vnxt[s * kWave]: slot s of this lane
-  uint32_t* const vbusy = s_busy + lane;
+  int64_t* const vnxt = s_nxt + lane;  // vnxt[s * kWave]: slot s of this lane
+  uint32_t* const vbusy = W.vb + (size_t)blockIdx.x * (size_t)(kRegionSlots * kWave) + lane;
   bool bad = false;
   // slots with an advert pending (view tick not kNever) and slots whose advertised busy
   // time is not 0, as bit masks: the rescans below visit only the first kind, and a
@@ -104,10 +105,17 @@ __global__ __launch_bounds__(64, 3) void replay_region_kernel(ReplayArgs A, Regi
       return;
     }
     mk = ~0ull;
-#pragma unroll 4
-    for (int s = 0; s < kRegionSlots; ++s) {
-      const uint64_t key = ((uint64_t)vbusy[s * kWave] << 32) | (uint32_t)(base + s * kWave + lane);
-      mk = key < mk ? key : mk;
+#pragma unroll 1
+    for (int s0 = 0; s0 < kRegionSlots; s0 += 8) {  // (8 loads in flight: few registers)
+      uint32_t bv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) bv[u] = vbusy[(s0 + u) * kWave];
+      sync_vm();  // (in this arm: see sync_vm)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint64_t key = ((uint64_t)bv[u] << 32) | (uint32_t)(base + (s0 + u) * kWave + lane);
+        mk = key < mk ? key : mk;
+      }
     }
   };
 
