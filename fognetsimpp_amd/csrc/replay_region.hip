@@ -329,12 +329,13 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   if (lane == 0) W.rec[blockIdx.x] = RegionRec{n_done, (int32_t)mp, (int32_t)err, 0};
 }
 
-// Per replication (256 threads): the regions' records merged, then the
-// statistics pass over the outputs (stats_accumulate, the fused epilogue's
-// code) with busy seconds, `last` and the a11 energy from the node records
-// (the tail's cumulative service and completion: FIFO), summed in node order
-// exactly as replay_wide.hip does.  A replication some region could not finish
-// goes to the hand-over list instead.
+// Per replication (256 threads): the regions' records merged, the node tails'
+// busy seconds and last completion (FIFO: the tail's cumulative service and
+// completion), then the statistics pass over the outputs (stats_accumulate, the
+// fused epilogue's code) by waves 1-3 while wave 0 sums the a11 energy in node
+// order (replay_wide.hip's order): the energy's serial chain needs only the last
+// completion.  A replication some region could not finish goes to the hand-over
+// list instead.
 constexpr int kFinThreads = 256;
 
 __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A, RegionWs W) {
@@ -342,12 +343,16 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   const int tid = threadIdx.x;
   const int B = W.B, N = A.N;
   constexpr int kFinWaves = kFinThreads / kWave;
+  constexpr int kStatThreads = kFinThreads - kWave;  // waves 1..3
   // (per-wave partial records: 4 x 152 B of LDS, so many blocks fit per CU)
   __shared__ Acc s_acc[kFinWaves];
   __shared__ int64_t s_abt[kFinThreads];
   __shared__ int32_t s_abk[kFinThreads];
   __shared__ uint32_t s_hist[FOGNET_HIST_METRICS * FOGNET_HIST_BINS];
   __shared__ int s_ok, s_done, s_mp;
+  __shared__ double s_energy;
+  __shared__ uint64_t s_busy;
+  __shared__ int64_t s_last;
   if (tid < kWave) {  // the regions' records, one per lane (B <= 64: N <= 65,536)
     RegionRec x{0, 0, FOGNET_OK, 0};
     if (tid < B) x = W.rec[(size_t)r * B + tid];
@@ -376,11 +381,8 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   for (int h = tid; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kFinThreads) s_hist[h] = 0u;
   s_abt[tid] = INT64_MAX;
   s_abk[tid] = INT32_MAX;
-  __syncthreads();
-  Acc a = acc_identity();
-  stats_accumulate<2, false>(A, tbase, n, tid, kFinThreads, a, nullptr, s_hist,
-                             [&](int k) { return A.dl[nbase + k]; }, s_abt, s_abk);
   // busy seconds and the last completion from the node tails (2 records in flight per thread)
+  Acc a = acc_identity();
   for (int j0 = tid; j0 < N; j0 += 2 * kFinThreads) {
     WideNode x[2];
 #pragma unroll
@@ -397,39 +399,60 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
     }
   }
   a = wave_merge(a);
-  const AbortPt ab_w = wave_min_abort(AbortPt{s_abt[tid], s_abk[tid]});  // (each thread's own slot)
-  if ((tid & (kWave - 1)) == 0) {
-    s_acc[tid / kWave] = a;
-    s_abt[tid] = ab_w.tick;
-    s_abk[tid] = ab_w.task;
+  if ((tid & (kWave - 1)) == 0) s_acc[tid / kWave] = a;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t busy = 0u;
+    int64_t last = INT64_MIN;
+    for (int w = 0; w < kFinWaves; ++w) {
+      busy += s_acc[w].busy;
+      last = max(last, s_acc[w].last);
+    }
+    s_busy = busy;
+    s_last = last;
+  }
+  __syncthreads();  // (s_acc is reused below)
+  if (tid < kWave) {
+    // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12), summed in
+    // node order (64 nodes at a time, then lane by lane) while waves 1-3 run the statistics pass
+    if (A.p_busy) {  // (an unused node's record has tl_C = 0)
+      const int64_t H = n > 0 ? s_last : 0;
+      const double sum = energy_sum_wave(nd, A.p_busy + nbase, A.p_idle + nbase, N, H,
+                                         A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, tid);
+      if (tid == 0) s_energy = sum;
+    }
+  } else {
+    Acc b = acc_identity();
+    stats_accumulate<2, false>(A, tbase, n, tid - kWave, kStatThreads, b, nullptr, s_hist,
+                               [&](int k) { return A.dl[nbase + k]; }, s_abt + kWave, s_abk + kWave);
+    b = wave_merge(b);
+    const AbortPt ab_w = wave_min_abort(AbortPt{s_abt[tid], s_abk[tid]});  // (each thread's own slot)
+    if ((tid & (kWave - 1)) == 0) {
+      s_acc[tid / kWave] = b;
+      s_abt[tid] = ab_w.tick;
+      s_abk[tid] = ab_w.task;
+    }
   }
   __syncthreads();
   if (tid == 0) {
-    Acc t = s_acc[0];
-    AbortPt ab = AbortPt{s_abt[0], s_abk[0]};
-    for (int w = 1; w < kFinWaves; ++w) {
+    Acc t = s_acc[1];
+    AbortPt ab = AbortPt{s_abt[kWave], s_abk[kWave]};
+    for (int w = 2; w < kFinWaves; ++w) {
       acc_merge(t, s_acc[w]);
       abort_min(ab.tick, ab.task, s_abt[w * kWave], s_abk[w * kWave]);
     }
-    s_acc[0] = t;
+    t.busy = s_busy;  // (the node tails': the statistics pass adds none)
+    t.last = s_last;
     S->n_tasks = n;
     S->max_pending = s_mp;
     S->status = FOGNET_OK;
     S->events = 2 * (int64_t)N + 4 * (int64_t)n;  // initial adverts + publish, arrival, release, advert per task
     write_rep_stats(S, t, ab, A.ref_abort);
+    if (A.p_busy) S->energy_j = s_energy;
   }
-  __syncthreads();  // (s_acc[0].last: the energy's horizon)
   if (A.hist) {
     for (int h = tid; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kFinThreads)
       if (s_hist[h]) atomicAdd((unsigned long long*)&A.hist[h], (unsigned long long)s_hist[h]);
-  }
-  // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12), summed in node
-  // order by the first wave (replay_wide.hip's order: 64 nodes at a time, then lane by lane)
-  if (A.p_busy && tid < kWave) {  // (an unused node's record has tl_C = 0)
-    const int64_t H = n > 0 ? s_acc[0].last : 0;
-    const double sum = energy_sum_wave(nd, A.p_busy + nbase, A.p_idle + nbase, N, H,
-                                       A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, tid);
-    if (tid == 0) S->energy_j = sum;
   }
 }
 
