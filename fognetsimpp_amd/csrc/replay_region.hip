@@ -39,10 +39,25 @@ constexpr uint32_t kRegSCap = 1u << 22;  // the wide kernel's kWideSCap: past it
 // (fognet_hip.h never returns it; tests see it under FOGNET_HIER_REGIONS=only).
 constexpr int32_t kRegionSeq = 0x53455121;
 
+#ifndef FOGNET_REGION_XCD
+#define FOGNET_REGION_XCD 0
+#endif
+
 // 4 waves per SIMD: 8 KiB of LDS each (the view's ticks), <= 128 VGPRs.
 __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, RegionWs W) {
   const int B = W.B;
+#if FOGNET_REGION_XCD
+  // XCD-aware order: workgroup x runs on XCD x % 8 (round robin), so replication r's B
+  // region wavefronts get x = r % 8 + 8 (B (r / 8) + b): one XCD, consecutive there (they
+  // all read r's trace, which then comes from that XCD's L2).  The grid covers R rounded
+  // up to 8 replications; the extra workgroups leave at once.
+  const int x8 = blockIdx.x & 7, sx = blockIdx.x >> 3;
+  const int r = x8 + 8 * (sx / B), b = sx - (sx / B) * B;
+  if (r >= A.R) return;
+#else
   const int r = blockIdx.x / B, b = blockIdx.x - (blockIdx.x / B) * B;
+#endif
+  const int rb = r * B + b;  // (r, b)'s region record and busy view
   const int lane = threadIdx.x;
   const int T = A.T, N = A.N;
   const int base = b * FOGNET_HIER_REGION_NODES;
@@ -59,7 +74,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   // slot), so the LDS of a wavefront is 8 KiB: 20 fit per CU, and 4 per SIMD by VGPRs
   __shared__ int64_t s_nxt[kRegionSlots * kWave];
   int64_t* const vnxt = s_nxt + lane;  // vnxt[s * kWave]: slot s of this lane
-  uint32_t* const vbusy = W.vb + (size_t)blockIdx.x * (size_t)(kRegionSlots * kWave) + lane;
+  uint32_t* const vbusy = W.vb + (size_t)rb * (size_t)(kRegionSlots * kWave) + lane;
   bool bad = false;
   // slots with an advert pending (view tick not kNever) and slots whose advertised busy
   // time is not 0, as bit masks: the rescans below visit only the first kind, and a
@@ -326,7 +341,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
            (int)blockIdx.x, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[8], pr[9], pr[10], pr[11], pr[12]);
 #endif
   const uint32_t mp = ~wave_min_u32(~max_pend);
-  if (lane == 0) W.rec[blockIdx.x] = RegionRec{n_done, (int32_t)mp, (int32_t)err, 0};
+  if (lane == 0) W.rec[rb] = RegionRec{n_done, (int32_t)mp, (int32_t)err, 0};
 }
 
 // Per replication (256 threads): the regions' records merged, the node tails'
@@ -459,7 +474,11 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
 }  // namespace
 
 hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s) {
+#if FOGNET_REGION_XCD
+  hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)((a.R + 7) / 8 * 8) * (unsigned)w.B), dim3(kWave), 0, s, a, w);
+#else
   hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w);
+#endif
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(region_finish_kernel, dim3(a.R), dim3(kFinThreads), 0, s, a, w);
