@@ -107,6 +107,9 @@ def main():
                     help="default REF_V3; c5: EXT_HIER (hierarchical brokers + mobility handoff, BASELINE configs[4])")
     ap.add_argument("--hier-threshold-s", type=int, default=60)
     ap.add_argument("--hier-up-ms", type=int, default=20)
+    ap.add_argument("--c5-recipe", default="light", choices=("light", "saturate"),
+                    help="c5: 'light' = fa.c5_params (device-generated; no region escalates), 'saturate' = "
+                         "fa.saturating_trace (host-built, T = 32,768: every region saturates and escalates)")
     ap.add_argument("--workload", default="c3", choices=("c1", "c3", "c4", "c5"))
     ap.add_argument("--R-total", type=int, default=None,
                     help="c4/c5: replications over all ranks (default 1,000,000 / 1024)")
@@ -118,7 +121,7 @@ def main():
         args.policy = "EXT_HIER" if args.workload == "c5" else "REF_V3"
     if args.workload in ("c4", "c5"):
         if args.T == 100_000:
-            args.T = 10_000
+            args.T = 32_768 if args.workload == "c5" and args.c5_recipe == "saturate" else 10_000
         if args.seed == 0x5EED0003:
             args.seed = 0x5EED0004 if args.workload == "c4" else 0x5EED0005
         if args.R_total is None:
@@ -167,11 +170,14 @@ def main():
         r0 = rank * R
         mg, sc = fa.sweep_params(np.arange(r0, r0 + R), N)
     t0 = time.time()
-    trace = fa.generate_trace(ctx, args.seed, R, T, N, mg, sc, r0=r0)
+    if args.workload == "c5" and args.c5_recipe == "saturate":
+        trace = fa.as_device_trace(fa.saturating_trace(args.seed, R, T, N, r0=r0), dev)
+    else:
+        trace = fa.generate_trace(ctx, args.seed, R, T, N, mg, sc, r0=r0)
     pb, pi = fa.power_model(trace["mips"].cpu().numpy())
     trace["p_busy"] = torch.from_numpy(pb).to(dev)
     trace["p_idle"] = torch.from_numpy(pi).to(dev)
-    if args.policy == "EXT_HIER":  # each publish's regional broker under the mobility model
+    if args.policy == "EXT_HIER" and "region" not in trace:  # each publish's regional broker (mobility model)
         trace["region"] = fa.mobility_regions(trace["arrive"], N)
     hier = dict(hier_threshold_s=args.hier_threshold_s, hier_up_tick=args.hier_up_ms * 10**9)
     out = fa.allocate_outputs(R, T, dev, N=N, energy=False, hist=True)
@@ -259,6 +265,16 @@ def main():
         except Exception:
             traffic = None
     ref = reference_prefix(rep, trace["arrive"])
+    hier_esc = None
+    if args.policy == "EXT_HIER" and N > _abi.HIER_REGION_NODES:
+        # escalations of the last step: a publish escalated iff its node lies outside its regional broker's
+        # region; a replication with any is handed back by the region pass to the sequential wide kernel
+        esc = (out.node // _abi.HIER_REGION_NODES) != trace["region"]
+        n_rep = torch.tensor([int(esc.any(dim=1).sum().item()), int(esc.sum().item())], dtype=torch.int64, device=dev)
+        if dist is not None:
+            dist.all_reduce(n_rep)
+        hier_esc = {"escalating_replications": int(n_rep[0]), "escalating_fraction": int(n_rep[0]) / args.R_total,
+                    "escalated_publishes": int(n_rep[1]), "threshold_s": args.hier_threshold_s}
     if dist is not None:  # job totals over the ranks' shards
         tot = torch.tensor([ref["ref_defined_decisions"], ref["ref_aborted_replications"], ref["replications"]],
                            dtype=torch.int64, device=dev)
@@ -288,8 +304,10 @@ def main():
             "scaling": "strong" if args.workload == "c5" else "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (device-generated Philox traces, "
-                    + ("C5 light-load recipe)" if args.workload == "c5" else "C3 policy-sweep recipe)"),
+            "data": ("synthetic (host-built fa.saturating_trace: every region saturates, escalations to the parent)"
+                     if args.workload == "c5" and args.c5_recipe == "saturate" else
+                     "synthetic (device-generated Philox traces, "
+                     + ("C5 light-load recipe)" if args.workload == "c5" else "C3 policy-sweep recipe)")),
             "config": {"workload": "C5 large topology (BASELINE.json configs[4])" if args.workload == "c5"
                        else "C3 policy sweep (BASELINE.json configs[2])", "R_per_gpu": R, "T": T, "N": N,
                        "R_total": args.R_total if args.workload == "c5" else R * world, "ring_capacity": args.ring,
@@ -302,13 +320,16 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": ("replay_region_kernel (one wavefront per regional broker) + region_finish_kernel "
-                                    "(statistics pass)" if args.policy == "EXT_HIER" and N > _abi.HIER_REGION_NODES
+                                    "(statistics pass)" + (" + replay_wide_kernel (the sequential replay of the handed-"
+                                                           "back replications)" if args.c5_recipe == "saturate" else "")
+                                    if args.policy == "EXT_HIER" and N > _abi.HIER_REGION_NODES
                                     else "replay_wide_kernel (statistics inline)" if N > 256
                                     else "replay_kernel (statistics pass fused)"), "kernel_avg_ms": replay_avg_s * 1e3,
                          "bytes_per_decision": bpd, "bytes_per_decision_source": "SURVEY.md §8(d)",
                          "valu_issue": valu},
             "cpu_baseline": cpu,
             "failed_replications": failed,
+            "hier_escalation": hier_esc,
             # the reference run of a replication ends at its first overflowing queueTime emission
             # (ComputeBrokerApp3.cc:238, no handler): what it defines is the prefix up to that tick; the
             # decisions after it are the engine's extension (fognet_hip.h "Reference signal values")

@@ -349,6 +349,8 @@ struct RegionWs {
   WideNode* nd;    // [R][N]
   RegionRec* rec;  // [R][B]
   uint32_t* vb;    // [R][B][16][64] advertised busy times (the region kernel's view, [slot][lane])
+  int32_t* quit;   // [R] zeroed before the launch: set when a region of r hands it back, so r's other
+                   // region wavefronts stop early (the sequential kernel replays r from the start)
   int32_t B;       // regions: ceil(N / FOGNET_HIER_REGION_NODES)
 };
 hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s);

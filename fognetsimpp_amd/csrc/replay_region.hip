@@ -38,25 +38,12 @@ constexpr uint32_t kRegSCap = 1u << 22;  // the wide kernel's kWideSCap: past it
 // Internal per-(replication, region) status: replay the replication sequentially
 // (fognet_hip.h never returns it; tests see it under FOGNET_HIER_REGIONS=only).
 constexpr int32_t kRegionSeq = 0x53455121;
-
-#ifndef FOGNET_REGION_XCD
-#define FOGNET_REGION_XCD 0
-#endif
+constexpr int kQuitEvery = 4;  // chunks between polls of the replication's quit flag
 
 // 4 waves per SIMD: 8 KiB of LDS each (the view's ticks), <= 128 VGPRs.
 __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, RegionWs W) {
   const int B = W.B;
-#if FOGNET_REGION_XCD
-  // XCD-aware order: workgroup x runs on XCD x % 8 (round robin), so replication r's B
-  // region wavefronts get x = r % 8 + 8 (B (r / 8) + b): one XCD, consecutive there (they
-  // all read r's trace, which then comes from that XCD's L2).  The grid covers R rounded
-  // up to 8 replications; the extra workgroups leave at once.
-  const int x8 = blockIdx.x & 7, sx = blockIdx.x >> 3;
-  const int r = x8 + 8 * (sx / B), b = sx - (sx / B) * B;
-  if (r >= A.R) return;
-#else
   const int r = blockIdx.x / B, b = blockIdx.x - (blockIdx.x / B) * B;
-#endif
   const int rb = r * B + b;  // (r, b)'s region record and busy view
   const int lane = threadIdx.x;
   const int T = A.T, N = A.N;
@@ -171,6 +158,12 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
 #endif
 
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
+    // another region of r handed it back: the sequential kernel replays r from the start
+    if ((c0 & (kQuitEvery * kWave - 1)) == 0 && c0 > 0 &&
+        __hip_atomic_load(W.quit + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+      err = kRegionSeq;
+      break;
+    }
     const int cnt = min(kWave, T - c0);
     const bool live = lane < cnt;
     const int64_t ca = live ? A.arrive[tbase + c0 + lane] : kNever;
@@ -341,7 +334,10 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
            (int)blockIdx.x, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[8], pr[9], pr[10], pr[11], pr[12]);
 #endif
   const uint32_t mp = ~wave_min_u32(~max_pend);
-  if (lane == 0) W.rec[rb] = RegionRec{n_done, (int32_t)mp, (int32_t)err, 0};
+  if (lane == 0) {
+    if (err != FOGNET_OK) __hip_atomic_store(W.quit + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    W.rec[rb] = RegionRec{n_done, (int32_t)mp, (int32_t)err, 0};
+  }
 }
 
 // Per replication (256 threads): the regions' records merged, the node tails'
@@ -381,9 +377,10 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
     }
   }
   __syncthreads();
-  if (!s_ok) {  // (the sequential replay overwrites the record; FOGNET_HIER_REGIONS=only leaves this status)
+  if (!s_ok) {  // the sequential replay overwrites the record
     if (tid == 0) {
-      A.out_stats[r].status = kRegionSeq;
+      // (FOGNET_HIER_REGIONS=only: no hand-over list, the replication stays unreplayed)
+      A.out_stats[r].status = A.wide_list ? kRegionSeq : FOGNET_ERR_UNSUPPORTED;
       if (A.wide_list) A.wide_list[atomicAdd(A.wide_count, 1)] = r;
     }
     return;
@@ -474,11 +471,7 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
 }  // namespace
 
 hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s) {
-#if FOGNET_REGION_XCD
-  hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)((a.R + 7) / 8 * 8) * (unsigned)w.B), dim3(kWave), 0, s, a, w);
-#else
   hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w);
-#endif
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(region_finish_kernel, dim3(a.R), dim3(kFinThreads), 0, s, a, w);

@@ -564,6 +564,101 @@ def mobility_regions(arrive, N: int, users: int = 256, period_s=(30, 45, 60, 75)
     return reg.to(torch.int32) if torch_in else reg.astype(np.int32)
 
 
+def _saturation_template(arrive0: np.ndarray, region: np.ndarray, sizes: list[int], lat_max: int):
+    """Roles of the publishes of one region sequence (saturating_trace): per
+    region, walk its publishes; a free publish p starts a pair on the region's
+    next fresh node (small task of S1 seconds, the region's next publish q a
+    giant task), S1 the smallest whole second above q's gap, so q reaches the
+    node before p completes; every publish up to p's completion advert (S1 + the
+    link latencies, bounded by ``lat_max``) is a zero-service filler.  Once every
+    node of the region has its pair, the publishes are zero-service tasks, which
+    the saturated regional broker escalates.
+    Returns role [T] (0 filler / escalation, 1 small, 2 giant), the pair's node
+    offset within its region [T] (-1 for fillers) and S1 [T]."""
+    T = arrive0.shape[0]
+    role = np.zeros(T, np.int8)
+    node = np.full(T, -1, np.int64)
+    s1 = np.zeros(T, np.int64)
+    tps = TICKS_PER_SECOND_I
+    for b, size in enumerate(sizes):
+        idx = np.flatnonzero(region == b)
+        m = 0
+        i = 0
+        while i + 1 < len(idx) and m < size:
+            p, q = idx[i], idx[i + 1]
+            S1 = (int(arrive0[q]) - int(arrive0[p])) // tps + 1
+            role[p], role[q] = 1, 2
+            node[p] = node[q] = m
+            s1[p] = S1
+            adv = int(arrive0[p]) + S1 * tps + lat_max  # the advert has reached the broker by then
+            i += 2
+            while i < len(idx) and int(arrive0[idx[i]]) <= adv:
+                i += 1
+            m += 1
+    return role, node, s1
+
+
+TICKS_PER_SECOND_I = 10**12
+
+
+def saturating_trace(seed: int, R: int, T: int, N: int, gap_s: float = 0.1, giant_s=(4000, 6000),
+                     users: int = 256, lat_ticks=(10**9, 10**10), escalate=None, r0: int = 0) -> dict:
+    """Builder-defined overload recipe for EXT_HIER at the C5 topology, host
+    numpy (the reference has no hierarchy; DESIGN.md §3.8 "Escalations at
+    N = 10,000").  Under the reference's stale view a regional broker herds its
+    publishes onto its lowest-index node until that node's first completion
+    advert arrives (BrokerBaseApp3.cc:123-130, 265-281), and it escalates only
+    when every node of its region advertises more than the threshold, so an
+    i.i.d. trace needs ~1024^2 publishes per region to saturate one.  This trace
+    saturates every region within ~3 publishes per node: each node gets one
+    pair -- a short task, then a giant one (giant_s seconds, more than the whole
+    filling phase) that reaches it before the short one completes, so its first
+    advert carries the giant's backlog -- and zero-service fillers until that
+    advert lands; afterwards every publish is a zero-service task escalated to
+    the parent's global argmin (the smallest advertised giant).  Publishes every
+    ``gap_s`` seconds (plus jitter), regions from :func:`mobility_regions`
+    (``users`` users), per-node link latencies in ``lat_ticks``, MIPS
+    1000 * (1 + j % 4).  The publish ticks and regions are shared by all
+    replications; global replication r0 + i gets its own giants and latencies
+    (Philox-free numpy streams keyed by (seed, r0 + i), so a shard equals the
+    same rows of the whole job), and its smallest giant sits in region
+    3 + (r0 + i) % 7 (B = 10), so escalations land in the wide kernel's upper
+    rows.  ``escalate`` ([R] bools, default all): a replication given False
+    gets 30-s tasks instead of giants, so its nodes advertise at most 30 s
+    (below the bench's 60-s threshold) and no region escalates (the region pass
+    finishes it).  Returns host arrays (make_batch layout) + ``region`` [R, T]."""
+    tps = TICKS_PER_SECOND_I
+    B = -(-N // _abi.HIER_REGION_NODES)
+    sizes = [min(_abi.HIER_REGION_NODES, N - b * _abi.HIER_REGION_NODES) for b in range(B)]
+    lo, hi = lat_ticks
+    shared = np.random.default_rng([seed & 0xFFFFFFFF, T, N])
+    g = int(gap_s * tps)
+    base = 2 * hi  # after every first advert (init = ul < hi)
+    arrive0 = base + np.arange(T, dtype=np.int64) * g + shared.integers(0, g // 2, size=T, dtype=np.int64)
+    region0 = mobility_regions(arrive0[None, :], N, users=users)[0]
+    role, off, s1 = _saturation_template(arrive0, region0, sizes, 2 * hi)
+    k = np.where(off >= 0, region0.astype(np.int64) * _abi.HIER_REGION_NODES + off, 0)
+    mips1 = (1000 * (1 + np.arange(N) % 4)).astype(np.int32)
+    mk = mips1[k].astype(np.int64)  # [T]: the MIPS of the pair's node
+    esc = np.ones(R, bool) if escalate is None else np.asarray(escalate, bool)
+    dl = np.empty((R, N), np.int64)
+    ul = np.empty((R, N), np.int64)
+    req = np.empty((R, T), np.int32)
+    for i in range(R):
+        rng = np.random.default_rng([seed & 0xFFFFFFFF, r0 + i])
+        dl[i] = rng.integers(lo, hi, size=N, dtype=np.int64)
+        ul[i] = rng.integers(lo, hi, size=N, dtype=np.int64)
+        giant = rng.integers(giant_s[0] + 1, giant_s[1], size=N, dtype=np.int64)
+        b = (3 + (r0 + i) % 7) % B  # the smallest giant of this replication
+        giant[b * _abi.HIER_REGION_NODES + int(rng.integers(0, sizes[b]))] = giant_s[0]
+        if not esc[i]:
+            giant[:] = 30
+        zero = rng.integers(0, 1000, size=T, dtype=np.int64)  # below every MIPS: zero service
+        req[i] = np.where(role == 1, s1 * mk, np.where(role == 2, giant[k] * mk, zero))
+    return dict(arrive=np.broadcast_to(arrive0, (R, T)).copy(), req=req, mips=np.broadcast_to(mips1, (R, N)).copy(),
+                dl=dl, ul=ul, init=ul.copy(), region=np.broadcast_to(region0, (R, T)).copy())
+
+
 def power_model(mips) -> tuple[np.ndarray, np.ndarray]:
     """Synthetic node power model for the a11 energy statistic (builder-defined;
     the reference has no fog-node energy model): busy power

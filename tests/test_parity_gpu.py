@@ -1380,10 +1380,12 @@ def test_hier_region_pass_and_handover(ctx, monkeypatch):
     reg = np.zeros_like(tr["req"])
     reg[1::2, 1::2] = 1
     reg[0, 5::7] = 1
-    tr = dict(tr, region=reg)
+    pb, pi = fa.power_model(tr["mips"])
+    tr = dict(tr, region=reg, p_busy=pb, p_idle=pi)
     kw = dict(policy="EXT_HIER", hier_threshold_s=0, hier_up_tick=10**12, hist=True)
     o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=6, hist=True,
-                     policy=ol.POLICY_EXT_HIER, region=reg, hier_threshold_s=0, hier_up_tick=10**12)
+                     policy=ol.POLICY_EXT_HIER, region=reg, hier_threshold_s=0, hier_up_tick=10**12,
+                     p_busy=pb, p_idle=pi)
     esc = (o["node"] // _abi.HIER_REGION_NODES != reg).sum(axis=1)
     assert list(esc > 0) == [False] * 5 + [True]
     dev = torch.device("cuda", ctx.device)
@@ -1396,6 +1398,7 @@ def test_hier_region_pass_and_handover(ctx, monkeypatch):
     for k, gk in (("node", out.node), ("status", out.status), ("start", out.start_tick), ("done", out.done_tick)):
         np.testing.assert_array_equal(gk.cpu().numpy()[:5], o[k][:5], err_msg=k)
     assert st[:5].tobytes() == o["stats"][:5].tobytes()
+    np.testing.assert_array_equal(out.node_energy.cpu().numpy()[:5], o["node_energy"][:5])
     np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"][:5].sum(axis=0))
     for mode in ("1", "0"):
         monkeypatch.setenv("FOGNET_HIER_REGIONS", mode)
@@ -1406,6 +1409,7 @@ def test_hier_region_pass_and_handover(ctx, monkeypatch):
         assert (g["stats"]["status"] == 0).all()
         assert_parity(tr, g, o)
         assert out.rep_stats().tobytes() == o["stats"].tobytes()
+        np.testing.assert_array_equal(out.node_energy.cpu().numpy(), o["node_energy"])
         np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
 
 
@@ -1518,3 +1522,75 @@ def test_c5_ext_hier_as_named(ctx, monkeypatch, mode):
     assert (o["node"] // _abi.HIER_REGION_NODES == h["region"]).all()  # (no escalation, see above)
     # every region's broker placed tasks
     assert len(np.unique(o["node"] // _abi.HIER_REGION_NODES)) == 10
+
+
+@pytest.fixture(scope="module")
+def c5_saturated():
+    """Eight C5-topology replications (N = 10,000 in 10 regions, mobility_regions,
+    T = 32,768) of fa.saturating_trace: six saturate every region and escalate
+    (~7,900 publishes each, from all ten regional brokers, to the parent's
+    global argmin in rows 0 and 3-8 of the wide kernel), two stay below the
+    threshold.  The oracle run (power model, histograms) is shared."""
+    R, T, N = 8, 32_768, 10_000
+    tr = fa.saturating_trace(11, R, T, N, escalate=[True] * 6 + [False] * 2)
+    pb, pi = fa.power_model(tr["mips"])
+    tr = dict(tr, p_busy=pb, p_idle=pi)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8, hist=True,
+                     policy=ol.POLICY_EXT_HIER, region=tr["region"], hier_threshold_s=60, hier_up_tick=20 * 10**9,
+                     p_busy=pb, p_idle=pi)
+    return tr, o
+
+
+def test_c5_saturated_trace_escalates_everywhere(c5_saturated):
+    """The oracle's side of the escalation tests below: escalations originate in
+    every region (rows 0-9 of the wide kernel's rotated lanes), land in rows 0
+    and 3..8 (the parent's smallest advertised giant, placed in region 3 + r %
+    7), and the non-escalating replications none."""
+    tr, o = c5_saturated
+    reg, node = tr["region"], o["node"]
+    esc = node // _abi.HIER_REGION_NODES != reg
+    n_esc = esc.sum(axis=1)
+    assert (n_esc[:6] > 5000).all() and (n_esc[6:] == 0).all()
+    assert set(np.unique(reg[esc])) == set(range(10))
+    dest = set(np.unique(node[esc] // _abi.HIER_REGION_NODES))
+    assert {3, 4, 5, 6, 7, 8} <= dest
+    for r in range(6):
+        assert (3 + r % 7) in set(np.unique(node[r][esc[r]] // _abi.HIER_REGION_NODES))
+    assert (o["stats"]["status"] == 0).all() and (o["stats"]["n_qtime_overflow"] == 0).all()
+
+
+@pytest.mark.parametrize("mode", ["1", "0", "only"])
+def test_c5_ext_hier_escalations(ctx, monkeypatch, c5_saturated, mode):
+    """EXT_HIER at the C5 topology WITH escalations: every
+    output, record (a11 energy included), per-node energy and histogram bin
+    against the oracle.  mode "1" (default): the region pass finishes the two
+    non-escalating replications and hands the six others to the sequential wide
+    kernel, which replays them from the start (regional argmin per region,
+    BrokerBaseApp3.cc:267-281; node FIFO of any length, ComputeBrokerApp3.cc:
+    305-309; escalated tasks of all ten rows); "0": the sequential kernel for all
+    eight; "only": the region pass alone -- the two finished replications equal
+    the oracle, the six others report FOGNET_ERR_UNSUPPORTED."""
+    tr, o = c5_saturated
+    monkeypatch.setenv("FOGNET_HIER_REGIONS", mode)
+    dev = torch.device("cuda", ctx.device)
+    out = fa.run_batch(ctx, fa.as_device_trace(tr, dev), policy="EXT_HIER", hier_threshold_s=60,
+                       hier_up_tick=20 * 10**9, hist=True)
+    torch.cuda.synchronize()
+    st = out.rep_stats()
+    g = dict(node=out.node.cpu().numpy(), status=out.status.cpu().numpy(), start=out.start_tick.cpu().numpy(),
+             done=out.done_tick.cpu().numpy(), stats=st)
+    energy = out.node_energy.cpu().numpy()
+    if mode == "only":
+        assert list(st["status"]) == [_abi.FOGNET_ERR_UNSUPPORTED] * 6 + [0, 0]
+        keep = slice(6, 8)
+        for k in ("node", "status", "start", "done"):
+            np.testing.assert_array_equal(g[k][keep], o[k][keep], err_msg=k)
+        assert st[keep].tobytes() == o["stats"][keep].tobytes()
+        np.testing.assert_array_equal(energy[keep], o["node_energy"][keep])
+        np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"][keep].sum(axis=0))
+        return
+    assert (st["status"] == 0).all()
+    assert_parity(tr, g, o)
+    assert st.tobytes() == o["stats"].tobytes()
+    np.testing.assert_array_equal(energy, o["node_energy"])
+    np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))

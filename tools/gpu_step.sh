@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU call of round 5: steps named in STEPS (space-separated), each under its own time limit,
+# stopping at the first failure.  Outputs under gpurun_out/r5/.
+#   tests:<pytest -k expr>   GPU tests matching the expression
+#   suite                    the whole GPU suite
+#   bench:<name>:<args>      one bench.py line (args with '+' for spaces) -> <name>.json
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r5; mkdir -p $O
+export TMPDIR=/tmp
+for s in $STEPS; do
+  echo "== $s $(date +%T)"
+  case "$s" in
+    tests:*)
+      k="${s#tests:}"; k="${k//+/ }"
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$k" > $O/pytest_k.log 2>&1 || { tail -40 $O/pytest_k.log; exit 1; }
+      tail -n 3 $O/pytest_k.log ;;
+    suite)
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+      tail -n 2 $O/pytest_gpu.log ;;
+    bench:*)
+      r="${s#bench:}"; name="${r%%:*}"; a="${r#*:}"; a="${a//+/ }"
+      env $BENV timeout -k 10 600 python bench.py $a > $O/bench_$name.log 2>&1 || { tail -20 $O/bench_$name.log; exit 1; }
+      grep '^{' $O/bench_$name.log | tail -n 1 > $O/bench_$name.json
+      python3 -c "import json; d=json.load(open('$O/bench_$name.json')); print('$name', round(d['ms_per_step'],3), 'ms/step', d['value'], d.get('failed_replications'), d.get('hier_escalation'), d['roofline'].get('kernel_avg_ms'))" ;;
+  esac
+done
+echo "== done $(date +%T)"
