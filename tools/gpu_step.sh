@@ -4,6 +4,7 @@
 #   tests:<pytest -k expr>   GPU tests matching the expression
 #   suite                    the whole GPU suite
 #   bench:<name>:<args>      one bench.py line (args with '+' for spaces) -> <name>.json
+#   ab:<variant>:<args>      bench.py on build/live/<variant> (or the tree's library: 'tree'), no CPU leg
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r5; mkdir -p $O
@@ -23,6 +24,11 @@ for s in $STEPS; do
       env $BENV timeout -k 10 600 python bench.py $a > $O/bench_$name.log 2>&1 || { tail -20 $O/bench_$name.log; exit 1; }
       grep '^{' $O/bench_$name.log | tail -n 1 > $O/bench_$name.json
       python3 -c "import json; d=json.load(open('$O/bench_$name.json')); print('$name', round(d['ms_per_step'],3), 'ms/step', d['value'], d.get('failed_replications'), d.get('hier_escalation'), d['roofline'].get('kernel_avg_ms'))" ;;
+    ab:*)  # ab:<variant under build/live, or "tree">:<bench args>: one bench line of a variant build
+      r="${s#ab:}"; v="${r%%:*}"; a="${r#*:}"; a="${a//+/ }"
+      lib=build/live/$v/libfognet_hip.so; [ "$v" = tree ] && lib=fognetsimpp_amd/libfognet_hip.so
+      FOGNET_LIB=$lib timeout -k 10 600 python tools/bench_var.py $a --no-cpu > $O/ab_$v.log 2>&1 || { tail -20 $O/ab_$v.log; exit 1; }
+      echo "ab $v [$a] $(grep '^{' $O/ab_$v.log | tail -n 1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), "ms/step kernel", round(d["roofline"]["kernel_avg_ms"],3), "failed", d["failed_replications"])')" ;;
   esac
 done
 echo "== done $(date +%T)"
