@@ -1276,486 +1276,13 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
 #endif
 }
 
-// ---- Sliding-window replay (replay_kernel, REF_V3; DESIGN.md §3.4 "Sliding
-// window").  replay_body walks the trace in aligned 64-publish chunks, so a
-// decision run that crosses a chunk boundary is pushed in two iterations (its
-// "resumed" half repeats the FIFO scan, the stores and the node update), and
-// every chunk pays a prologue and an output flush.  Here each iteration's
-// window starts at the run's first publish: lane l holds publish jp + l, read
-// from a three-chunk LDS ring that LDS-DMA fills two chunks ahead, so a run of
-// up to 64 publishes is one iteration, and its outputs are stored by the run's
-// lanes directly.  The division tables go (S = req / MIPS in fp64 with an exact
-// correction, MIPS of the chosen node by a scalar load), which pays for the
-// third chunk buffer within the 10-KiB LDS budget of 16 workgroups per CU.
-constexpr int kWinBufs = 3;
-
-// floor(n / m) for n < 2^31, 1 <= m < 2^31: the fp64 quotient with rm = 1/m
-// (correctly rounded) is within 2^-21 of n/m, so its truncation is off by at
-// most one, which the remainder test corrects.
-__device__ __forceinline__ uint32_t div_rm(uint32_t n, uint32_t m, double rm) {
-  const uint32_t q = (uint32_t)((double)n * rm);
-  const int64_t rem = (int64_t)n - (int64_t)((uint64_t)q * m);
-  return rem < 0 ? q - 1u : (rem >= (int64_t)m ? q + 1u : q);
-}
-
-template <int NPL>
-__device__ __forceinline__ void replay_body_win(const ReplayArgs& A, const int r) {
-  constexpr int kSet = 0;  // prefetch register set (v112..)
-  const int lane = threadIdx.x;
-  __shared__ int64_t s_dl[NPL * kWave];
-  __shared__ int64_t s_ul[NPL * kWave];
-  __shared__ int64_t s_tld[NPL * kWave];   // tail completion tick (INT64_MIN: node never used)
-  __shared__ uint32_t s_tlC[NPL * kWave];  // tail cumulative service (mod 2^32)
-  __shared__ uint8_t s_tlS[NPL * kWave];   // tail service seconds (< 256 while the replication stays here)
-  // staged trace chunks: chunk c in buffer c % 3, {arrive lo | arrive hi | req} x 64 each
-  __shared__ uint32_t s_ch[kWinBufs * 3 * kWave];
-
-  const int T = A.T, N = A.N;
-  const size_t nbase = (size_t)r * (size_t)A.node_stride;
-  const size_t tbase = (size_t)r * (size_t)T;
-  const uint32_t qmask = (1u << A.q_log2) - 1u;
-  const int64_t arrive0 = T > 0 ? A.arrive[tbase] : kNever;
-  const uint32_t lds_ch = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)s_ch;
-  const int nchunks = (T + kWave - 1) / kWave;
-  uint32_t ops = 0u;  // tally of issued vector-memory instructions (see kPrefetchOps)
-  uint32_t cst = 0u;  // byte b: `ops` after the DMA into chunk buffer b was issued
-  int c_dma = 0;      // chunks [0, c_dma) have been issued
-  auto stage = [&](int c) {
-    const int cc = min(kWave, T - c * kWave);
-    const int b = c % kWinBufs;
-    chunk_dma(A.arrive + tbase + (size_t)c * kWave, A.req + tbase + (size_t)c * kWave, (uint32_t)min(lane, cc - 1),
-              __builtin_amdgcn_readfirstlane(lds_ch + (uint32_t)b * (3u * kWave * 4u)));
-    ops += kChunkOps;
-    cst = set_stamp(cst, b, ops);
-  };
-  for (; c_dma < min(kWinBufs, nchunks); ++c_dma) stage(c_dma);
-
-  // ---- node parameters + preconditions (fognet_hip.h, fognet_batch_in)
-  bool bad = false;
-  Slot st[NPL];
-#pragma unroll
-  for (int s = 0; s < NPL; ++s) {
-    const int k = s * kWave + lane;
-    int64_t d = 0, u = 0;
-    if (k < N) {
-      const int32_t m = A.mips[nbase + k];
-      d = A.dl[nbase + k];
-      u = A.ul[nbase + k];
-      const int64_t ia = A.init[nbase + k];
-      bad |= (m <= 0) | (d < 0) | (u < 0) | (d > kMaxTick) | (u > kMaxTick) | (ia < u) | (ia >= arrive0);
-    }
-    s_dl[k] = d;
-    s_ul[k] = u;
-    // every node's first advert {MIPS, busyTime = 0.0} has reached the broker
-    st[s].vkey = k < N ? (uint32_t)k : kNoKey;
-    st[s].nxt = kNever;
-    st[s].hd_C = 0u;
-    st[s].hd_S = 0u;
-    st[s].tl_a = 0;
-    s_tld[k] = INT64_MIN;
-    s_tlC[k] = 0u;
-    s_tlS[k] = 0u;
-    st[s].cnt = 0u;
-  }
-  __syncthreads();
-
-  uint32_t err = ballot(bad) ? (uint32_t)FOGNET_ERR_ARG : (uint32_t)FOGNET_OK;
-  if (N <= 0) err = FOGNET_ERR_NO_NODES;
-
-  RingWord* const ring_r = A.ring + (size_t)r * (size_t)N * ((size_t)qmask + 1u);
-  const int q_log2 = A.q_log2;
-  auto lane_now = [&]() -> uint32_t {
-    uint32_t l = (uint32_t)lane;
-    asm volatile("" : "+v"(l));
-    return l;
-  };
-  auto ring_s = [&](int s) -> RingWord* {
-    const uint32_t k = (uint32_t)(s * kWave) + lane_now();
-    return ring_r + ((size_t)(k < (uint32_t)N ? k : 0u) << q_log2);
-  };
-  uint32_t best = view_min<NPL>(st);
-  bool dirty = false;
-  int64_t prev_t = INT64_MIN;  // tick of publish jp - 1
-  uint32_t max_pend = 0u;
-  uint32_t pf = 0u;  // per-slot stamps of the youngest head+1 loads (set_stamp)
-  int64_t n_done = 0;
-  uint32_t scan = 0u;
-#if FOGNET_REPLAY_PROFILE == 2
-  uint64_t p_t[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const uint64_t p_start = __builtin_amdgcn_s_memtime();
-  uint64_t p_last = p_start;
-#endif
-#if FOGNET_REPLAY_PROFILE == 1
-  uint64_t p_iter = 0, p_advit = 0, p_adv = 0, p_end_k = 0, p_end_j = 0, p_end_c = 0, p_hz = 0, p_refill = 0, p_w0 = 0,
-           p_rd = 0, p_chunks = 0, p_pk0 = 0, p_resume = 0, p_same = 0, p_endh_same = 0;
-  int prev_k = -1;
-  auto young = [&](int s, bool need) { return ballot(need) && ((ops - (pf >> (8 * s))) & 0xFFu) < 2u; };
-#endif
-  // A run that used up its window continues in the next one while the
-  // publishes stay within its horizon E_carry (argmin unchanged).
-  bool carry = false;
-  int64_t E_carry = 0;
-  // the chosen node's MIPS and its reciprocal, kept while the decision stays
-  int k_div = -1;
-  uint32_t m_k = 1u;
-  double rm_k = 1.0;
-  // issue priority (see board_update)
-  constexpr bool kPrio = FOGNET_PRIO != 0;
-  uint32_t b_slot = 0u;
-  float b_scale = 0.0f;
-  int next_board = 0;
-  if constexpr (kPrio) {
-    b_slot = board_slot();
-    b_scale = 1048576.0f / (float)(T > 0 ? T : 1);
-  }
-
-  for (int jp = 0; jp < T && err == FOGNET_OK;) {
-    const int cw = jp >> 6;  // the window [jp, jp + 64) lies in chunks cw and cw + 1
-    // chunk cw - 1 is consumed: its buffer takes chunk cw + 2 (the window advances at most one chunk
-    // per iteration, so one DMA per iteration keeps two chunks ahead)
-    if (c_dma < nchunks && c_dma <= cw + 2) {
-      stage(c_dma);
-      ++c_dma;
-    }
-    if constexpr (kPrio) {
-      if (jp >= next_board) {
-        next_board += kPrioEvery * kWave;
-        const uint32_t my = __builtin_amdgcn_readfirstlane((uint32_t)((float)jp * b_scale));
-#if FOGNET_PRIO == 2
-        if (A.board) board_update(A.board, b_slot, my, lane);
-#else
-        set_prio(3u - min(my >> 18, 3u));
-#endif
-      }
-    }
-    const int cnt = min(kWave, T - jp);
-    const bool live = lane < cnt;
-    const int c_last = (jp + cnt - 1) >> 6;
-    wait_vm((ops - (cst >> (8 * (c_last % kWinBufs)))) & 0xFFu);  // the window's chunks have landed in LDS
-    int64_t ca;
-    int32_t cr;
-    {
-      const uint32_t p = (uint32_t)jp + lane_now();
-      const uint32_t w = ((p >> 6) % (uint32_t)kWinBufs) * (3u * kWave) + (p & (kWave - 1));
-      ca = live ? (int64_t)(((uint64_t)s_ch[w + kWave] << 32) | s_ch[w]) : kNever;
-      cr = live ? (int32_t)s_ch[w + 2 * kWave] : 0;
-    }
-    PROF(p_chunks++; p_iter++;)
-    TMARK(0)
-    // trace preconditions: nondecreasing ticks, requirement >= 0, ticks < 2^61
-    const int64_t prv = dpp_or_i64<kDppWaveShr1>(prev_t, ca);  // lane 0 gets prev_t
-    if (ballot(live && (ca < prv || cr < 0 || ca > kMaxTick))) {
-      err = FOGNET_ERR_ARG;
-      break;
-    }
-    const int64_t t_last = readlane_i64(ca, cnt - 1);  // only picks which horizons are evaluated exactly
-    const int64_t t_p = readlane_i64(ca, 0);
-
-    const bool resume = carry && t_p <= E_carry;
-    carry = false;
-    int64_t E = E_carry;
-    if (!resume) {
-      // 1) completion adverts that reached the broker strictly before t_p (replay_body's rounds)
-      for (;;) {
-        bool any = false;
-        static_for<0, NPL>([&](auto sc) {
-          constexpr int s = decltype(sc)::value;
-          const bool due = st[s].nxt < t_p;
-          const uint64_t dm = ballot(due);
-          if (!dm) return;
-          const uint32_t pd = pending(st[s]);
-          any = true;
-          dirty = true;
-          PROF(p_advit++; p_adv += __popcll(ballot(due)); p_rd++; p_w0 += young(s, due && pending(st[s]) >= 2u);)
-          TMARK(1)
-          const u32x4 nhw = read_nh<s, kSet>((dm & lanes_ge(pd, 2u)) != 0, pf, ops);
-          TMARK(8)
-          if (dm & lanes_ge(pd, 3u) & ballot((st[s].cnt & 0x10000u) == 0u)) {
-            ops += 1u;
-            pf = set_stamp(pf, s, ops);
-          }
-          if (due) {
-            const int k = s * kWave + lane;
-            apply_advert<s, kSet>(st[s], nhw, k, s_dl[k], s_ul[k], s_tlC[k], s_tlS[k], ring_s(s), qmask, ops, scan);
-          }
-        });
-        if (!any) break;
-      }
-      TMARK(1)
-      // 2) argmin over the advertised view (ties -> lowest index)
-      if (dirty) {
-        best = view_min<NPL>(st);
-        dirty = false;
-      }
-      TMARK(2)
-      const int k = (int)(best & 0xFFu);
-      PROF(p_same += k == prev_k;)
-      // 3) run horizon: earliest advert that could change the decision
-      int64_t e_lane = kNever;
-      static_for<0, NPL>([&](auto sc) {
-        constexpr int s = decltype(sc)::value;
-        const int j = s * kWave + lane;
-        const uint32_t pd = pending(st[s]);
-        const bool rel = j < N && j != k && (uint32_t)j < best && pd >= 1u;
-        bool deep = false;
-        if (rel) {
-          const uint32_t tlC_j = s_tlC[j];
-          if (arrives_before(st[s].tl_a, st[s].nxt - s_ul[j], s_dl[j], head_S(st[s]))) {
-            const int64_t h = horizon_all_in(st[s], j, best, tlC_j);
-            e_lane = h < e_lane ? h : e_lane;
-          } else if (st[s].nxt < t_last) {
-            deep = true;
-          } else {
-            e_lane = st[s].nxt < e_lane ? st[s].nxt : e_lane;  // beyond this window: its first advert
-          }
-        }
-        const uint64_t dm = ballot(deep);
-        if (dm) {
-          PROF(p_hz++; p_rd++; p_w0 += young(s, deep && pending(st[s]) >= 2u);)
-          TMARK(3)
-          const u32x4 nhw = read_nh<s, kSet>((dm & lanes_ge(pd, 2u)) != 0, pf, ops);
-          TMARK(9)
-          if (deep) {
-            const int64_t h =
-                horizon(st[s], nhw, j, best, s_tlC[j], s_tlS[j], s_dl[j], s_ul[j], ring_s(s), qmask, scan);
-            e_lane = h < e_lane ? h : e_lane;
-          }
-        }
-      });
-      E = (int64_t)wave_min_u64((uint64_t)e_lane);  // all candidates are >= 0
-    } else {
-      PROF(p_resume++;)
-    }
-    const int k = (int)(best & 0xFFu);
-    const int ks = k / kWave, kl = k % kWave;
-    PROF(const int64_t E_other = E;)
-    TMARK(3)
-
-    // node k: parameters and tail state (uniform)
-    const int64_t dl_k = s_dl[k], ul_k = s_ul[k];
-    if (k != k_div) {  // double tskTime = requiredMIPS / MIPS (:276): the divisor's reciprocal once per node
-      k_div = k;
-      m_k = (uint32_t)__builtin_amdgcn_readfirstlane(A.mips[nbase + k]);
-      rm_k = 1.0 / (double)m_k;
-    }
-    const uint32_t tlC_k = s_tlC[k], tlS_k = s_tlS[k];
-    const int64_t tld_k = s_tld[k];
-    uint32_t cnt_k = 0u;
-    int64_t nxt_k = 0;
-#pragma unroll
-    for (int s = 0; s < NPL; ++s) {
-      if (s == ks) {
-        cnt_k = readlane_u32(st[s].cnt, kl);
-        nxt_k = readlane_i64(st[s].nxt, kl);
-      }
-    }
-    const uint32_t pend_k = ((cnt_k & 0xFFFFu) - (cnt_k >> 16)) & 0xFFFFu;
-    if (resume) {
-      // E_carry already holds k's own bound
-    } else if (pend_k > 0u) {
-      E = nxt_k < E ? nxt_k : E;  // k's own next advert changes its key
-    } else {
-      // the run's first task becomes k's head: its advert ends the run
-      const uint32_t s_p = div_rm(readlane_u32((uint32_t)cr, 0), m_k, rm_k);
-      const int64_t a_p = t_p + dl_k;
-      const int64_t done_p = (a_p > tld_k ? a_p : tld_k) + (int64_t)(s_p & 0xFFFFu) * kTicksPerSecond;
-      const int64_t x_p = done_p + ul_k;
-      E = x_p < E ? x_p : E;
-    }
-
-    // 4) the run: publishes jp .. jp + L - 1 (a prefix of the window) with tick <= E all go to node k
-    const bool in_run = (live && ca <= E) || lane == 0;
-    const uint64_t run_mask = ballot(in_run);
-    const int L = __popcll(run_mask);
-
-    // 5) FIFO recurrence over the run (replay_body's scans, the run starting at lane 0)
-    uint32_t S = 0u;
-    int64_t a = 0, dd = 0;
-    bool lerr = false, lwide = false;
-    if (in_run) {
-      S = div_rm((uint32_t)cr, m_k, rm_k);
-      a = ca + dl_k;
-      dd = (int64_t)S * kTicksPerSecond;
-      lerr = a > kMaxTick;
-      lwide = S > A.max_s || S > kRingSMask || a > kRingAMax;
-    }
-    uint32_t Cs = S;
-    Cs = scan_add_level<0x111, 0xF>(Cs);  // row_shr:1
-    Cs = scan_add_level<0x112, 0xF>(Cs);  // row_shr:2
-    Cs = scan_add_level<0x114, 0xF>(Cs);  // row_shr:4
-    Cs = scan_add_level<0x118, 0xF>(Cs);  // row_shr:8
-    Cs = scan_add_level<0x142, 0xA>(Cs);  // row_bcast:15
-    Cs = scan_add_level<0x143, 0xC>(Cs);  // row_bcast:31
-    const int64_t base_done = tld_k;  // INT64_MIN when k never ran a task
-    int64_t done;
-    uint32_t status;
-    if (base_done > (int64_t)((uint64_t)readlane_i64(ca, L - 1) + (uint64_t)dl_k)) {
-      done = (int64_t)((uint64_t)base_done + (uint64_t)ticks_of(Cs));
-      status = 4u;  // busy: "task queued" (:304-313)
-    } else {
-      int64_t X = in_run ? (int64_t)((uint64_t)a - (uint64_t)ticks_of(Cs - S)) : INT64_MIN;
-      int64_t xt = INT64_MIN;
-      X = scan_max_level<0x111, 0xF>(X, xt);
-      X = scan_max_level<0x112, 0xF>(X, xt);
-      X = scan_max_level<0x114, 0xF>(X, xt);
-      X = scan_max_level<0x118, 0xF>(X, xt);
-      X = scan_max_level<0x142, 0xA>(X, xt);
-      X = scan_max_level<0x143, 0xC>(X, xt);
-      const int64_t dmax = base_done > X ? base_done : X;
-      done = (int64_t)((uint64_t)dmax + (uint64_t)ticks_of(Cs));
-      const int64_t done_up = dpp_or_i64<kDppWaveShr1>(0, done);
-      const uint32_t S_up = dpp_or_u32<kDppWaveShr1>(0u, S);
-      const int64_t prev_done = lane == 0 ? base_done : done_up;
-      const uint32_t prev_S = lane == 0 ? tlS_k : S_up;
-      if (prev_done < a) {
-        status = 5u;  // idle: "task assigned" (:282-301)
-      } else if (prev_done > a) {
-        status = 4u;  // busy: "task queued" (:304-313)
-      } else {        // completion of the previous task at the same tick
-        status = (dl_k < (int64_t)prev_S * kTicksPerSecond) ? 5u : 4u;
-      }
-    }
-    const int64_t start = done - dd;
-    lerr = lerr || (in_run && done > kMaxTick);
-    if (ballot(lerr)) {
-      err = FOGNET_ERR_ARG;
-      break;
-    }
-    if (ballot(lwide) || pend_k + (uint32_t)L - 1u > qmask) {
-      err = kNeedsWide;
-      break;
-    }
-    TMARK(4)
-    // ring entries and per-task outputs, stored by the run's lanes
-    RingWord* const ring_k = ring_r + ((size_t)k << q_log2);
-    if (in_run) {
-      ring_k[((cnt_k & 0xFFFFu) + lane_now()) & qmask] = ((uint64_t)a << kRingSBits) | S;
-      const size_t o = tbase + (size_t)jp;
-      const uint32_t l = lane_now();
-      // nontemporal: the outputs are re-read only by the epilogue, long after they left L2
-      __builtin_nontemporal_store(k, (A.out_node + o) + l);
-      __builtin_nontemporal_store((uint8_t)status, (A.out_status + o) + l);
-      __builtin_nontemporal_store(start, (A.out_start + o) + l);
-      __builtin_nontemporal_store(done, (A.out_done + o) + l);
-    }
-    ops += 5u;
-    TMARK(5)
-
-    // 6) node k's state after the run
-    const int lz = L - 1;
-    const int64_t a_z = readlane_i64(a, lz), done_z = readlane_i64(done, lz);
-    const uint32_t C_z = readlane_u32(tlC_k + Cs, lz), S_z = readlane_u32(S, lz);
-    const int64_t done_f = readlane_i64(done, 0);
-    const uint32_t C_f = readlane_u32(tlC_k + Cs, 0), S_f = readlane_u32(S, 0);
-    prev_t = readlane_i64(ca, lz);
-#pragma unroll
-    for (int s = 0; s < NPL; ++s) {
-      if (s == ks) {
-        if (lane == kl) {
-          if (pend_k == 0u) {
-            st[s].hd_C = C_f;
-            st[s].hd_S = S_f;
-            st[s].nxt = done_f + ul_k;
-          }
-          st[s].tl_a = a_z;
-          s_tld[k] = done_z;
-          s_tlC[k] = C_z;
-          s_tlS[k] = S_z;
-          st[s].cnt = (cnt_k & 0xFFFF0000u) | ((cnt_k + (uint32_t)L) & 0xFFFFu);
-        }
-        const uint32_t pl = pend_k + (uint32_t)L;
-        if ((pend_k <= 1u && pl >= 2u) || ((cnt_k & 0x10000u) != 0u && pend_k <= 2u && pl >= 3u)) {
-          refill_nh<kSet>(s, st[s], ring_s(s), qmask, kl);
-          PROF(p_refill++;)
-          ops += 1u;
-          pf = set_stamp(pf, s, ops);
-        }
-      }
-    }
-    const uint32_t pend_after = pend_k + (uint32_t)L;
-    max_pend = pend_after > max_pend ? pend_after : max_pend;
-    n_done += L;
-    if (L == kWave) {  // the window is used up and E still bounds the decision
-      carry = true;
-      E_carry = E;
-    }
-    TMARK(6)
-    PROF(p_pk0 += pend_k == 0u; if (L == cnt) p_end_c++; else if (E == E_other) p_end_j++; else p_end_k++;
-         prev_k = k;)
-    jp += L;
-  }
-  // drain the inline-asm prefetches, the DMA and the stores before the wave retires / re-reads
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (kPrio && FOGNET_PRIO == 2) {
-    if (A.board && lane == 0) __hip_atomic_store(A.board + b_slot, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-#if FOGNET_REPLAY_PROFILE == 2
-  TMARK(7)
-#endif
-#if FOGNET_REPLAY_PROFILE == 1
-  uint64_t p_scan = 0;
-  for (int l = 0; l < kWave; ++l) p_scan += readlane_u32(scan, l);
-#endif
-  if (lane == 0 && err == kNeedsWide && A.wide_list) A.wide_list[atomicAdd(A.wide_count, 1)] = r;
-  if (lane == 0 && A.out_stats) {
-    fognet_rep_stats* S = A.out_stats + r;
-    S->n_tasks = n_done;
-    S->max_pending = (int32_t)max_pend;
-    S->status = (int32_t)err;
-    S->events = 2 * (int64_t)N + 4 * n_done;
-#if FOGNET_REPLAY_PROFILE == 2
-    S->n_queued = p_t[0];
-    S->n_started = p_t[1];
-    S->last_tick = p_t[2];
-    S->queue_min_raw = p_t[3];
-    S->queue_max_raw = p_t[4];
-    S->resp_min_ticks = p_t[5];
-    S->resp_max_ticks = p_t[6];
-    S->queue_sum_lo = p_t[7];
-    S->queue_sq_lo = p_t[8];
-    S->queue_sq_hi = p_t[9];
-    S->queue_sum_hi = p_last - p_start;
-#endif
-#if FOGNET_REPLAY_PROFILE == 1
-    S->n_queued = p_iter;
-    S->n_started = p_advit;
-    S->last_tick = p_adv;
-    S->queue_min_raw = p_scan;
-    S->queue_max_raw = p_end_k;
-    S->resp_min_ticks = p_hz;
-    S->resp_max_ticks = p_refill;
-    S->queue_sum_lo = p_w0;
-    S->queue_sum_hi = p_rd;
-    S->queue_sq_lo = p_chunks;
-    S->queue_sq_hi = p_end_j;
-    S->resp_sum_hi = p_end_c;
-    S->resp_sq_lo = p_resume;
-    S->resp_sum_lo = p_pk0;
-    S->busy_s = (int64_t)p_same;
-    S->resp_sq_hi = 0;
-#endif
-  }
-#if !defined(FOGNET_REPLAY_PROFILE) || FOGNET_REPLAY_PROFILE == 0
-  if (A.fuse_stats && A.out_stats && err != kNeedsWide) {
-    static_assert(kWinBufs * 3 * kWave >= 128 + 2 * kWave + kWave, "epilogue scratch fits the chunk ring");
-    fused_stats_epilogue<NPL>(A, r, n_done, err, s_tld, s_tlC, s_ul, s_dl, s_ch,
-                              reinterpret_cast<int64_t*>(s_ch + 128), lane);
-  }
-#endif
-}
-
 // 4 waves per SIMD (<= 128 VGPRs) and <= 10 KiB of LDS (160 KiB / 16): 16
 // replications resident per CU, so the 4096-replication sweep runs in a single
 // wave of workgroups on 256 CUs.  (11 KiB of LDS admits only 14 per CU, and
 // the last 512 replications then run as a second, mostly idle round.)
 template <int NPL, int POL>
 __global__ __launch_bounds__(64, 4) __attribute__((amdgpu_num_vgpr(kNhBase / 2))) void replay_kernel(ReplayArgs A) {
-#ifndef FOGNET_CHUNKED
-  if constexpr (POL == FOGNET_POLICY_REF_V3)
-    replay_body_win<NPL>(A, blockIdx.x);
-  else
-#endif
-    replay_body<NPL, POL, false, false>(A, blockIdx.x, blockIdx.x);
+  replay_body<NPL, POL, false, false>(A, blockIdx.x, blockIdx.x);
 }
 
 // Statistics in the loop (ReplayArgs::inloop): 3 waves per SIMD like the
