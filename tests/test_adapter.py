@@ -1,8 +1,10 @@
-"""The OMNeT++ adapter (integration/BrokerBaseAppHip.{h,cc,ned})
-is real code: it type-checks against a minimal stub of the OMNeT++ / INET
-identifiers it touches (tests/adapter/stub: the reference's member names,
-types and access, BrokerBaseApp3.h:24-64), and on a GPU a driver feeds it
-adverts and publishes and checks every offloaded task against the oracle."""
+"""The OMNeT++ adapters (integration/BrokerBaseAppHip.{h,cc,ned} for the v3
+broker, integration/BrokerBaseApp2Hip.{h,cc,ned} for the v2 broker C1's ini
+selects) are real code: they type-check against a minimal
+stub of the OMNeT++ / INET identifiers they touch (tests/adapter/stub: the
+reference's member names, types and access, BrokerBaseApp3.h:24-64,
+BrokerBaseApp2.h:27-60), and on a GPU a driver feeds each adverts and
+publishes and checks every offloaded task against the oracle."""
 import os
 import subprocess
 
@@ -13,25 +15,31 @@ INC = ["-I", os.path.join(ROOT, "tests", "adapter", "stub"), "-I", os.path.join(
        "-I", os.path.join(ROOT, "integration")]
 
 
-def test_adapter_type_checks_against_the_reference_interface():
+ADAPTERS = {"v3": ("BrokerBaseAppHip.cc", "adapter_drive"), "v2": ("BrokerBaseApp2Hip.cc", "adapter2_drive")}
+
+
+@pytest.mark.parametrize("which", sorted(ADAPTERS))
+def test_adapter_type_checks_against_the_reference_interface(which):
     for std in ("c++11", "c++14", "c++17"):  # OMNeT++ 4.6 builds with C++11
         subprocess.run(["g++", f"-std={std}", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
-                        *INC, os.path.join(ROOT, "integration", "BrokerBaseAppHip.cc")], check=True)
+                        *INC, os.path.join(ROOT, "integration", ADAPTERS[which][0])], check=True)
 
 
-def build_driver(out_dir) -> str:
-    exe = os.path.join(str(out_dir), "adapter_drive")
+def build_driver(out_dir, which="v3") -> str:
+    name = ADAPTERS[which][1]
+    exe = os.path.join(str(out_dir), name)
     lib = os.path.join(ROOT, "fognetsimpp_amd")
     orc = os.path.join(ROOT, "oracle", "build")
     subprocess.run(["g++", "-std=c++14", "-O1", "-Wall", "-Werror", "-Wno-unused-parameter", *INC,
-                    os.path.join(ROOT, "tests", "adapter", "adapter_drive.cpp"), "-o", exe,
+                    os.path.join(ROOT, "tests", "adapter", name + ".cpp"), "-o", exe,
                     "-L", orc, "-loracle", "-L", lib, "-lfognet_hip", "-L/opt/rocm/lib", "-lamdhip64",
                     f"-Wl,-rpath,{orc}", f"-Wl,-rpath,{lib}", "-Wl,-rpath,/opt/rocm/lib"], check=True)
     return exe
 
 
-def test_adapter_driver_links(tmp_path):
-    assert os.path.exists(build_driver(tmp_path))
+@pytest.mark.parametrize("which", sorted(ADAPTERS))
+def test_adapter_driver_links(tmp_path, which):
+    assert os.path.exists(build_driver(tmp_path, which))
 
 
 @pytest.mark.gpu
@@ -42,4 +50,16 @@ def test_adapter_offloads_like_the_reference_on_gpu(tmp_path):
     p = subprocess.run([build_driver(tmp_path)], capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "adapter: all checks passed" in p.stdout
+    print(p.stdout)
+
+
+@pytest.mark.gpu
+def test_v2_adapter_forwards_like_the_reference_on_gpu(tmp_path):
+    """Every publish the v2 adapter forwards is recorded and its task goes to the
+    node orc_decide_v2 picks on the MIPS view at that moment (ties, zero MIPS,
+    N = 0 .. 1000), or is not sent when that node's MIPS is too small (:262);
+    local publishes reach the base class; one device decision per view."""
+    p = subprocess.run([build_driver(tmp_path, "v2")], capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "adapter2: all checks passed" in p.stdout
     print(p.stdout)
