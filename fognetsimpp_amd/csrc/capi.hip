@@ -435,17 +435,27 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     if (a.policy == FOGNET_POLICY_EXT_HIER && !a.down && !stats_only && a.T > 0 && B >= 2 && use_regions()) {
       // one wavefront per (replication, region) while no region escalates (replay_region.hip), the
       // statistics pass, then the sequential wide kernel for the replications some region handed back.
-      // workspace: [hand-over counter | list [R] | quit flags [R] | region records [R][B] | entries [R][T] |
-      // node records [R][N] | busy view [R][B][1024]]; the hand-over launch reuses the space from the
-      // entries on (stream order: after the statistics pass has read the node records), with one workspace
-      // slot per handed-over replication up to kWideFallbackSlots (so an escalation-heavy job replays its
-      // hand-overs side by side, as the sequential-only path does)
+      // workspace: [hand-over counter | list [R] | quit flags [R] | region records [R][B] | segment offsets
+      // [R][B+1] | entries [R][T] | node records [R][N] | busy view [R][B][1024] | region-sorted trace and
+      // outputs [R][T]]; the hand-over launch reuses the space from the entries on (stream order: after the
+      // finish kernel has read the node records and the sorted outputs), with one workspace slot per
+      // handed-over replication up to kWideFallbackSlots (an escalation-heavy job replays its hand-overs
+      // side by side, as the sequential-only path does)
+      const size_t RT = (size_t)a.R * (size_t)a.T;
       const size_t o_quit = align256(256 + (size_t)a.R * sizeof(int32_t));
       const size_t o_rec = o_quit + align256((size_t)a.R * sizeof(int32_t));
-      const size_t o_e = o_rec + align256((size_t)a.R * (size_t)B * sizeof(fognet::RegionRec));
-      const size_t o_nd = o_e + align256((size_t)a.R * (size_t)a.T * sizeof(fognet::WideEntry));
+      const size_t o_seg = o_rec + align256((size_t)a.R * (size_t)B * sizeof(fognet::RegionRec));
+      const size_t o_e = o_seg + align256((size_t)a.R * (size_t)(B + 1) * sizeof(int32_t));
+      const size_t o_nd = o_e + align256(RT * sizeof(fognet::WideEntry));
       const size_t o_vb = o_nd + align256((size_t)a.R * (size_t)a.N * sizeof(fognet::WideNode));
-      const size_t body = o_vb - o_e + (size_t)a.R * (size_t)B * FOGNET_HIER_REGION_NODES * sizeof(uint32_t);
+      const size_t o_sa = o_vb + align256((size_t)a.R * (size_t)B * FOGNET_HIER_REGION_NODES * sizeof(uint32_t));
+      const size_t o_sq = o_sa + align256(RT * sizeof(int64_t));
+      const size_t o_inv = o_sq + align256(RT * sizeof(int32_t));
+      const size_t o_on = o_inv + align256(RT * sizeof(int32_t));
+      const size_t o_os = o_on + align256(RT * sizeof(int32_t));
+      const size_t o_ost = o_os + align256(RT);
+      const size_t o_od = o_ost + align256(RT * sizeof(int64_t));
+      const size_t body = o_od + RT * sizeof(int64_t) - o_e;
       const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
       const size_t fb = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
       rc = ensure(c, (void**)&c->ring, &c->ring_bytes, o_e + (body > fb ? body : fb), "region replay workspace");
@@ -457,10 +467,21 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       if (e != hipSuccess) return hip_fail(c, e, "hand-over counter");
       e = hipMemsetAsync(base + o_quit, 0, (size_t)a.R * sizeof(int32_t), (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(c, e, "region quit flags");
-      const fognet::RegionWs w{reinterpret_cast<fognet::WideEntry*>(base + o_e),
-                               reinterpret_cast<fognet::WideNode*>(base + o_nd),
-                               reinterpret_cast<fognet::RegionRec*>(base + o_rec),
-                               reinterpret_cast<uint32_t*>(base + o_vb), reinterpret_cast<int32_t*>(base + o_quit), B};
+      fognet::RegionWs w;
+      w.e = reinterpret_cast<fognet::WideEntry*>(base + o_e);
+      w.nd = reinterpret_cast<fognet::WideNode*>(base + o_nd);
+      w.rec = reinterpret_cast<fognet::RegionRec*>(base + o_rec);
+      w.vb = reinterpret_cast<uint32_t*>(base + o_vb);
+      w.quit = reinterpret_cast<int32_t*>(base + o_quit);
+      w.seg = reinterpret_cast<int32_t*>(base + o_seg);
+      w.s_arr = reinterpret_cast<int64_t*>(base + o_sa);
+      w.s_req = reinterpret_cast<int32_t*>(base + o_sq);
+      w.inv = reinterpret_cast<int32_t*>(base + o_inv);
+      w.o_node = reinterpret_cast<int32_t*>(base + o_on);
+      w.o_status = reinterpret_cast<uint8_t*>(base + o_os);
+      w.o_start = reinterpret_cast<int64_t*>(base + o_ost);
+      w.o_done = reinterpret_cast<int64_t*>(base + o_od);
+      w.B = B;
       if (regions_only()) a.wide_list = nullptr;
       e = fognet::launch_replay_region(a, w, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(c, e, "region replay launch");

@@ -345,12 +345,20 @@ struct RegionRec {
   int32_t n_done, max_pend, status, pad;
 };
 struct RegionWs {
-  WideEntry* e;    // [R][T]
+  WideEntry* e;    // [R][T] chain entries, indexed by the task's position in the region-sorted order
   WideNode* nd;    // [R][N]
   RegionRec* rec;  // [R][B]
   uint32_t* vb;    // [R][B][16][64] advertised busy times (the region kernel's view, [slot][lane])
-  int32_t* quit;   // [R] zeroed before the launch: set when a region of r hands it back, so r's other
-                   // region wavefronts stop early (the sequential kernel replays r from the start)
+  int32_t* quit;   // [R] zeroed before the launch: set when a region of r hands it back (or the trace is
+                   // invalid), so r's other region wavefronts stop early (the sequential kernel replays r)
+  int32_t* seg;    // [R][B + 1] region b's publishes are sorted positions [seg[b], seg[b + 1])
+  int64_t* s_arr;  // [R][T] publish ticks, region-sorted (stable: trace order within a region)
+  int32_t* s_req;  // [R][T] MIPSRequired, region-sorted
+  int32_t* inv;    // [R][T] sorted position of task i
+  int32_t* o_node;   // [R][T] the region pass's per-task outputs, region-sorted (region_finish_kernel
+  uint8_t* o_status; //        writes them to the caller's arrays in trace order)
+  int64_t* o_start;
+  int64_t* o_done;
   int32_t B;       // regions: ceil(N / FOGNET_HIER_REGION_NODES)
 };
 hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s);

@@ -9,21 +9,27 @@
 // changes only at adverts of its own nodes (BrokerBaseApp3.cc:123-130), whose
 // busy values depend only on the tasks its own broker sent them
 // (ComputeBrokerApp3.cc:224-320).  So each (replication, region) pair is
-// replayed by its own wavefront over the region's publishes only: B waves per
-// replication instead of one, each walking a tenth of the chain.  The same
-// closed form as replay_wide.hip: node j of region b (local
-// index l = j - 1024 b) lives on lane l % 64, slot l / 64, with its view
-// (next advert tick, advertised busy) in this lane's registers (16 slots), its
-// record (WideNode) and its tasks' chain (WideEntry) in HBM.
-//
+// replayed by its own wavefront over the region's publishes only:
+//   * region_sort_kernel (one 256-thread block per replication) sorts the
+//     publishes by region, stably (a counting sort), so region b's publishes
+//     are the contiguous positions [seg[b], seg[b+1]) of a sorted copy of the
+//     trace, and checks the trace's preconditions once;
+//   * replay_region_kernel walks its region's segment 64 publishes at a time
+//     with the flat wide kernel's closed form and decision runs (replay_wide.hip,
+//     DESIGN.md §3.6): due adverts applied lane-parallel, the regional minimum
+//     key, then every publish up to the run horizon E pushed onto the chosen
+//     node with one FIFO scan.  Node l of the region (index base + l) lives on
+//     lane l % 64, slot l / 64: next-advert ticks and run-horizon offsets in
+//     LDS, advertised busy times in HBM, records and task chains in HBM, the
+//     lane's last-pushed record cached in registers;
+//   * region_finish_kernel merges the regions' records, writes the outputs back
+//     in trace order and runs the statistics pass (the same Acc record,
+//     histogram and a11 energy as the wide kernel's inline statistics).
 // A replication in which any region meets an escalation (or anything else this
-// kernel does not model: a saturated busy time, a service time past 2^22 s, an
+// pass does not model: a saturated busy time, a service time past 2^22 s, an
 // invalid input) is replayed again from the start by the sequential wide
 // kernel (the hand-over list, like the register kernel's), which defines every
-// result of such a replication; nothing of this pass survives for it.  For the
-// others region_finish_kernel merges the regions' records and runs the
-// statistics pass over the per-task outputs (the same Acc record, histogram and
-// a11 energy as the wide kernel's inline statistics).
+// result of such a replication; nothing of this pass survives for it.
 #include "replay_common.h"
 
 namespace fognet {
@@ -34,13 +40,103 @@ constexpr int kRegionSlots = FOGNET_HIER_REGION_NODES / kWave;  // 16 view slots
 static_assert(kRegionSlots == kWideGroupSlots, "a region is one wide-kernel group row");
 constexpr uint32_t kRegBusySat = 0xFFFFFFFFu;
 constexpr uint32_t kRegSCap = 1u << 22;  // the wide kernel's kWideSCap: past it the sequential kernel decides
+constexpr uint32_t kRegWCap = 1u << 21;  // run-horizon offsets are capped like replay_wide.hip's node_w
 
 // Internal per-(replication, region) status: replay the replication sequentially
-// (fognet_hip.h never returns it; tests see it under FOGNET_HIER_REGIONS=only).
+// (fognet_hip.h never returns it; under FOGNET_HIER_REGIONS=only the finish kernel
+// reports FOGNET_ERR_UNSUPPORTED instead).
 constexpr int32_t kRegionSeq = 0x53455121;
 constexpr int kQuitEvery = 4;  // chunks between polls of the replication's quit flag
 
-// 4 waves per SIMD: 8 KiB of LDS each (the view's ticks), <= 128 VGPRs.
+// ---- region_sort_kernel: stable counting sort of one replication's publishes by region
+constexpr int kSortThreads = 256;
+constexpr int kSortWaves = kSortThreads / kWave;
+
+__global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A, RegionWs W) {
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+  const int T = A.T, B = W.B;
+  const size_t tbase = (size_t)r * (size_t)T;
+  __shared__ uint32_t s_cnt[kWave];             // per region: count, then the next free position
+  __shared__ uint32_t s_wc[kSortWaves][kWave];  // per wave and region: the tile's publishes
+  __shared__ int s_bad;
+  if (tid < kWave) s_cnt[tid] = 0u;
+  if (tid == 0) s_bad = 0;
+  __syncthreads();
+  // counts, and the trace preconditions the sequential kernel reports (nondecreasing ticks,
+  // requirement >= 0, ticks < 2^61, a region of the node set): a violation hands r over
+  bool bad = false;
+  for (int i = tid; i < T; i += kSortThreads) {
+    const int32_t g = A.region[tbase + i];
+    const int64_t t = A.arrive[tbase + i];
+    const int64_t tp = i > 0 ? A.arrive[tbase + i - 1] : INT64_MIN;
+    if (g < 0 || g >= B || A.req[tbase + i] < 0 || t > kMaxTick || t < tp) bad = true;
+    else atomicAdd(&s_cnt[g], 1u);
+  }
+  if (bad) s_bad = 1;
+  __syncthreads();
+  if (s_bad) {
+    if (tid == 0) __hip_atomic_store(W.quit + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  int32_t* const seg = W.seg + (size_t)r * (size_t)(B + 1);
+  if (tid == 0) {
+    uint32_t acc = 0u;
+    for (int b = 0; b < B; ++b) {
+      const uint32_t c = s_cnt[b];
+      s_cnt[b] = acc;
+      seg[b] = (int32_t)acc;
+      acc += c;
+    }
+    seg[B] = (int32_t)acc;
+  }
+  // tiles of 256 publishes: a publish's position = its region's next free position + the
+  // publishes of its region in earlier waves of the tile + those in earlier lanes of its wave
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int i0 = 0; i0 < T; i0 += kSortThreads) {
+    s_wc[wv][lane] = 0u;
+    __syncthreads();
+    const int i = i0 + tid;
+    const bool live = i < T;
+    const int32_t g = live ? A.region[tbase + i] : -1;
+    uint32_t rank = 0u;
+    for (uint64_t rem = ballot(live); rem;) {
+      const int g0 = __builtin_amdgcn_readlane(g, (int)__builtin_ctzll(rem));
+      const uint64_t m = ballot(live && g == g0);
+      if (live && g == g0) rank = (uint32_t)__popcll(m & lt);
+      if (lane == 0) s_wc[wv][g0] = (uint32_t)__popcll(m);
+      rem &= ~m;
+    }
+    __syncthreads();
+    if (live) {
+      uint32_t pos = s_cnt[g] + rank;
+      for (int w = 0; w < wv; ++w) pos += s_wc[w][g];
+      W.inv[tbase + i] = (int32_t)pos;
+      W.s_arr[tbase + pos] = A.arrive[tbase + i];
+      W.s_req[tbase + pos] = A.req[tbase + i];
+    }
+    __syncthreads();
+    if (tid < B) {
+      uint32_t c = 0u;
+      for (int w = 0; w < kSortWaves; ++w) c += s_wc[w][tid];
+      s_cnt[tid] += c;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- replay_region_kernel
+// Run horizon offset of a node (replay_wide.hip node_w): with every pending task
+// arrived before its head completes, the node's adverts carry busy values that
+// fall by at most the seconds elapsed from v1 = tl_C - hd_C on, so an advert with
+// busy <= busy_b comes no earlier than w = nxt + (v1 - busy_b) s; the offset v1
+// (capped) is kept per slot, w = nxt + offset.  Tasks still in flight: offset 0.
+__device__ __forceinline__ uint32_t w_offset(const WideNode& h, int64_t dl) {
+  if (h.npend == 0 || !arrives_before(h.tl_a, h.hd_done, dl, h.hd_S)) return 0u;
+  const uint64_t v1 = h.tl_C - h.hd_C;
+  return v1 < (uint64_t)kRegWCap ? (uint32_t)v1 : kRegWCap;
+}
+
+// 4 waves per SIMD (<= 128 VGPRs); 12 KiB of LDS per wavefront (view ticks and horizon offsets).
 __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, RegionWs W) {
   const int B = W.B;
   const int r = blockIdx.x / B, b = blockIdx.x - (blockIdx.x / B) * B;
@@ -51,16 +147,23 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   const int nb = min(FOGNET_HIER_REGION_NODES, N - base);  // nodes of this region (>= 1)
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)T;
-  WideEntry* const e = W.e + tbase;
+  WideEntry* const e = W.e + tbase;  // indexed by sorted position
   WideNode* const nd = W.nd + (size_t)r * (size_t)N;
+  const int32_t* const seg = W.seg + (size_t)r * (size_t)(B + 1);
   const int64_t arrive0 = T > 0 ? A.arrive[tbase] : kNever;
+  uint32_t err = __hip_atomic_load(W.quit + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0
+                     ? (uint32_t)kRegionSeq : (uint32_t)FOGNET_OK;  // (an invalid trace: see the sort)
+  const int s0 = err == FOGNET_OK ? seg[b] : 0;
+  const int nseg = err == FOGNET_OK ? seg[b + 1] - s0 : 0;  // this region's publishes
 
   // ---- this lane's nodes (local l = s * 64 + lane) and their view ([slot][lane]: each lane
-  // touches only its own column): next advert ticks in LDS (conflict-free); advertised busy
-  // times in HBM (RegionWs::vb; read back only by a key rescan of a lane without a zero-busy
-  // slot), so the LDS of a wavefront is 8 KiB: 20 fit per CU, and 4 per SIMD by VGPRs
+  // touches only its own column): next advert ticks and run-horizon offsets in LDS
+  // (conflict-free); advertised busy times in HBM (RegionWs::vb; read back only by a key
+  // rescan of a lane without a zero-busy slot)
   __shared__ int64_t s_nxt[kRegionSlots * kWave];
+  __shared__ uint32_t s_woff[kRegionSlots * kWave];
   int64_t* const vnxt = s_nxt + lane;  // vnxt[s * kWave]: slot s of this lane
+  uint32_t* const vwoff = s_woff + lane;
   uint32_t* const vbusy = W.vb + (size_t)rb * (size_t)(kRegionSlots * kWave) + lane;
   bool bad = false;
   // slots with an advert pending (view tick not kNever) and slots whose advertised busy
@@ -71,6 +174,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   for (int s = 0; s < kRegionSlots; ++s) {
     const int l = s * kWave + lane;
     vnxt[s * kWave] = kNever;
+    vwoff[s * kWave] = 0u;
     vbusy[s * kWave] = l < nb ? 0u : kRegBusySat;  // (past the region: never the minimum)
     nzb |= l < nb ? 0u : 1u << s;
     if (l < nb) {
@@ -81,25 +185,28 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
       nd[j] = WideNode{-1, -1, 0, -1, 0, 0u, 0, 0, 0u, 0u, 0u};
     }
   }
-  // the lane's earliest advert (slot ms) and smallest view key (busy << 32 | j)
-  int64_t mn = kNever;
+  // the lane's earliest advert (slot ms), smallest run-horizon bound w and smallest view
+  // key (busy << 32 | j)
+  int64_t mn = kNever, mw = kNever;
   int ms = 0;
   uint64_t mk = lane < nb ? (uint64_t)(uint32_t)(base + lane) : ~0ull;
-  // after slot sl's view tick became xs: the earliest over the pending slots (ties: the
-  // smallest slot)
-  auto rescan_nxt = [&](int sl, int64_t xs) {
-    mn = xs;
-    ms = sl;
-    for (uint32_t m = act & ~(1u << sl); m; m &= m - 1u) {
+  // earliest advert and smallest w over the pending slots (ties: the smallest slot)
+  auto rescan_nw = [&]() {
+    mn = kNever;
+    mw = kNever;
+    ms = 0;
+    for (uint32_t m = act; m; m &= m - 1u) {
       const int s = __builtin_ctz(m);
       const int64_t x = vnxt[s * kWave];
-      if (x < mn || (x == mn && s < ms)) {
+      const int64_t w = x + ticks_of(vwoff[s * kWave]);
+      if (x < mn) {
         mn = x;
         ms = s;
       }
+      mw = w < mw ? w : mw;
     }
   };
-  // (partially unrolled: a full unroll issues all 16 LDS loads at once and holds 32 VGPRs)
+  // (partially unrolled: a full unroll issues all 16 loads at once and holds 32 VGPRs)
   auto rescan_key = [&]() {
     const uint32_t z = ~nzb & ((1u << kRegionSlots) - 1u);
     if (z) {  // a zero-busy slot: the smallest one holds the smallest key
@@ -108,23 +215,22 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
     }
     mk = ~0ull;
 #pragma unroll 1
-    for (int s0 = 0; s0 < kRegionSlots; s0 += 8) {  // (8 loads in flight: few registers)
+    for (int q0 = 0; q0 < kRegionSlots; q0 += 8) {  // (8 loads in flight: few registers)
       uint32_t bv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) bv[u] = vbusy[(s0 + u) * kWave];
+      for (int u = 0; u < 8; ++u) bv[u] = vbusy[(q0 + u) * kWave];
       sync_vm();  // (in this arm: see sync_vm)
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const uint64_t key = ((uint64_t)bv[u] << 32) | (uint32_t)(base + (s0 + u) * kWave + lane);
+        const uint64_t key = ((uint64_t)bv[u] << 32) | (uint32_t)(base + (q0 + u) * kWave + lane);
         mk = key < mk ? key : mk;
       }
     }
   };
 
-  uint32_t err = ballot(bad) ? (uint32_t)kRegionSeq : (uint32_t)FOGNET_OK;
+  if (ballot(bad)) err = kRegionSeq;
   uint32_t max_pend = 0u;
   int n_done = 0;
-  int64_t prev_t = INT64_MIN;
   // the node this lane pushed to last (the stale view keeps choosing it): its
   // record and parameters in registers, written back when the lane pushes to
   // another node and at the end (replay_wide.hip's cache)
@@ -135,8 +241,6 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   auto cache_node = [&](uint32_t kk, int kl) {
     if (lane == kl && (int)kk != cj) {
       if (cj >= 0) nd[cj] = ch;
-
-
       cj = (int)kk;
       ch = nd[kk];
       c_dv = udiv_magic((uint32_t)A.mips[nbase + kk]);
@@ -147,9 +251,17 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   };
   bool view_changed = true;
   uint64_t key = 0ull;  // the regional broker's choice: its smallest view key
+  // a run that used up its chunk continues in the next one while the publishes stay
+  // within its horizon E_carry (the decision unchanged: no advert can change it before)
+  bool carry = false;
+  int64_t E_carry = 0;
+  const int64_t* const sa = W.s_arr + tbase + s0;
+  const int32_t* const sq = W.s_req + tbase + s0;
 #ifdef FOGNET_REGION_PROF
-  uint64_t pr[16] = {};
-  uint64_t pt0 = clock64(), pt = 0;
+  // profile build only: loop counters and clock64 segments, printed for a few wavefronts
+  uint64_t pr[12] = {};
+  uint64_t pt = clock64();
+  const uint64_t pt0 = pt;
 #define PRC(i, v) pr[i] += (v)
 #define PRT(i) { const uint64_t _n = clock64(); pr[i] += _n - pt; pt = _n; }
 #else
@@ -157,137 +269,191 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
 #define PRT(i)
 #endif
 
-  for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
+  for (int c0 = 0; c0 < nseg && err == FOGNET_OK; c0 += kWave) {
     // another region of r handed it back: the sequential kernel replays r from the start
     if ((c0 & (kQuitEvery * kWave - 1)) == 0 && c0 > 0 &&
         __hip_atomic_load(W.quit + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
       err = kRegionSeq;
       break;
     }
-    const int cnt = min(kWave, T - c0);
+    const int cnt = min(kWave, nseg - c0);
     const bool live = lane < cnt;
-    const int64_t ca = live ? A.arrive[tbase + c0 + lane] : kNever;
-    const int32_t cr = live ? A.req[tbase + c0 + lane] : 0;
-    const int32_t cg = live ? A.region[tbase + c0 + lane] : 0;
-    // trace preconditions (the sequential kernel reports them)
-    const int64_t prv = dpp_or_i64<kDppWaveShr1>(prev_t, ca);  // lane 0 gets prev_t
-    if (ballot(live && (ca < prv || cr < 0 || ca > kMaxTick || cg < 0 || cg >= B))) {
-      err = kRegionSeq;
-      break;
-    }
-    prev_t = readlane_i64(ca, cnt - 1);
-    // this chunk's publishes of region b; each member lane keeps its task's outputs until the chunk ends
-    uint64_t mem = ballot(live && cg == b);
-#ifdef FOGNET_REGION_PROF
-    pt = clock64();
-#endif
+    const int64_t ca = live ? sa[c0 + lane] : kNever;
+    const int32_t cr = live ? sq[c0 + lane] : 0;
+    // this chunk's pushed tasks, one per lane (sorted position s0 + c0 + lane): outputs
+    // stored once per chunk, coalesced
     bool q_on = false;
     uint32_t q_k = 0u, q_status = 0u;
     int64_t q_start = 0, q_done = 0;
-    while (mem) {
-      const int jp = (int)__builtin_ctzll(mem);
-      mem &= mem - 1ull;
+    int jp = 0;
+    while (jp < cnt) {
       const int64_t t = readlane_i64(ca, jp);
-
-      // 1) completion adverts that reached the broker strictly before t, lane-parallel
-      bool lbroken = false;
-      if (ballot(mn < t)) view_changed = true;
+      const bool resume = carry && t <= E_carry;
+      carry = false;
+      int64_t E = E_carry;
       PRC(0, 1);
-      while (ballot(mn < t)) {
-        PRC(1, 1);
-        PRC(2, __builtin_popcountll(ballot(mn < t)));
-        PRC(3, __builtin_popcountll(ballot(mn < t && base + ms * kWave + lane == cj)));
-        PRC(4, __builtin_popcountll(ballot(mn < t && base + ms * kWave + lane == cj && ch.npend >= 2)));
-        if (mn < t) {
-          const int sl = ms;
-          const int j = base + sl * kWave + lane;
-          const bool hit = j == cj;
-          int64_t nxt_j;
-          uint32_t busy_j;
-          bool broken = false;
-          // the cached record is updated in place (no copy of it through a merged value)
-          if (hit) {
-            (void)apply_wide_advert(ch, e, c_dl, c_ul, 0, nxt_j, busy_j, broken);
-            while (nxt_j < t && !broken) (void)apply_wide_advert(ch, e, c_dl, c_ul, 0, nxt_j, busy_j, broken);
-          } else {  // (waited for here, not where the arms meet: sync_vm)
-            WideNode h = nd[j];
-            const int64_t dl_j = A.dl[nbase + j], ul_j = A.ul[nbase + j];
-            sync_vm();
-            (void)apply_wide_advert(h, e, dl_j, ul_j, 0, nxt_j, busy_j, broken);
-            while (nxt_j < t && !broken) (void)apply_wide_advert(h, e, dl_j, ul_j, 0, nxt_j, busy_j, broken);
-            nd[j] = h;
+      PRC(1, resume ? 1 : 0);
+      PRT(7)
+      if (!resume) {
+        // 1) completion adverts that reached the broker strictly before t, lane-parallel
+        bool lbroken = false;
+        if (ballot(mn < t)) view_changed = true;
+        while (ballot(mn < t)) {
+          PRC(2, 1);
+          PRC(3, __popcll(ballot(mn < t)));
+          PRC(4, __popcll(ballot(mn < t && base + ms * kWave + lane == cj)));
+          if (mn < t) {
+            const int sl = ms;
+            const int j = base + sl * kWave + lane;
+            const bool hit = j == cj;
+            int64_t nxt_j;
+            uint32_t busy_j, off_j;
+            bool broken = false;
+            // the node's adverts that are due, in order; the cached record is updated in place
+            if (hit) {
+              (void)apply_wide_advert(ch, e, c_dl, c_ul, 0, nxt_j, busy_j, broken);
+              while (nxt_j < t && !broken) (void)apply_wide_advert(ch, e, c_dl, c_ul, 0, nxt_j, busy_j, broken);
+              off_j = w_offset(ch, c_dl);
+            } else {  // (waited for here, not where the arms meet: sync_vm)
+              WideNode h = nd[j];
+              const int64_t dl_j = A.dl[nbase + j], ul_j = A.ul[nbase + j];
+              sync_vm();
+              (void)apply_wide_advert(h, e, dl_j, ul_j, 0, nxt_j, busy_j, broken);
+              while (nxt_j < t && !broken) (void)apply_wide_advert(h, e, dl_j, ul_j, 0, nxt_j, busy_j, broken);
+              off_j = w_offset(h, dl_j);
+              nd[j] = h;
+            }
+            lbroken |= broken;
+            vnxt[sl * kWave] = nxt_j;
+            vwoff[sl * kWave] = off_j;
+            vbusy[sl * kWave] = busy_j;
+            act = nxt_j != kNever ? act | (1u << sl) : act & ~(1u << sl);
+            nzb = busy_j != 0u ? nzb | (1u << sl) : nzb & ~(1u << sl);
+            rescan_nw();
+            // the key: only j's changed; a rescan only when j held the minimum and grew
+            const uint64_t nk = ((uint64_t)busy_j << 32) | (uint32_t)j;
+            if ((uint32_t)mk == (uint32_t)j && nk > mk) rescan_key();
+            else mk = nk < mk ? nk : mk;
           }
-          lbroken |= broken;
-          vnxt[sl * kWave] = nxt_j;
-          vbusy[sl * kWave] = busy_j;
-          act = nxt_j != kNever ? act | (1u << sl) : act & ~(1u << sl);
-          nzb = busy_j != 0u ? nzb | (1u << sl) : nzb & ~(1u << sl);
-          rescan_nxt(sl, nxt_j);
-          // the key: only j's changed; a rescan only when j held the minimum and grew
-          const uint64_t nk = ((uint64_t)busy_j << 32) | (uint32_t)j;
-          PRC(6, __builtin_popcountll(ballot((uint32_t)mk == (uint32_t)j && nk > mk)));
-          if ((uint32_t)mk == (uint32_t)j && nk > mk) rescan_key();
-          else mk = nk < mk ? nk : mk;
         }
-      }
-      if (ballot(lbroken)) {
-        err = FOGNET_ERR_INTERNAL;
-        break;
-      }
-      PRT(8)
-      // 2) the regional broker's decision; above the threshold it would escalate
-      PRC(7, view_changed ? 1 : 0);
-      if (view_changed) {
-        key = wave_min_u64(mk);
-        view_changed = false;
-      }
-      if ((key >> 32) > (uint64_t)A.hier_thr || (key >> 32) >= kRegBusySat) {
-        err = kRegionSeq;
-        break;
+        if (ballot(lbroken)) {
+          err = FOGNET_ERR_INTERNAL;
+          break;
+        }
+        PRT(8)
+        // 2) the regional broker's decision; above the threshold it would escalate
+        if (view_changed) {
+          key = wave_min_u64(mk);
+          view_changed = false;
+        }
+        if ((key >> 32) > (uint64_t)A.hier_thr || (key >> 32) >= kRegBusySat) {
+          err = kRegionSeq;
+          break;
+        }
+        // 3) run horizon over the region's nodes (replay_wide.hip): no advert of another node
+        //    changes the decision before max(min nxt, min w - busy_b s)
+        const int64_t MN = (int64_t)wave_min_u64((uint64_t)mn);
+        const int64_t MW = (int64_t)wave_min_u64((uint64_t)mw);
+        const uint32_t busy_b = (uint32_t)(key >> 32);
+        E = MN;
+        if (busy_b < kRegWCap && (uint64_t)(MW - MN) > (uint64_t)ticks_of(busy_b)) E = MW - ticks_of(busy_b);
       }
       const uint32_t k = (uint32_t)key;
       const int kl = ((int)k - base) & (kWave - 1);
-
-      // 3) the task reaches node k (ComputeBrokerApp3.cc:269-320): FIFO single server
-      PRC(5, ballot(lane == kl && (int)k != cj) ? 1 : 0);
-      PRC(12, (k - base) / kWave);
       PRT(9)
+      PRC(5, ballot(lane == kl && (int)k != cj) ? 1 : 0);
+
+      // 4) node k (ComputeBrokerApp3.cc:269-320): FIFO single server, record cached in its lane
       cache_node(k, kl);
       const UDiv div_k{readlane_u32(c_dv.m, kl), readlane_u32(c_dv.sh, kl)};
       const int64_t dl_k = readlane_i64(c_dl, kl), ul_k = readlane_i64(c_ul, kl);
       const int32_t tl = (int32_t)readlane_u32((uint32_t)ch.tl, kl);
+      const int32_t npend0 = (int32_t)readlane_u32((uint32_t)ch.npend, kl);
       const int64_t tl_done = readlane_i64(ch.tl_done, kl);
       const uint64_t tl_C = (uint64_t)readlane_i64((int64_t)ch.tl_C, kl);
       const uint32_t tl_S = readlane_u32(ch.tl_S, kl);
-      const uint32_t S = udiv(readlane_u32((uint32_t)cr, jp), div_k);  // double tskTime = requiredMIPS / MIPS (:276)
-      const int64_t a = t + dl_k;
       const int64_t base_done = tl >= 0 ? tl_done : INT64_MIN;
-      const int64_t start = a > base_done ? a : base_done;
-      // (a <= 2^62 and S < 2^22: no int64 overflow below)
-      const int64_t done = S < kRegSCap ? start + ticks_of(S) : kNever;
-      if (a > kMaxTick || done > kMaxTick) {  // past the tick range: the sequential kernel refuses it
+      if (!resume) {
+        if (npend0 > 0) {  // k's own next advert changes its key
+          const int64_t nxt_k = readlane_i64(ch.hd_done, kl) + ul_k;
+          E = nxt_k < E ? nxt_k : E;
+        } else {  // the run's first task becomes k's head: its advert ends the run
+          const uint32_t S0 = udiv(readlane_u32((uint32_t)cr, jp), div_k);
+          const int64_t a0 = t + dl_k;  // (<= 2^62)
+          const int64_t st0 = a0 > base_done ? a0 : base_done;
+          int64_t x0 = kNever;  // (past the tick range the run is refused below anyway)
+          if (S0 < kRegSCap && st0 <= kMaxTick) x0 = st0 + ticks_of(S0) + ul_k;  // (< 2^61 + 2^62 + 2^61)
+          E = x0 < E ? x0 : E;
+        }
+      }
+      // the run: publishes jp .. jq-1 of the segment (contiguous lanes: nondecreasing ticks)
+      const uint64_t run_mask = ballot((lane >= jp && live && ca <= E) || lane == jp);
+      const int jq = jp + __popcll(run_mask >> jp);
+      const int Lr = jq - jp;
+      const bool in_run = lane >= jp && lane < jq;
+      const bool one = Lr == 1;  // a single publish needs no wave scans
+      uint32_t S = 0u;
+      int64_t a = 0;
+      if (in_run) {
+        S = udiv((uint32_t)cr, div_k);  // double tskTime = requiredMIPS / MIPS (:276)
+        a = ca + dl_k;
+      }
+      // FIFO recurrence over the run: done_m = max(base, max_{i<=m} (a_i - P_{i-1})) + P_m
+      const uint32_t Cs = one ? S : wave_scan_add_u32(in_run ? min(S, kRegSCap) : 0u);  // (< 64 * 2^22)
+      // a service prefix of 2^22 s or more, or an arrival past 2^61 ticks, puts the run past the
+      // tick range (the wide kernel's kPastRange): the sequential kernel decides the replication
+      if (ballot(in_run && (Cs >= kRegSCap || a > kMaxTick))) {
         err = kRegionSeq;
         break;
       }
-      uint32_t status;
-      if (base_done < a) status = 5u;       // idle: "task assigned" (:282-301)
-      else if (base_done > a) status = 4u;  // busy: "task queued" (:304-313)
-      else status = dl_k < (int64_t)min(tl_S, kRegSCap) * kTicksPerSecond ? 5u : 4u;  // same-tick completion
-      const int i = c0 + jp;
-      const uint64_t C = tl_C + S;
+      int64_t X = in_run ? a - ticks_of(Cs - S) : INT64_MIN;
+      if (!one) X = wave_scan_max_i64(X);
+      const int64_t dmax = base_done > X ? base_done : X;
+      const int64_t start = dmax + ticks_of(Cs - S);
+      const int64_t done = dmax + ticks_of(Cs);
+      if (ballot(in_run && done > kMaxTick)) {
+        err = kRegionSeq;
+        break;
+      }
+      int64_t prev_done = base_done;
+      uint32_t prev_S = tl_S;
+      if (!one) {
+        const int64_t dn_up = dpp_or_i64<kDppWaveShr1>(0, done);
+        const uint32_t S_up = dpp_or_u32<kDppWaveShr1>(0u, S);
+        if (lane != jp) {
+          prev_done = dn_up;
+          prev_S = S_up;
+        }
+      }
+      uint32_t status = 0u;
+      if (in_run) {
+        if (prev_done < a) status = 5u;       // idle: "task assigned" (:282-301)
+        else if (prev_done > a) status = 4u;  // busy: "task queued" (:304-313)
+        else status = dl_k < (int64_t)min(prev_S, kRegSCap) * kTicksPerSecond ? 5u : 4u;  // same-tick completion
+        const int i = s0 + c0 + lane;  // the task's sorted position: chained in order on node k
+        e[i] = WideEntry{a, done, tl_C + Cs, S, lane == jp ? tl : i - 1, lane + 1 < jq ? i + 1 : -1, 0};
+        q_on = true;
+        q_k = k;
+        q_status = status;
+        q_start = start;
+        q_done = done;
+      }
+      // 5) node k's record after the run (owner lane)
+      const int lz = jq - 1;
+      const int64_t a_z = readlane_i64(a, lz), done_z = readlane_i64(done, lz);
+      const uint32_t Cs_z = readlane_u32(Cs, lz), S_z = readlane_u32(S, lz);
+      const int64_t done_f = readlane_i64(done, jp);
+      const uint32_t S_f = readlane_u32(S, jp);
       if (lane == kl) {
-        e[i] = WideEntry{a, done, C, S, tl, -1, 0};
         WideNode h = ch;
-        // (no three-way branch on npend: that shape, with a store in the middle arm, was
-        // miscompiled on gfx950 -- DESIGN.md §3.6 "The hd_next miscompile"; hd_next is set
-        // after the two-way branch instead)
-        if (h.npend == 0) {  // the task is the node's head: its advert is the node's next one
-          h.hd = i;
-          h.hd_done = done;
-          h.hd_C = C;
-          h.hd_S = S;
-          const int sk = ((int)k - base) / kWave;
-          const int64_t x = done + ul_k;
+        const int i0 = s0 + c0 + jp, iz = s0 + c0 + lz;
+        const int sk = ((int)k - base) / kWave;
+        if (h.npend == 0) {  // the run's first task is the node's head: its advert is the node's next one
+          h.hd = i0;
+          h.hd_done = done_f;
+          h.hd_C = tl_C + S_f;
+          h.hd_S = S_f;
+          const int64_t x = done_f + ul_k;
           vnxt[sk * kWave] = x;
           act |= 1u << sk;
           if (x < mn) {
@@ -295,43 +461,51 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
             ms = sk;
           }
         } else if (h.npend >= 2) {
-          e[h.tl].next = i;
+          e[h.tl].next = i0;
         }
-        if (h.npend == 1) h.hd_next = i;  // the tail is the head
-        h.tl = i;
-        h.tl_a = a;
-        h.tl_done = done;
-        h.tl_C = C;
-        h.tl_S = S;
-        h.npend += 1;
+        // hd_next after the two-way branch, not in a third arm (DESIGN.md §3.6 "The hd_next
+        // miscompile"): the run's second task on an idle node, its first on a node whose one
+        // pending task is the tail
+        if (h.npend == 1 || (h.npend == 0 && Lr > 1)) h.hd_next = h.npend == 1 ? i0 : i0 + 1;
+        h.tl = iz;
+        h.tl_a = a_z;
+        h.tl_done = done_z;
+        h.tl_C = tl_C + Cs_z;
+        h.tl_S = S_z;
+        h.npend += Lr;
         ch = h;
         max_pend = max(max_pend, (uint32_t)h.npend);
+        // k's horizon offset (a larger one may leave mw stale-small: conservative, shorter runs)
+        const uint32_t off_k = w_offset(h, dl_k);
+        vwoff[sk * kWave] = off_k;
+        const int64_t w_k = h.hd_done + ul_k + ticks_of(off_k);
+        mw = w_k < mw ? w_k : mw;
       }
-      if (lane == jp) {
-        q_on = true;
-        q_k = k;
-        q_status = status;
-        q_start = start;
-        q_done = done;
-      }
-      n_done += 1;
+      n_done += Lr;
+      PRC(6, Lr);
       PRT(10)
+      if (jq == cnt) {  // the chunk is used up and E still bounds the decision
+        carry = true;
+        E_carry = E;
+      }
+      jp = jq;
     }
-    // the chunk's outputs (member lanes, coalesced)
+    // the chunk's outputs (pushed lanes, coalesced, region-sorted order)
     if (q_on) {
-      const size_t o = tbase + (size_t)(c0 + lane);
-      A.out_node[o] = (int32_t)q_k;
-      A.out_status[o] = (uint8_t)q_status;
-      A.out_start[o] = q_start;
-      A.out_done[o] = q_done;
+      const size_t o = tbase + (size_t)(s0 + c0 + lane);
+      W.o_node[o] = (int32_t)q_k;
+      W.o_status[o] = (uint8_t)q_status;
+      W.o_start[o] = q_start;
+      W.o_done[o] = q_done;
     }
   }
   if (cj >= 0) nd[cj] = ch;
 #ifdef FOGNET_REGION_PROF
   pr[11] = clock64() - pt0;
-  if (lane == 0 && (blockIdx.x < 3 || blockIdx.x % 1000 == 7))
-    printf("RPROF blk %d pubs %lu rounds %lu advl %lu hit %lu hit_e %lu cmiss %lu krescan %lu dec %lu cyc_adv %lu cyc_dec %lu cyc_push %lu cyc_tot %lu slotsum %lu\n",
-           (int)blockIdx.x, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[8], pr[9], pr[10], pr[11], pr[12]);
+  if (lane == 0 && (blockIdx.x < 3 || blockIdx.x % 997 == 7))
+    printf("RPROF blk %d iters %lu resumed %lu advrounds %lu adverts %lu advhit %lu kmiss %lu pubs %lu cyc_pre %lu "
+           "cyc_adv %lu cyc_dec %lu cyc_run %lu cyc_tot %lu\n",
+           (int)blockIdx.x, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[8], pr[9], pr[10], pr[11]);
 #endif
   const uint32_t mp = ~wave_min_u32(~max_pend);
   if (lane == 0) {
@@ -342,11 +516,12 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
 
 // Per replication (256 threads): the regions' records merged, the node tails'
 // busy seconds and last completion (FIFO: the tail's cumulative service and
-// completion), then the statistics pass over the outputs (stats_accumulate, the
-// fused epilogue's code) by waves 1-3 while wave 0 sums the a11 energy in node
-// order (replay_wide.hip's order): the energy's serial chain needs only the last
-// completion.  A replication some region could not finish goes to the hand-over
-// list instead.
+// completion), then the statistics pass in trace order -- each task's outputs
+// gathered from its sorted position, written to the caller's arrays and
+// accumulated (the fused epilogue's arithmetic) -- by waves 1-3 while wave 0
+// sums the a11 energy in node order (replay_wide.hip's order): the energy's
+// serial chain needs only the last completion.  A replication some region could
+// not finish goes to the hand-over list instead.
 constexpr int kFinThreads = 256;
 
 __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A, RegionWs W) {
@@ -434,9 +609,56 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
       if (tid == 0) s_energy = sum;
     }
   } else {
+    // tasks i = i0, i0 + 192, ... in trace order: position p = inv[i]; the outputs gathered from p,
+    // written to task i, and accumulated (stats_accumulate's arithmetic, task index i)
+    constexpr int U = 2;
+    const int i0 = tid - kWave;
+    const bool hist = A.hist != nullptr;
     Acc b = acc_identity();
-    stats_accumulate<2, false>(A, tbase, n, tid - kWave, kStatThreads, b, nullptr, s_hist,
-                               [&](int k) { return A.dl[nbase + k]; }, s_abt + kWave, s_abk + kWave);
+    for (int ib = i0; ib < n; ib += kStatThreads * U) {
+      int64_t t[U], st0[U], dn[U];
+      int32_t kk[U], pp[U];
+      uint32_t stt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = ib + u * kStatThreads;
+        const size_t o = tbase + (size_t)(i < n ? i : ib);  // past the end: reload task ib (in bounds, unused)
+        t[u] = A.arrive[o];
+        pp[u] = W.inv[o];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t p = tbase + (size_t)pp[u];
+        kk[u] = W.o_node[p];
+        stt[u] = W.o_status[p];
+        st0[u] = W.o_start[p];
+        dn[u] = W.o_done[p];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = ib + u * kStatThreads;
+        if (i < n) {
+          const size_t o = tbase + (size_t)i;
+          A.out_node[o] = kk[u];
+          A.out_status[o] = (uint8_t)stt[u];
+          A.out_start[o] = st0[u];
+          A.out_done[o] = dn[u];
+          const int64_t resp = dn[u] - t[u];
+          add_moment(b.rs_lo, b.rs_hi, b.rq_lo, b.rq_hi, (uint64_t)resp);
+          b.rmin = min(b.rmin, resp);
+          b.rmax = max(b.rmax, resp);
+          if (hist) atomicAdd(&s_hist[FOGNET_HIST_BINS + hist_bin(resp)], 1u);
+          if (stt[u] == 4u) {  // queueTime emission (ComputeBrokerApp3.cc:238), enqueued at its arrival
+            b.n4 += 1u;
+            if (!acc_qtime(b.qs_lo, b.qs_hi, b.qq_lo, b.qq_hi, b.qq_top, b.qmin, b.qmax, b.nqt, b.nqo, st0[u],
+                           t[u] + A.dl[nbase + kk[u]], hist ? s_hist : nullptr))
+              abort_min(s_abt[tid], s_abk[tid], st0[u], i);
+          } else {
+            b.n5 += 1u;
+          }
+        }
+      }
+    }
     b = wave_merge(b);
     const AbortPt ab_w = wave_min_abort(AbortPt{s_abt[tid], s_abk[tid]});  // (each thread's own slot)
     if ((tid & (kWave - 1)) == 0) {
@@ -471,8 +693,11 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
 }  // namespace
 
 hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s) {
-  hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w);
+  hipLaunchKernelGGL(region_sort_kernel, dim3(a.R), dim3(kSortThreads), 0, s, a, w);
   hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w);
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(region_finish_kernel, dim3(a.R), dim3(kFinThreads), 0, s, a, w);
   return hipGetLastError();

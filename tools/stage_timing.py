@@ -14,12 +14,15 @@ dev = torch.device("cuda", 0)
 ctx = fa.Context(0)
 mg, sc = (fa.c5_params if C5 else fa.sweep_params)(np.arange(R), N)
 tr = fa.generate_trace(ctx, 0x5EED0005 if C5 else 0x5EED0003, R, T, N, mg, sc)
+POL = os.environ.get("POLICY", "REF_V3")
+if POL == "EXT_HIER":
+    tr["region"] = fa.mobility_regions(tr["arrive"], N)
 out = fa.allocate_outputs(R, T, dev, N=N, energy=False, hist=True)
 torch.cuda.synchronize()
 for stage in os.environ.get("FOGNET_STAGES", "all,replay,stats,all,replay").split(","):
     ts = []
     for i in range(4):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(); fa.run_batch(ctx, tr, out, ring_capacity=2048, stage=stage); b.record()
+        a.record(); fa.run_batch(ctx, tr, out, ring_capacity=2048, stage=stage, policy=POL); b.record()
         torch.cuda.synchronize(); ts.append(a.elapsed_time(b))
-    print(os.path.basename(os.path.dirname(_abi.LIB_PATH)), stage, ["%.2f" % t for t in ts], "min %.2f" % min(ts), flush=True)
+    print(os.path.basename(os.path.dirname(_abi.LIB_PATH)), POL, stage, ["%.2f" % t for t in ts], "min %.2f" % min(ts), flush=True)
