@@ -48,8 +48,8 @@ constexpr uint32_t kRegWCap = 1u << 21;  // run-horizon offsets are capped like 
 constexpr int32_t kRegionSeq = 0x53455121;
 constexpr int kQuitEvery = 4;  // chunks between polls of the replication's quit flag
 
-// ---- region_sort_kernel: stable counting sort of one replication's publishes by region
-constexpr int kSortThreads = 256;
+// ---- region_sort_kernel: stable counting sort of one replication's publishes by region (one block)
+constexpr int kSortThreads = 1024;  // (a replication's 10,000 publishes in 10 tiles)
 constexpr int kSortWaves = kSortThreads / kWave;
 
 __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A, RegionWs W) {
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
     }
     seg[B] = (int32_t)acc;
   }
-  // tiles of 256 publishes: a publish's position = its region's next free position + the
+  // tiles of kSortThreads publishes: a publish's position = its region's next free position + the
   // publishes of its region in earlier waves of the tile + those in earlier lanes of its wave
   const uint64_t lt = (1ull << lane) - 1ull;
   for (int i0 = 0; i0 < T; i0 += kSortThreads) {
@@ -125,11 +125,12 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
 }
 
 // ---- replay_region_kernel
-// Run horizon offset of a node (replay_wide.hip node_w): with every pending task
-// arrived before its head completes, the node's adverts carry busy values that
-// fall by at most the seconds elapsed from v1 = tl_C - hd_C on, so an advert with
-// busy <= busy_b comes no earlier than w = nxt + (v1 - busy_b) s; the offset v1
-// (capped) is kept per slot, w = nxt + offset.  Tasks still in flight: offset 0.
+// Run horizon offset of a node (replay.hip horizon_all_in): with every pending
+// task arrived before its head completes, the node's next advert carries
+// v1 = tl_C - hd_C and each later one falls by at most the seconds elapsed, so an
+// advert with busy <= thr comes no earlier than nxt + (v1 - thr) s.  The offset
+// v1 (capped: a smaller one only shortens runs) is kept per slot; tasks still in
+// flight: offset 0 (the bound is then the next advert itself).
 __device__ __forceinline__ uint32_t w_offset(const WideNode& h, int64_t dl) {
   if (h.npend == 0 || !arrives_before(h.tl_a, h.hd_done, dl, h.hd_S)) return 0u;
   const uint64_t v1 = h.tl_C - h.hd_C;
@@ -185,25 +186,21 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
       nd[j] = WideNode{-1, -1, 0, -1, 0, 0u, 0, 0, 0u, 0u, 0u};
     }
   }
-  // the lane's earliest advert (slot ms), smallest run-horizon bound w and smallest view
-  // key (busy << 32 | j)
-  int64_t mn = kNever, mw = kNever;
+  // the lane's earliest advert (slot ms) and smallest view key (busy << 32 | j)
+  int64_t mn = kNever;
   int ms = 0;
   uint64_t mk = lane < nb ? (uint64_t)(uint32_t)(base + lane) : ~0ull;
-  // earliest advert and smallest w over the pending slots (ties: the smallest slot)
-  auto rescan_nw = [&]() {
+  // earliest advert over the pending slots (ties: the smallest slot)
+  auto rescan_nxt = [&]() {
     mn = kNever;
-    mw = kNever;
     ms = 0;
     for (uint32_t m = act; m; m &= m - 1u) {
       const int s = __builtin_ctz(m);
       const int64_t x = vnxt[s * kWave];
-      const int64_t w = x + ticks_of(vwoff[s * kWave]);
       if (x < mn) {
         mn = x;
         ms = s;
       }
-      mw = w < mw ? w : mw;
     }
   };
   // (partially unrolled: a full unroll issues all 16 loads at once and holds 32 VGPRs)
@@ -329,7 +326,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
             vbusy[sl * kWave] = busy_j;
             act = nxt_j != kNever ? act | (1u << sl) : act & ~(1u << sl);
             nzb = busy_j != 0u ? nzb | (1u << sl) : nzb & ~(1u << sl);
-            rescan_nw();
+            rescan_nxt();
             // the key: only j's changed; a rescan only when j held the minimum and grew
             const uint64_t nk = ((uint64_t)busy_j << 32) | (uint32_t)j;
             if ((uint32_t)mk == (uint32_t)j && nk > mk) rescan_key();
@@ -350,20 +347,13 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
           err = kRegionSeq;
           break;
         }
-        // 3) run horizon over the region's nodes (replay_wide.hip): no advert of another node
-        //    changes the decision before max(min nxt, min w - busy_b s)
-        const int64_t MN = (int64_t)wave_min_u64((uint64_t)mn);
-        const int64_t MW = (int64_t)wave_min_u64((uint64_t)mw);
-        const uint32_t busy_b = (uint32_t)(key >> 32);
-        E = MN;
-        if (busy_b < kRegWCap && (uint64_t)(MW - MN) > (uint64_t)ticks_of(busy_b)) E = MW - ticks_of(busy_b);
       }
       const uint32_t k = (uint32_t)key;
       const int kl = ((int)k - base) & (kWave - 1);
       PRT(9)
       PRC(5, ballot(lane == kl && (int)k != cj) ? 1 : 0);
 
-      // 4) node k (ComputeBrokerApp3.cc:269-320): FIFO single server, record cached in its lane
+      // 3) node k (ComputeBrokerApp3.cc:269-320): FIFO single server, record cached in its lane
       cache_node(k, kl);
       const UDiv div_k{readlane_u32(c_dv.m, kl), readlane_u32(c_dv.sh, kl)};
       const int64_t dl_k = readlane_i64(c_dl, kl), ul_k = readlane_i64(c_ul, kl);
@@ -374,16 +364,42 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
       const uint32_t tl_S = readlane_u32(ch.tl_S, kl);
       const int64_t base_done = tl >= 0 ? tl_done : INT64_MIN;
       if (!resume) {
-        if (npend0 > 0) {  // k's own next advert changes its key
-          const int64_t nxt_k = readlane_i64(ch.hd_done, kl) + ul_k;
-          E = nxt_k < E ? nxt_k : E;
-        } else {  // the run's first task becomes k's head: its advert ends the run
+        // k's own next advert changes its key; when k is idle the run's first task becomes its
+        // head and that task's advert ends the run
+        int64_t kb;
+        if (npend0 > 0) {
+          kb = readlane_i64(ch.hd_done, kl) + ul_k;
+        } else {
           const uint32_t S0 = udiv(readlane_u32((uint32_t)cr, jp), div_k);
           const int64_t a0 = t + dl_k;  // (<= 2^62)
           const int64_t st0 = a0 > base_done ? a0 : base_done;
-          int64_t x0 = kNever;  // (past the tick range the run is refused below anyway)
-          if (S0 < kRegSCap && st0 <= kMaxTick) x0 = st0 + ticks_of(S0) + ul_k;  // (< 2^61 + 2^62 + 2^61)
-          E = x0 < E ? x0 : E;
+          kb = kNever;  // (past the tick range the run is refused below anyway)
+          if (S0 < kRegSCap && st0 <= kMaxTick) kb = st0 + ticks_of(S0) + ul_k;  // (< 2^61 + 2^62 + 2^61)
+        }
+        if (jp + 1 < cnt && readlane_i64(ca, jp + 1) > kb) {
+          // the next publish comes after k's advert: a run of one, whatever the other nodes'
+          // adverts (any horizon is at least t: every advert before t has been applied)
+          E = t;
+        } else {
+          // 4) run horizon (replay.hip's horizon_all_in, per pending node of the lane): an advert
+          //    of j takes the decision from k = (busy_b, k) only with a busy value v <= thr_j =
+          //    busy_b - (j > k) (BrokerBaseApp3.cc:273, ties -> the lower index), and j's adverts
+          //    from its next one (at nxt_j, carrying v1 = offset) on fall by at most the seconds
+          //    elapsed, so none comes before max(nxt_j, w_j - thr_j s); thr_j < 0: never
+          const uint32_t busy_b = (uint32_t)(key >> 32), kk = (uint32_t)key;
+          int64_t e_lane = kNever;
+          for (uint32_t m = act; m; m &= m - 1u) {
+            const int s = __builtin_ctz(m);
+            const uint32_t j = (uint32_t)(base + s * kWave + lane);
+            const int64_t thr = (int64_t)busy_b - (j > kk ? 1 : 0);
+            if (j == kk || thr < 0) continue;  // (k's own advert bounds the run below)
+            const int64_t x = vnxt[s * kWave];
+            const uint32_t off = vwoff[s * kWave];
+            const int64_t bnd = (uint64_t)thr >= off ? x : x + ticks_of(off - (uint32_t)thr);
+            e_lane = bnd < e_lane ? bnd : e_lane;
+          }
+          E = (int64_t)wave_min_u64((uint64_t)e_lane);
+          E = kb < E ? kb : E;
         }
       }
       // the run: publishes jp .. jq-1 of the segment (contiguous lanes: nondecreasing ticks)
@@ -475,11 +491,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
         h.npend += Lr;
         ch = h;
         max_pend = max(max_pend, (uint32_t)h.npend);
-        // k's horizon offset (a larger one may leave mw stale-small: conservative, shorter runs)
-        const uint32_t off_k = w_offset(h, dl_k);
-        vwoff[sk * kWave] = off_k;
-        const int64_t w_k = h.hd_done + ul_k + ticks_of(off_k);
-        mw = w_k < mw ? w_k : mw;
+        vwoff[sk * kWave] = w_offset(h, dl_k);  // k's horizon offset
       }
       n_done += Lr;
       PRC(6, Lr);
@@ -522,7 +534,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
 // sums the a11 energy in node order (replay_wide.hip's order): the energy's
 // serial chain needs only the last completion.  A replication some region could
 // not finish goes to the hand-over list instead.
-constexpr int kFinThreads = 256;
+constexpr int kFinThreads = 256;  // wave 0: the energy chain; waves 1-3: the statistics pass
 
 __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A, RegionWs W) {
   const int r = blockIdx.x;
@@ -530,7 +542,7 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   const int B = W.B, N = A.N;
   constexpr int kFinWaves = kFinThreads / kWave;
   constexpr int kStatThreads = kFinThreads - kWave;  // waves 1..3
-  // (per-wave partial records: 4 x 152 B of LDS, so many blocks fit per CU)
+  // (per-wave partial records: 4 x 152 B of LDS)
   __shared__ Acc s_acc[kFinWaves];
   __shared__ int64_t s_abt[kFinThreads];
   __shared__ int32_t s_abk[kFinThreads];
@@ -591,6 +603,7 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   if (tid == 0) {
     uint64_t busy = 0u;
     int64_t last = INT64_MIN;
+#pragma unroll 1
     for (int w = 0; w < kFinWaves; ++w) {
       busy += s_acc[w].busy;
       last = max(last, s_acc[w].last);
@@ -602,7 +615,11 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   if (tid < kWave) {
     // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12), summed in
     // node order (64 nodes at a time, then lane by lane) while waves 1-3 run the statistics pass
+#ifndef FOGNET_FIN_NOENERGY
     if (A.p_busy) {  // (an unused node's record has tl_C = 0)
+#else
+    if (false) {  // timing probe only
+#endif
       const int64_t H = n > 0 ? s_last : 0;
       const double sum = energy_sum_wave(nd, A.p_busy + nbase, A.p_idle + nbase, N, H,
                                          A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, tid);
@@ -611,11 +628,15 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   } else {
     // tasks i = i0, i0 + 192, ... in trace order: position p = inv[i]; the outputs gathered from p,
     // written to task i, and accumulated (stats_accumulate's arithmetic, task index i)
-    constexpr int U = 2;
+    constexpr int U = 4;  // (two dependent loads per task: keep 8 in flight)
     const int i0 = tid - kWave;
     const bool hist = A.hist != nullptr;
     Acc b = acc_identity();
+#ifdef FOGNET_FIN_NOSTATS
+    for (int ib = n; ib < n; ib += kStatThreads * U) {  // timing probe only
+#else
     for (int ib = i0; ib < n; ib += kStatThreads * U) {
+#endif
       int64_t t[U], st0[U], dn[U];
       int32_t kk[U], pp[U];
       uint32_t stt[U];
@@ -671,6 +692,7 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   if (tid == 0) {
     Acc t = s_acc[1];
     AbortPt ab = AbortPt{s_abt[kWave], s_abk[kWave]};
+#pragma unroll 1
     for (int w = 2; w < kFinWaves; ++w) {
       acc_merge(t, s_acc[w]);
       abort_min(ab.tick, ab.task, s_abt[w * kWave], s_abk[w * kWave]);

@@ -5,6 +5,7 @@
 #   suite                    the whole GPU suite
 #   bench:<name>:<args>      one bench.py line (args with '+' for spaces) -> <name>.json
 #   ab:<variant>:<args>      bench.py on build/live/<variant> (or the tree's library: 'tree'), no CPU leg
+#   kt:<name>:<args>         rocprofv3 kernel trace + warm-up-free stats of bench.py (KTLIB=<variant>: a variant build)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r5; mkdir -p $O
@@ -37,6 +38,14 @@ for s in $STEPS; do
       r="${s#stage:}"; v="${r%%:*}"; R="${r#*:}"
       lib=build/live/$v/libfognet_hip.so; [ "$v" = tree ] && lib=fognetsimpp_amd/libfognet_hip.so
       FOGNET_LIB=$lib FOGNET_STAGES=${STAGES:-all,replay,all,replay} timeout -k 10 300 python tools/stage_timing.py $R 2>&1 | grep -v Warning | sed "s/^/[$v R=$R] /" ;;
+    kt:*)  # kt:<name>:<bench args>: rocprofv3 kernel trace + stats of one bench.py run (warm-up dispatches dropped)
+      r="${s#kt:}"; name="${r%%:*}"; a="${r#*:}"; a="${a//+/ }"
+      if [ -n "$KTLIB" ]; then prog="tools/bench_var.py"; export FOGNET_LIB=build/live/$KTLIB/libfognet_hip.so; else prog=bench.py; fi
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$name -o kt -- python3 $prog $a > $O/kt_$name.log 2>&1 || { tail -20 $O/kt_$name.log; exit 1; }
+      unset FOGNET_LIB
+      python3 tools/kstats.py $O/kt_$name --skip ${SKIP:-1} --out $O/kstats_$name.csv && python3 -c "
+import csv
+for r in list(csv.DictReader(open('$O/kstats_$name.csv')))[:6]: print('  ', r['Name'][:90], r['Calls'], round(float(r['AverageNs'])/1e3, 1), 'us')" ;;
   esac
 done
 echo "== done $(date +%T)"
