@@ -930,12 +930,23 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       //    that task's advert bounds the run too
       int jq = jp + 1;
       if constexpr (!kPerPublish) {
-        // run horizon (node_w): no other node's advert changes the decision before E
-        const int64_t MN = (int64_t)wave_min_u64((uint64_t)mn);
-        const int64_t MW = (int64_t)wave_min_u64((uint64_t)mw);
+        // run horizon (node_w), per group of the lane with a pending advert: node j takes the
+        // decision from k = (busy_b, k) only with an advert of busy v <= thr_j = busy_b - (j > k)
+        // (ties -> the lower index), which comes no earlier than max(nxt_j, w_j - thr_j s), so
+        // the group's adverts none before max(min nxt, min w - thr s) with thr its largest thr_j;
+        // a group whose nodes all have larger indices than k, with busy_b = 0, never matters
         const uint32_t busy_b = (uint32_t)(k_key >> 32);
-        int64_t E = MN;
-        if (busy_b < (1u << 21) && (uint64_t)(MW - MN) > (uint64_t)ticks_of(busy_b)) E = MW - ticks_of(busy_b);
+        int64_t e_lane = kNever;
+        for (uint64_t m = gact; m; m &= m - 1ull) {
+          const int g = (int)__builtin_ctzll(m);
+          const uint32_t thr = busy_b - (((uint32_t)(g * kWave * kWideGroupSlots) + (uint32_t)lane > k) ? 1u : 0u);
+          if (thr == 0xFFFFFFFFu) continue;  // (busy_b = 0 and every node of the group after k)
+          const int64_t gx = L.g_nxt[g * kWave + lane], gw = L.g_w[g * kWave + lane];
+          int64_t bnd = gx;
+          if (thr < (1u << 21) && (uint64_t)(gw - gx) > (uint64_t)ticks_of(thr)) bnd = gw - ticks_of(thr);
+          e_lane = bnd < e_lane ? bnd : e_lane;
+        }
+        int64_t E = (int64_t)wave_min_u64((uint64_t)e_lane);
         if (npend0 > 0) {  // k's own next advert changes its key
           const int64_t hd_done_k = readlane_i64(ch.hd_done, kl);
           const int64_t nxt_k = hd_done_k == kNever ? kNever : hd_done_k + ul_k;
