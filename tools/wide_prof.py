@@ -1,12 +1,12 @@
 """C5 loop counters of replay_wide_kernel (GPU; profile build:
-EXTRA=-DFOGNET_WIDE_PROF tools/build_variant.sh wideprof).  Per decision: publish
+EXTRA=-DFOGNET_WIDE_PROF tools/build_variant.sh wideprof, FOGNET_HIER_REGIONS=0 for the sequential EXT_HIER).  Per decision: publish
 iterations, advert-loop iterations, adverts applied, adverts followed by a due
 advert of the same node, adverts on the lane's cached node, group key rescans, runs."""
 import os, sys
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fognetsimpp_amd import _abi
-_abi.LIB_PATH = os.environ.get("FOGNET_LIB", "build/ab/wideprof/libfognet_hip.so")
+_abi.LIB_PATH = os.environ.get("FOGNET_LIB", "build/live/wideprof/libfognet_hip.so")
 import fognetsimpp_amd as fa
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 T, N = 10_000, 10_000
