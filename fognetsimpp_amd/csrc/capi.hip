@@ -101,7 +101,7 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a, boo
   if (in->policy != FOGNET_POLICY_REF_V3 && in->policy != FOGNET_POLICY_EXT_LAT && in->policy != FOGNET_POLICY_EXT_HIER)
     return fail(c, FOGNET_ERR_UNSUPPORTED, "unknown policy");
   if (in->policy == FOGNET_POLICY_EXT_HIER) {
-    if (in->R > 0 && in->T > 0 && !in->region) return fail(c, FOGNET_ERR_ARG, "EXT_HIER needs the region array");
+    if (!generated && in->R > 0 && in->T > 0 && !in->region) return fail(c, FOGNET_ERR_ARG, "EXT_HIER needs the region array");
     if (in->hier_threshold_s < 0 || in->hier_up_tick < 0 || in->hier_up_tick >= ((int64_t)1 << 50))
       return fail(c, FOGNET_ERR_ARG, "EXT_HIER: threshold >= 0 and 0 <= up latency < 2^50 ticks");
   }
@@ -560,16 +560,17 @@ int fognet_run_generated_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t 
   if (in->arrive_tick || in->req_mips || in->mips || in->dl_tick || in->ul_tick || in->init_adv_tick || in->down_tick ||
       in->region)
     return fail(c, FOGNET_ERR_ARG, "generated replay: the trace and node-parameter arrays must be NULL (generated)");
-  if (in->policy != FOGNET_POLICY_REF_V3 && in->policy != FOGNET_POLICY_EXT_LAT)
-    return fail(c, FOGNET_ERR_UNSUPPORTED, "generated replay: policy REF_V3 or EXT_LAT");
+  // (EXT_HIER: each publish's region from the mobility model of fa.mobility_regions, computed in the
+  // kernel, replication by replication on the sequential wide kernel)
   if (out->node || out->status || out->start_tick || out->done_tick)
     return fail(c, FOGNET_ERR_ARG, "generated replay: statistics only (per-task arrays must be NULL)");
   if (!out->stats) return fail(c, FOGNET_ERR_ARG, "stats output is required (per-replication status)");
   if (r0 < 0 || p->req_lo < 0 || p->req_hi < p->req_lo) return fail(c, FOGNET_ERR_ARG, "bad r0 or req range");
   if (in->R > 0 && (!p->mean_gap_ticks || !p->lat_scale)) return fail(c, FOGNET_ERR_ARG, "null generator parameters");
-  // per-node totals come from the node tails' 32-bit cumulative service (MIPS >= 1000)
-  if (in->T > 0 && (uint64_t)in->T * (uint64_t)(p->req_hi / 1000) >= (1ull << 32))
-    return fail(c, FOGNET_ERR_UNSUPPORTED, "generated replay: T * req_hi / 1000 must stay below 2^32");
+  // the register kernel's in-loop statistics take per-node totals from the node tails' 32-bit
+  // cumulative service (MIPS >= 1000): past 2^32 service seconds per replication the wide kernel
+  // (64-bit cumulative sums) replays the generated traces instead
+  const bool long_run = in->T > 0 && (uint64_t)in->T * (uint64_t)(p->req_hi / 1000) >= (1ull << 32);
   fognet::ReplayArgs a;
   int rc = prepare(c, in, &a, true);
   if (rc) return rc;
@@ -585,7 +586,7 @@ int fognet_run_generated_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t 
   a.hist = out->hist;
   if (a.out_energy && !a.p_busy) return fail(c, FOGNET_ERR_ARG, "node_energy_j needs the power model (p_busy_w/p_idle_w)");
   hipError_t e;
-  if (use_wide(a.N)) {
+  if (use_wide(a.N) || long_run || a.policy == FOGNET_POLICY_EXT_HIER) {
     const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N, true);
     rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ws, "wide replay workspace");
     if (rc) return rc;

@@ -119,6 +119,21 @@ __device__ __forceinline__ void gen_chunk(const GenRep& g, int c0, int T, int la
 // and SimTime * double round with toInt64(x) = floor(x + 0.5) and throw
 // outside the int64 range.  Every double operation is separately rounded.
 
+// Generated EXT_HIER (fognet_run_generated_dev): the regional broker of publish i
+// of a replication under the builder-defined mobility model of
+// fognetsimpp_amd.mobility_regions with its defaults (256 users; user u = i mod 256
+// starts in region u mod B and moves one region, +1 for even u and -1 for odd u,
+// every 30 / 45 / 60 / 75 s (u mod 4) from the replication's first publish t0).
+constexpr int kGenHierUsers = 256;
+__device__ __forceinline__ int32_t gen_region(int64_t i, int64_t t, int64_t t0, int B) {
+  const int64_t u = i % kGenHierUsers;
+  const int64_t per = (int64_t)(30 + 15 * (int)(u % 4)) * kTicksPerSecond;
+  const int64_t hops = (t - t0) / per;  // (t >= t0: a floor division)
+  int64_t reg = (u % B) + ((u % 2) ? -hops : hops);
+  reg %= B;
+  return (int32_t)(reg < 0 ? reg + B : reg);
+}
+
 __device__ __forceinline__ double simtime_dbl(int64_t t) { return mul_rn((double)t, 1e-12); }
 
 // SimTime::toInt64; false where the reference throws cRuntimeError

@@ -652,6 +652,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   uint64_t reg_dirty = 0ull;                   // regions with an advert applied since the last decision
   bool glob_valid = false;
 
+  int64_t gen_t0 = 0;  // generated EXT_HIER: the first publish's tick (the mobility model's origin)
   for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
     const bool live = lane < cnt;
@@ -671,7 +672,14 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
       cr = live ? A.req[tbase + c0 + lane] : 0;
     }
     int32_t cg = 0;  // EXT_HIER: the publish's regional broker (region = group of the LDS minima)
-    if constexpr (kHier) cg = live ? A.region[tbase + c0 + lane] : 0;
+    if constexpr (kHier) {
+      if (gen) {  // generated: the mobility model (replay_common.h gen_region) from the first publish's tick
+        if (c0 == 0) gen_t0 = readlane_i64(ca, 0);
+        cg = live ? gen_region(c0 + lane, ca, gen_t0, L.G) : 0;
+      } else {
+        cg = live ? A.region[tbase + c0 + lane] : 0;
+      }
+    }
     // trace preconditions: nondecreasing ticks, requirement >= 0, ticks < 2^61
     const int64_t prv = dpp_or_i64<kDppWaveShr1>(prev_t, ca);  // lane 0 gets prev_t
     if (ballot(live && (ca < prv || cr < 0 || ca > kMaxTick || (kHier && (cg < 0 || cg >= L.G))))) {

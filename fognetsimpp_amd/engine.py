@@ -286,13 +286,15 @@ def run_batch(ctx: Context, trace: dict, out: BatchResult | None = None, ring_ca
 def run_generated(ctx: Context, seed: int, R: int, T: int, N: int, mean_gap_ticks, lat_scale, r0: int = 0,
                   req_lo: int = 1000, req_hi: int = 64000, out: BatchResult | None = None, ring_capacity: int = 0,
                   policy: str | int = "REF_V3", power=None, hist: bool = True, energy: bool = False,
-                  device=None, stream=None) -> BatchResult:
+                  device=None, stream=None, hier_threshold_s: int = 60, hier_up_tick: int = 20 * 10**9) -> BatchResult:
     """Statistics-only replay of generated replications r0 .. r0+R-1
     (fognet_run_generated_dev): the trace recipe of
     :func:`generate_trace` is computed inside the replay kernel 64 publishes at
     a time, so neither the trace nor per-task outputs exist in memory.  The
     records equal ``generate_trace`` + ``run_batch`` on the same replications.
-    ``power``: optional (p_busy, p_idle) device tensors [R, N] or [N]."""
+    ``power``: optional (p_busy, p_idle) device tensors [R, N] or [N].
+    ``policy="EXT_HIER"``: each publish's regional broker is the one
+    :func:`mobility_regions` (defaults) gives, computed in the kernel."""
     device = device if device is not None else torch.device("cuda", ctx.device)
     if isinstance(mean_gap_ticks, torch.Tensor):
         mg, ls = mean_gap_ticks.reshape(R).contiguous(), lat_scale.reshape(R).contiguous()
@@ -311,8 +313,9 @@ def run_generated(ctx: Context, seed: int, R: int, T: int, N: int, mean_gap_tick
         raise FognetError(_abi.FOGNET_ERR_ARG, "stats buffer too small")
     pol = POLICIES[policy] if isinstance(policy, str) else int(policy)
     gp = _abi.GenParams(seed & 0xFFFFFFFF, req_lo, req_hi, 0, _ptr(mg), _ptr(ls))
+    hier = pol == _abi.FOGNET_POLICY_EXT_HIER
     bi = _abi.BatchIn(R, T, N, pol, stride, ring_capacity, None, None, None, None, None, None,
-                      _ptr(pb), _ptr(pi), None, None, 0, 0, 0)
+                      _ptr(pb), _ptr(pi), None, None, hier_up_tick if hier else 0, hier_threshold_s if hier else 0, 0)
     bo = _abi.BatchOut(None, None, None, None, _ptr(out.stats), _ptr(out.node_energy), _ptr(out.hist))
     s = C.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(device)
     ctx.check(ctx._lib.fognet_run_generated_dev(ctx.handle, C.byref(gp), r0, C.byref(bi), C.byref(bo), s),

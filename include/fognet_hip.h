@@ -477,9 +477,14 @@ int fognet_gen_trace_dev(fognet_ctx *ctx, const fognet_gen_params *p, int64_t r0
  * trace and the node parameters computed inside the replay kernel; no trace
  * and no per-task output ever reaches memory.  Results equal
  * fognet_gen_trace_dev + fognet_run_batch_dev on the same replications.
- *   in:  R, T, N, policy (REF_V3 or EXT_LAT), ring_capacity, p_busy_w/p_idle_w,
- *        node_stride; every trace/node-parameter pointer, down_tick and region
- *        must be NULL.  T * (req_hi / 1000) < 2^32 (node totals are 32-bit).
+ *   in:  R, T, N, policy, ring_capacity, p_busy_w/p_idle_w, node_stride (and
+ *        hier_threshold_s / hier_up_tick for EXT_HIER); every trace/node-parameter
+ *        pointer, down_tick and region must be NULL.  EXT_HIER: publish i's regional
+ *        broker follows the builder-defined mobility model of the Python mirror's
+ *        mobility_regions with its defaults (256 users, user i mod 256 starts in
+ *        region (i mod 256) mod B, moves +1 (even) / -1 (odd) every 30/45/60/75 s
+ *        (user mod 4) from the first publish), computed in the kernel; EXT_HIER and
+ *        replays with T * (req_hi / 1000) >= 2^32 run on the wide kernel.
  *   out: stats [R] (required), hist (added to), node_energy_j (nullable);
  *        node/status/start_tick/done_tick must be NULL. */
 int fognet_run_generated_dev(fognet_ctx *ctx, const fognet_gen_params *p, int64_t r0,

@@ -727,10 +727,7 @@ def test_generated_preconditions(ctx):
     """fognet_run_generated_dev refuses what it cannot replay exactly."""
     mg, sc = fa.sweep_params(np.arange(2), 8)
     with pytest.raises(fa.FognetError) as e:
-        fa.run_generated(ctx, 1, 2, 100, 8, mg, sc, policy="EXT_HIER")
-    assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED
-    with pytest.raises(fa.FognetError) as e:  # T * req_hi / 1000 >= 2^32: node totals would wrap
-        fa.run_generated(ctx, 1, 2, 2_000_000, 8, mg, sc, req_hi=4_000_000)
+        fa.run_generated(ctx, 1, 2, 100, 8, mg, sc, policy=7)
     assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED
     out = fa.run_generated(ctx, 1, 2, 0, 8, mg, sc)  # empty traces
     torch.cuda.synchronize()
@@ -1594,3 +1591,46 @@ def test_c5_ext_hier_escalations(ctx, monkeypatch, c5_saturated, mode):
     assert st.tobytes() == o["stats"].tobytes()
     np.testing.assert_array_equal(energy, o["node_energy"])
     np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
+
+
+@pytest.mark.parametrize("kind", ["ext_hier", "long"])
+def test_generated_wide_paths_equal_materialized(ctx, kind):
+    """Generated replays the register kernel does not take run on the wide
+    kernel, with the trace still computed in the kernel: EXT_HIER (each
+    publish's region from fa.mobility_regions' model, in the kernel; N = 1,030:
+    a 6-node second region that saturates, threshold 0, so it escalates) and requirement ranges with
+    T * req_hi / 1000 >= 2^32 (round 4 refused them: the register kernel's node
+    totals are 32-bit; any task of more than 255 s leaves that kernel anyway, and
+    at N = 16 such traces run past 2^61 ticks, so both paths report the same
+    FOGNET_ERR_ARG record).  Records, histograms and per-node energy equal
+    fognet_gen_trace_dev + the materialised replay bit for bit."""
+    dev = torch.device("cuda", ctx.device)
+    if kind == "ext_hier":
+        R, T, N, seed, rq, kw = 6, 12000, 1030, 0x5EED0007, (1000, 64000), dict(hier_threshold_s=0, hier_up_tick=10**12)
+        mg, sc = fa.sweep_params(np.arange(R), N, rho=0.9)
+        pol = "EXT_HIER"
+    else:
+        R, T, N, seed, rq, kw = 2, 2100, 16, 0x5EED0008, (1000, 2_100_000_000), {}
+        assert T * (rq[1] // 1000) >= 2**32
+        mg, sc = fa.sweep_params(np.arange(R), N, req_lo=rq[0], req_hi=rq[1])
+        pol = "REF_V3"
+    tr = fa.generate_trace(ctx, seed, R, T, N, mg, sc, req_lo=rq[0], req_hi=rq[1])
+    pb, pi = fa.power_model(tr["mips"].cpu().numpy())
+    power = (torch.from_numpy(pb).to(dev), torch.from_numpy(pi).to(dev))
+    tr = {k: v for k, v in tr.items() if not k.startswith("_")}
+    tr["p_busy"], tr["p_idle"] = power
+    if pol == "EXT_HIER":
+        tr["region"] = fa.mobility_regions(tr["arrive"], N)
+    ref = fa.run_batch(ctx, tr, policy=pol, hist=True, **kw)
+    gen = fa.run_generated(ctx, seed, R, T, N, mg, sc, req_lo=rq[0], req_hi=rq[1], policy=pol, power=power,
+                           hist=True, energy=True, **kw)
+    torch.cuda.synchronize()
+    st = ref.rep_stats()
+    if pol == "EXT_HIER":  # the regional brokers escalate somewhere
+        assert (st["status"] == 0).all()
+        node, reg = ref.node.cpu().numpy(), tr["region"].cpu().numpy()
+        assert (node // _abi.HIER_REGION_NODES != reg).any()
+    else:
+        assert (st["status"] == _abi.FOGNET_ERR_ARG).all()
+    assert gen.rep_stats().tobytes() == st.tobytes()
+    assert torch.equal(gen.hist, ref.hist) and torch.equal(gen.node_energy, ref.node_energy)
