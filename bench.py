@@ -111,6 +111,7 @@ def main():
                     help="c5: 'light' = fa.c5_params (device-generated; no region escalates), 'saturate' = "
                          "fa.saturating_trace (host-built, T = 32,768: every region saturates and escalates)")
     ap.add_argument("--workload", default="c3", choices=("c1", "c3", "c4", "c5"))
+    ap.add_argument("--v2-nodes", type=int, default=5, help="c1: compute brokers (the example has 5)")
     ap.add_argument("--R-total", type=int, default=None,
                     help="c4/c5: replications over all ranks (default 1,000,000 / 1024)")
     ap.add_argument("--block", type=int, default=0,
@@ -341,9 +342,31 @@ def main():
                       "energy_j": float(energy[0]), "busy_s": summary["busy_s"],
                       "hist_counts": [int(hist[0].sum()), int(hist[1].sum())]},
         }
+        line["roofline"].update(rocprof_kernel_avg(args, line))
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def rocprof_kernel_avg(args, line):
+    """The committed rocprofv3 average launch of the dominant kernel for this exact workload
+    (profiles/kernel_profile_<workload>[_<policy>|_<recipe>].json, written by tools/kprof_sidecar.py from a
+    kernel trace of the bench command itself): quoted only when its config equals this line's and the
+    average does not exceed this run's ms_per_step."""
+    tag = args.workload + ("" if args.policy in (None, "EXT_HIER" if args.workload == "c5" else "REF_V3")
+                           else f"_{args.policy}") + ("_saturate" if getattr(args, "c5_recipe", "light") == "saturate"
+                                                     and args.workload == "c5" else "")
+    path = os.path.join(ROOT, "profiles", f"kernel_profile_{tag}.json")
+    if not os.path.exists(path) or line["n_gpus"] != 1:
+        return {"kernel_avg_ms_rocprof": None}
+    try:
+        side = json.load(open(path))
+    except ValueError:
+        return {"kernel_avg_ms_rocprof": None}
+    if side.get("config") != line["config"] or side["avg_ms"] > line["ms_per_step"]:
+        return {"kernel_avg_ms_rocprof": None, "rocprof_profile_rejected": os.path.relpath(path, ROOT)}
+    return {"kernel_avg_ms_rocprof": side["avg_ms"], "rocprof_profile": os.path.relpath(path, ROOT),
+            "rocprof_command": side["command"], "rocprof_tree": side.get("tree")}
 
 
 def bench_c4(args, ctx, dev, dist, world, rank):
@@ -489,7 +512,7 @@ def bench_c1(args, ctx, dev, dist, world, rank):
     from fognetsimpp_amd.dist import shard
     MS = 10**9
     stop = 1000 * 10**12  # wirelessNet.ini:50 stopTime = 1000 s
-    n_nodes = 5
+    n_nodes = args.v2_nodes  # wirelessNet.ini: 5 ComputeBrokers (more: a timing of the v2 kernel's wider node sets)
     r0, R = shard(args.R_total, world, rank)
     t0 = time.time()
     gens = [formats.gen_trace_mqtt(r0 + r + 1, [0], [50 * MS], [MS], [-1], stop) for r in range(R)]  # :48 sendInterval

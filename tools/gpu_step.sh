@@ -5,7 +5,8 @@
 #   suite                    the whole GPU suite
 #   bench:<name>:<args>      one bench.py line (args with '+' for spaces) -> <name>.json
 #   ab:<variant>:<args>      bench.py on build/live/<variant> (or the tree's library: 'tree'), no CPU leg
-#   kt:<name>:<args>         rocprofv3 kernel trace + warm-up-free stats of bench.py (KTLIB=<variant>: a variant build)
+#   kt:<name>:<args>         rocprofv3 kernel trace + warm-up-free stats of bench.py (KTLIB=<variant>: a variant build;
+#                            KTKERNEL=<kernel>: also the kernel_profile sidecar bench.py quotes)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r5; mkdir -p $O
@@ -45,7 +46,12 @@ for s in $STEPS; do
       unset FOGNET_LIB
       python3 tools/kstats.py $O/kt_$name --skip ${SKIP:-1} --out $O/kstats_$name.csv && python3 -c "
 import csv
-for r in list(csv.DictReader(open('$O/kstats_$name.csv')))[:6]: print('  ', r['Name'][:90], r['Calls'], round(float(r['AverageNs'])/1e3, 1), 'us')" ;;
+for r in list(csv.DictReader(open('$O/kstats_$name.csv')))[:6]: print('  ', r['Name'][:90], r['Calls'], round(float(r['AverageNs'])/1e3, 1), 'us')" || exit 1
+      # KTKERNEL=<kernel name>: the bench.py sidecar (kernel_avg_ms_rocprof) of this profiled bench run
+      if [ -n "$KTKERNEL" ] && [ -z "$KTLIB" ]; then
+        python3 tools/kprof_sidecar.py $O/kt_$name.log $O/kstats_$name.csv --kernel $KTKERNEL --out $O/kernel_profile_$name.json \
+          --cmd "rocprofv3 --kernel-trace --stats --output-format csv -d <dir> -o kt -- python3 bench.py $a; tools/kstats.py --skip ${SKIP:-1}" || exit 1
+      fi ;;
   esac
 done
 echo "== done $(date +%T)"
