@@ -30,7 +30,7 @@ for s in $STEPS; do
       r="${s#ab:}"; v="${r%%:*}"; a="${r#*:}"; a="${a//+/ }"
       lib=build/live/$v/libfognet_hip.so; [ "$v" = tree ] && lib=fognetsimpp_amd/libfognet_hip.so
       FOGNET_LIB=$lib timeout -k 10 600 python tools/bench_var.py $a --no-cpu > $O/ab_$v.log 2>&1 || { tail -20 $O/ab_$v.log; exit 1; }
-      echo "ab $v [$a] $(grep '^{' $O/ab_$v.log | tail -n 1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), "ms/step kernel", round(d["roofline"]["kernel_avg_ms"],3), "failed", d["failed_replications"])')" ;;
+      echo "ab $v [$a] $(grep '^{' $O/ab_$v.log | tail -n 1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), "ms/step kernel", d["roofline"].get("kernel_avg_ms", d["roofline"].get("kernel_ms_per_step")), "failed", d["failed_replications"])')" ;;
     prof:*)  # prof:<variant under build/live>:<count|time>:<R>: replay_counters.py on a profile build
       r="${s#prof:}"; v="${r%%:*}"; r="${r#*:}"; m="${r%%:*}"; R="${r#*:}"
       FOGNET_LIB=build/live/$v/libfognet_hip.so timeout -k 10 300 python tools/replay_counters.py --mode $m --R $R --out $O/prof_${v}_${m}_R$R.json > /dev/null 2> $O/prof_$v.err || { tail $O/prof_$v.err; exit 1; }
