@@ -276,6 +276,9 @@ def main():
             dist.all_reduce(n_rep)
         hier_esc = {"escalating_replications": int(n_rep[0]), "escalating_fraction": int(n_rep[0]) / args.R_total,
                     "escalated_publishes": int(n_rep[1]), "threshold_s": args.hier_threshold_s}
+        # the path each launch took (fognet_hier_path_stats, warm-up included): the region pass, or
+        # straight to the sequential replay once a region pass handed most replications over
+        hier_esc["region_launches"], hier_esc["sequential_launches"] = ctx.hier_path_stats()
     if dist is not None:  # job totals over the ranks' shards
         tot = torch.tensor([ref["ref_defined_decisions"], ref["ref_aborted_replications"], ref["replications"]],
                            dtype=torch.int64, device=dev)
@@ -320,9 +323,13 @@ def main():
                        "parallelism": f"replications sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": ("replay_region_kernel (one wavefront per regional broker) + region_finish_kernel "
-                                    "(statistics pass)" + (" + replay_wide_kernel (the sequential replay of the handed-"
-                                                           "back replications)" if args.c5_recipe == "saturate" else "")
+                         "kernel": (("replay_wide_kernel (sequential replay of every replication: the warm-up's "
+                                     "region pass handed all of them over, so the automatic path choice skips it; "
+                                     "fognet_hier_path_stats)" if hier_esc and hier_esc["sequential_launches"] >= args.steps
+                                     else "replay_region_kernel (one wavefront per regional broker) + "
+                                     "region_finish_kernel (statistics pass)" +
+                                     (" + replay_wide_kernel (the sequential replay of the handed-back replications)"
+                                      if hier_esc and hier_esc["escalating_replications"] else ""))
                                     if args.policy == "EXT_HIER" and N > _abi.HIER_REGION_NODES
                                     else "replay_wide_kernel (statistics inline)" if N > 256
                                     else "replay_kernel (statistics pass fused)"), "kernel_avg_ms": replay_avg_s * 1e3,

@@ -201,6 +201,7 @@ SIGNATURES = {
     "fognet_run_generated_dev": (C.c_int, [P, C.POINTER(GenParams), C.c_int64, C.POINTER(BatchIn),
                                            C.POINTER(BatchOut), P]),
     "fognet_sync": (C.c_int, [P]),
+    "fognet_hier_path_stats": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "fognet_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "fognet_comm_create": (C.c_int, [P, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.POINTER(P)]),
     "fognet_comm_destroy": (None, [P]),

@@ -28,6 +28,14 @@ struct fognet_ctx {
   void* host_stage = nullptr;
   void* host_stage_dev = nullptr;
   size_t host_stage_bytes = 0;
+  // EXT_HIER path choice (fognet_hier_path_stats): the hand-over count of the last region pass,
+  // copied back into pinned memory on the launch stream and read once its event has passed
+  int32_t* hier_host = nullptr;  // [0] handed-over replications, [1] R of that launch
+  hipEvent_t hier_ev = nullptr;
+  bool hier_pending = false;
+  bool hier_seq = false;  // the last measured region pass handed most replications over
+  int hier_seq_runs = 0;  // launches sent straight to the sequential replay since that measurement
+  int64_t hier_region_launches = 0, hier_seq_launches = 0;
   std::string err;
 };
 
@@ -167,6 +175,10 @@ bool use_regions() {
   const char* f = getenv("FOGNET_HIER_REGIONS");
   return f == nullptr || strcmp(f, "0") != 0;
 }
+bool regions_auto() { return getenv("FOGNET_HIER_REGIONS") == nullptr; }
+// automatic mode: after a region pass that handed most replications over, this many launches go
+// straight to the sequential replay before a region pass measures again
+constexpr int kHierReprobe = 15;
 bool regions_only() {
   const char* f = getenv("FOGNET_HIER_REGIONS");
   return f != nullptr && strcmp(f, "only") == 0;
@@ -248,8 +260,17 @@ void fognet_destroy(fognet_ctx* c) {
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->red) (void)hipFree(c->red);
   if (c->host_stage) (void)hipHostFree(c->host_stage);
+  if (c->hier_ev) (void)hipEventSynchronize(c->hier_ev), (void)hipEventDestroy(c->hier_ev);
+  if (c->hier_host) (void)hipHostFree(c->hier_host);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+int fognet_hier_path_stats(const fognet_ctx* c, int64_t* region_launches, int64_t* sequential_launches) {
+  if (!c) return FOGNET_ERR_ARG;
+  if (region_launches) *region_launches = c->hier_region_launches;
+  if (sequential_launches) *sequential_launches = c->hier_seq_launches;
+  return FOGNET_OK;
 }
 
 const char* fognet_last_error(const fognet_ctx* c) { return c ? c->err.c_str() : "null context"; }
@@ -432,7 +453,24 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     if (!(which & 1)) return FOGNET_OK;
     a.no_task_out = stats_only ? 1 : 0;
     const int32_t B = (a.N + FOGNET_HIER_REGION_NODES - 1) / FOGNET_HIER_REGION_NODES;
-    if (a.policy == FOGNET_POLICY_EXT_HIER && !a.down && !stats_only && a.T > 0 && B >= 2 && use_regions()) {
+    const bool hier_split = a.policy == FOGNET_POLICY_EXT_HIER && !a.down && !stats_only && a.T > 0 && B >= 2;
+    bool regions = hier_split && use_regions();
+    if (regions && regions_auto()) {
+      // the last region pass's hand-over count, if it has reached the host (never waited for)
+      if (c->hier_pending && hipEventQuery(c->hier_ev) == hipSuccess) {
+        c->hier_pending = false;
+        c->hier_seq = 2 * (int64_t)c->hier_host[0] > (int64_t)c->hier_host[1];
+        c->hier_seq_runs = 0;
+      }
+      if (c->hier_seq && c->hier_seq_runs < kHierReprobe) {
+        regions = false;  // most replications escalated: the region pass would only be replayed again
+        ++c->hier_seq_runs;
+      } else {
+        c->hier_seq = false;  // (measure again)
+      }
+    }
+    if (hier_split) ++(regions ? c->hier_region_launches : c->hier_seq_launches);
+    if (regions) {
       // one wavefront per (replication, region) while no region escalates (replay_region.hip), the
       // statistics pass, then the sequential wide kernel for the replications some region handed back.
       // workspace: [hand-over counter | list [R] | quit flags [R] | region records [R][B] | segment offsets
@@ -487,7 +525,20 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       if (e != hipSuccess) return hip_fail(c, e, "region replay launch");
       if (regions_only()) return FOGNET_OK;
       e = fognet::launch_replay_wide(a, base + o_e, slots, (hipStream_t)stream);
-      return e == hipSuccess ? FOGNET_OK : hip_fail(c, e, "wide hand-over launch");
+      if (e != hipSuccess) return hip_fail(c, e, "wide hand-over launch");
+      if (regions_auto()) {  // the hand-over count back to the host, asynchronously
+        if (!c->hier_host && hipHostMalloc((void**)&c->hier_host, 2 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
+          c->hier_host = nullptr;
+        if (!c->hier_ev && hipEventCreateWithFlags(&c->hier_ev, hipEventDisableTiming) != hipSuccess) c->hier_ev = nullptr;
+        if (c->hier_host && c->hier_ev) {
+          c->hier_host[1] = a.R;
+          e = hipMemcpyAsync(c->hier_host, a.wide_count, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream);
+          if (e == hipSuccess) e = hipEventRecord(c->hier_ev, (hipStream_t)stream);
+          if (e != hipSuccess) return hip_fail(c, e, "hand-over count copy");
+          c->hier_pending = true;
+        }
+      }
+      return FOGNET_OK;
     }
     const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N);
     rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ws, "wide replay workspace");

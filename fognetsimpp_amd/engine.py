@@ -82,6 +82,13 @@ class Context:
     def sync(self):
         self.check(self._lib.fognet_sync(self._h), "sync")
 
+    def hier_path_stats(self) -> tuple[int, int]:
+        """EXT_HIER launches (N > 1024) that took the region pass / went straight to the
+        sequential replay (fognet_hier_path_stats; FOGNET_HIER_REGIONS in fognet_hip.h)."""
+        a, b = C.c_int64(0), C.c_int64(0)
+        self.check(self._lib.fognet_hier_path_stats(self._h, C.byref(a), C.byref(b)), "hier_path_stats")
+        return int(a.value), int(b.value)
+
 
 class BrokerBaseApp3:
     """Allocation policy of BrokerBaseApp3 (src/mqttapp/BrokerBaseApp3.cc).

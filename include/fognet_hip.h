@@ -493,6 +493,20 @@ int fognet_run_generated_dev(fognet_ctx *ctx, const fognet_gen_params *p, int64_
 /* Synchronise the context's device. */
 int fognet_sync(fognet_ctx *ctx);
 
+/* EXT_HIER with N > 1024 (more than one region), fognet_run_batch[_dev]: the path each
+ * launch took (diagnostic).  A launch first replays every (replication, region) pair on
+ * its own wavefront and hands a replication with any escalation to the sequential
+ * replay, which replays it from the start (region_launches); or it runs the sequential
+ * replay for every replication (sequential_launches).  Both give identical results.
+ * FOGNET_HIER_REGIONS (environment): unset -- automatic: while the last region pass
+ * whose hand-over count has reached the host (copied back asynchronously, read without
+ * waiting) handed more than half of its replications over, the next launches go
+ * straight to the sequential replay, with a region pass again every 16th launch to
+ * re-measure; "1" -- always the region pass; "0" -- always sequential; "only" -- the
+ * region pass without the hand-over (testing: a handed-over replication then reports
+ * FOGNET_ERR_UNSUPPORTED). */
+int fognet_hier_path_stats(const fognet_ctx *ctx, int64_t *region_launches, int64_t *sequential_launches);
+
 /* ---- Multi-GPU statistics exchange over RCCL (xGMI), SURVEY.md §8(b)
  * `fognet_allreduce_stats` and §8(e): replications are sharded over ranks (one
  * process per GPU) and this end-of-run exchange is the only collective.  RCCL

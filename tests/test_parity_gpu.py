@@ -1593,6 +1593,43 @@ def test_c5_ext_hier_escalations(ctx, monkeypatch, c5_saturated, mode):
     np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
 
 
+def test_c5_ext_hier_automatic_path(monkeypatch, c5_saturated):
+    """FOGNET_HIER_REGIONS unset (the default): the first launch takes the region
+    pass, which hands six of the eight replications over; once that count has
+    reached the host, the next launch goes straight to the sequential replay
+    (fognet_hier_path_stats); every output, record, per-node energy and histogram
+    equals the oracle on both launches.  A light C5 trace (no escalation) keeps the
+    region pass."""
+    tr, o = c5_saturated
+    monkeypatch.delenv("FOGNET_HIER_REGIONS", raising=False)
+    c = fa.Context(0)  # (a fresh context: the measurement is per context)
+    dev = torch.device("cuda", c.device)
+    d = fa.as_device_trace(tr, dev)
+    for launch in range(2):
+        out = fa.run_batch(c, d, policy="EXT_HIER", hier_threshold_s=60, hier_up_tick=20 * 10**9, hist=True)
+        torch.cuda.synchronize()
+        assert c.hier_path_stats() == ((1, 0) if launch == 0 else (1, 1))
+        st = out.rep_stats()
+        g = dict(node=out.node.cpu().numpy(), status=out.status.cpu().numpy(), start=out.start_tick.cpu().numpy(),
+                 done=out.done_tick.cpu().numpy(), stats=st)
+        assert (st["status"] == 0).all()
+        assert_parity(tr, g, o)
+        assert st.tobytes() == o["stats"].tobytes()
+        np.testing.assert_array_equal(out.node_energy.cpu().numpy(), o["node_energy"])
+        np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
+    R, T, N = 4, 10_000, 10_000
+    mg, sc = fa.c5_params(np.arange(R), N)
+    light = fa.generate_trace(c, 0x5EED0005, R, T, N, mg, sc)
+    light["region"] = fa.mobility_regions(light["arrive"], N)
+    c2 = fa.Context(0)
+    for _ in range(2):
+        fa.run_batch(c2, light, policy="EXT_HIER", hier_threshold_s=60, hier_up_tick=20 * 10**9)
+        torch.cuda.synchronize()
+    assert c2.hier_path_stats() == (2, 0)
+    c.close()
+    c2.close()
+
+
 @pytest.mark.parametrize("kind", ["ext_hier", "long"])
 def test_generated_wide_paths_equal_materialized(ctx, kind):
     """Generated replays the register kernel does not take run on the wide
