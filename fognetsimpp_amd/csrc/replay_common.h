@@ -544,10 +544,14 @@ __device__ __forceinline__ bool apply_wide_advert(WideNode& h, const WideEntry* 
 // (its tail's cumulative sum, nd[j].tl_C), each operation separately rounded, summed in node
 // order (0, 1, ..., N-1) by one wavefront (all 64 lanes active; the sum is returned in every
 // lane).  kDepth chunks of 64 nodes have their loads issued before the first of them is summed:
-// the sum is one dependent chain, so the record and power loads must not each wait in it.
+// the sum is one dependent chain, so the record and power loads must not each wait in it.  Each
+// chunk's 64 terms go through LDS (s_buf: 64 doubles of the caller's) and are read back by every
+// lane at the same address (a broadcast, 16 at a time), so the chain is a run of fp64 adds on
+// VGPRs; taking each term with v_readlane put an SGPR hand-off into every add (~80 cycles per
+// node at C5's 10,000 nodes).
 template <int kDepth = 8>
 __device__ __forceinline__ double energy_sum_wave(const WideNode* nd, const double* p_busy, const double* p_idle,
-                                                  int N, int64_t H, double* out_row, int lane) {
+                                                  int N, int64_t H, double* out_row, int lane, double* s_buf) {
   double sum = 0.0;
   for (int c0 = 0; c0 < N; c0 += kDepth * kWave) {
     double en[kDepth];
@@ -567,15 +571,26 @@ __device__ __forceinline__ double energy_sum_wave(const WideNode* nd, const doub
     for (int u = 0; u < kDepth; ++u) {
       const int j0 = c0 + u * kWave;
       const int m = min(kWave, N - j0);
+      if (m <= 0) break;
+      s_buf[lane] = en[u];
+      // every lane's term is in LDS before any lane reads the chunk (one wavefront)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
       if (m == kWave) {
-        // a full chunk: constant lane indices, no loop branch between the dependent adds (a
-        // counted loop cost ~40 cycles per node: readlane hazards, vcc compare, taken branch)
 #pragma unroll
-        for (int l = 0; l < kWave; ++l)
-          sum = add_rn(sum, __longlong_as_double(readlane_i64(__double_as_longlong(en[u]), l)));
+        for (int q = 0; q < kWave; q += 16) {
+          double v[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) v[k] = s_buf[q + k];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) sum = add_rn(sum, v[k]);
+        }
       } else {
-        for (int l = 0; l < m; ++l) sum = add_rn(sum, __longlong_as_double(readlane_i64(__double_as_longlong(en[u]), l)));
+        for (int l = 0; l < m; ++l) sum = add_rn(sum, s_buf[l]);
       }
+      // the chunk's reads are done before the next chunk's writes
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
     }
   }
   return sum;

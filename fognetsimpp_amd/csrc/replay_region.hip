@@ -549,6 +549,7 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   __shared__ uint32_t s_hist[FOGNET_HIST_METRICS * FOGNET_HIST_BINS];
   __shared__ int s_ok, s_done, s_mp;
   __shared__ double s_energy;
+  __shared__ double s_ebuf[kWave];  // the energy chain's terms, one chunk at a time
   __shared__ uint64_t s_busy;
   __shared__ int64_t s_last;
   if (tid < kWave) {  // the regions' records, one per lane (B <= 64: N <= 65,536)
@@ -622,7 +623,7 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
 #endif
       const int64_t H = n > 0 ? s_last : 0;
       const double sum = energy_sum_wave(nd, A.p_busy + nbase, A.p_idle + nbase, N, H,
-                                         A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, tid);
+                                         A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, tid, s_ebuf);
       if (tid == 0) s_energy = sum;
     }
   } else {

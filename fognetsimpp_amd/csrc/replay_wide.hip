@@ -1188,7 +1188,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     // per node j (lane j % 64 here), then summed in node order 64 at a time
     const int64_t H = n_done > 0 ? acc.last : 0;
     const double sum = energy_sum_wave(nd, A.p_busy + nbase, A.p_idle + nbase, N, H,
-                                       A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, lane);
+                                       A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, lane,
+                                       reinterpret_cast<double*>(L.g_nxt));  // (the group minima are dead here)
     if (lane == 0) S->energy_j = sum;
   }
   if (hist) {

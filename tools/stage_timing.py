@@ -17,7 +17,10 @@ tr = fa.generate_trace(ctx, 0x5EED0005 if C5 else 0x5EED0003, R, T, N, mg, sc)
 POL = os.environ.get("POLICY", "REF_V3")
 if POL == "EXT_HIER":
     tr["region"] = fa.mobility_regions(tr["arrive"], N)
-out = fa.allocate_outputs(R, T, dev, N=N, energy=False, hist=True)
+if os.environ.get("POWER"):  # the a11 power model (energy per node and per replication), as the bench runs it
+    pb, pi = fa.power_model(tr["mips"].cpu().numpy())
+    tr["p_busy"], tr["p_idle"] = torch.as_tensor(pb, device=dev), torch.as_tensor(pi, device=dev)
+out = fa.allocate_outputs(R, T, dev, N=N, energy=bool(os.environ.get("POWER")), hist=True)
 torch.cuda.synchronize()
 for stage in os.environ.get("FOGNET_STAGES", "all,replay,stats,all,replay").split(","):
     ts = []
