@@ -40,7 +40,10 @@ constexpr int kRegionSlots = FOGNET_HIER_REGION_NODES / kWave;  // 16 view slots
 static_assert(kRegionSlots == kWideGroupSlots, "a region is one wide-kernel group row");
 constexpr uint32_t kRegBusySat = 0xFFFFFFFFu;
 constexpr uint32_t kRegSCap = 1u << 22;  // the wide kernel's kWideSCap: past it the sequential kernel decides
-constexpr uint32_t kRegWCap = 1u << 21;  // run-horizon offsets are capped like replay_wide.hip's node_w
+// Run-horizon offsets are capped (replay_wide.hip's node_w caps at 2^21 s): a smaller offset only
+// shortens runs.  16 bits here, so the view ticks and offsets take 10 KiB of LDS per wavefront and
+// 16 wavefronts fit per CU (12 KiB with 32-bit offsets: 13); C5's offsets are minutes at most.
+constexpr uint32_t kRegWCap = 0xFFFFu;
 
 // Internal per-(replication, region) status: replay the replication sequentially
 // (fognet_hip.h never returns it; under FOGNET_HIER_REGIONS=only the finish kernel
@@ -137,7 +140,7 @@ __device__ __forceinline__ uint32_t w_offset(const WideNode& h, int64_t dl) {
   return v1 < (uint64_t)kRegWCap ? (uint32_t)v1 : kRegWCap;
 }
 
-// 4 waves per SIMD (<= 128 VGPRs); 12 KiB of LDS per wavefront (view ticks and horizon offsets).
+// 4 waves per SIMD (<= 128 VGPRs); 10 KiB of LDS per wavefront (view ticks and horizon offsets).
 __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, RegionWs W) {
   const int B = W.B;
   const int r = blockIdx.x / B, b = blockIdx.x - (blockIdx.x / B) * B;
@@ -162,9 +165,9 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   // (conflict-free); advertised busy times in HBM (RegionWs::vb; read back only by a key
   // rescan of a lane without a zero-busy slot)
   __shared__ int64_t s_nxt[kRegionSlots * kWave];
-  __shared__ uint32_t s_woff[kRegionSlots * kWave];
+  __shared__ uint16_t s_woff[kRegionSlots * kWave];
   int64_t* const vnxt = s_nxt + lane;  // vnxt[s * kWave]: slot s of this lane
-  uint32_t* const vwoff = s_woff + lane;
+  uint16_t* const vwoff = s_woff + lane;
   uint32_t* const vbusy = W.vb + (size_t)rb * (size_t)(kRegionSlots * kWave) + lane;
   bool bad = false;
   // slots with an advert pending (view tick not kNever) and slots whose advertised busy
@@ -322,7 +325,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
             }
             lbroken |= broken;
             vnxt[sl * kWave] = nxt_j;
-            vwoff[sl * kWave] = off_j;
+            vwoff[sl * kWave] = (uint16_t)off_j;
             vbusy[sl * kWave] = busy_j;
             act = nxt_j != kNever ? act | (1u << sl) : act & ~(1u << sl);
             nzb = busy_j != 0u ? nzb | (1u << sl) : nzb & ~(1u << sl);
@@ -491,7 +494,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
         h.npend += Lr;
         ch = h;
         max_pend = max(max_pend, (uint32_t)h.npend);
-        vwoff[sk * kWave] = w_offset(h, dl_k);  // k's horizon offset
+        vwoff[sk * kWave] = (uint16_t)w_offset(h, dl_k);  // k's horizon offset
       }
       n_done += Lr;
       PRC(6, Lr);
