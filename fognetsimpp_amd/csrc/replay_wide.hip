@@ -768,16 +768,33 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           int64_t gmn = nxt_j, gmw = w_j;
           int gsi = si;
           if constexpr (!kPerPublish) V.w[sl] = w_j;
-          for (uint32_t m = gm0 & 0xFFFFu & ~bit; m; m &= m - 1u) {
-            const int i = __builtin_ctz(m);
-            const int64_t x = V.nxt[g * kWideGroupSlots + i];
-            int64_t w = kNever;
-            if constexpr (!kPerPublish) w = V.w[g * kWideGroupSlots + i];
-            if (x < gmn || (x == gmn && i < gsi)) {
-              gmn = x;
-              gsi = i;
+          // the group's other pending slots, four at a time: their view loads are all issued before
+          // the first compare (one HBM round trip per four slots, not per slot)
+          for (uint32_t m = gm0 & 0xFFFFu & ~bit; m;) {
+            int ix[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              ok[u] = m != 0u;
+              ix[u] = ok[u] ? __builtin_ctz(m) : 0;
+              m = ok[u] ? m & (m - 1u) : m;
             }
-            gmw = w < gmw ? w : gmw;
+            int64_t xs[4], ws[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              xs[u] = V.nxt[g * kWideGroupSlots + ix[u]];
+              ws[u] = kNever;
+              if constexpr (!kPerPublish) ws[u] = V.w[g * kWideGroupSlots + ix[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (!ok[u]) continue;
+              if (xs[u] < gmn || (xs[u] == gmn && ix[u] < gsi)) {
+                gmn = xs[u];
+                gsi = ix[u];
+              }
+              gmw = ws[u] < gmw ? ws[u] : gmw;
+            }
           }
           L.g_nxt[g * kWave + lane] = gmn;
           L.g_j[g * kWave + lane] = gmn == kNever ? lane : wnode<kHier>(g * kWideGroupSlots + gsi, lane);
