@@ -359,6 +359,8 @@ struct RegionWs {
   uint8_t* o_status; //        writes them to the caller's arrays in trace order)
   int64_t* o_start;
   int64_t* o_done;
+  uint32_t* okey;  // [R][B] dispatch key of each (replication, region): estimated load, quantised (region_sort_kernel)
+  int32_t* perm;   // [R * B] the region wavefronts' dispatch order: lightest estimated load first (region_order_kernel)
   int32_t B;       // regions: ceil(N / FOGNET_HIER_REGION_NODES)
 };
 hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s);

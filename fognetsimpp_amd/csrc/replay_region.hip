@@ -62,7 +62,16 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
   __shared__ uint32_t s_cnt[kWave];             // per region: count, then the next free position
   __shared__ uint32_t s_wc[kSortWaves][kWave];  // per wave and region: the tile's publishes
   __shared__ int s_bad;
-  if (tid < kWave) s_cnt[tid] = 0u;
+  // the dispatch key's inputs per region: publishes, first and last tick, requirements, node MIPS
+  __shared__ uint32_t s_n[kWave];
+  __shared__ unsigned long long s_t0[kWave], s_t1[kWave], s_rq[kWave], s_mp[kWave];
+  if (tid < kWave) {
+    s_cnt[tid] = 0u;
+    s_t0[tid] = ~0ull;
+    s_t1[tid] = 0ull;
+    s_rq[tid] = 0ull;
+    s_mp[tid] = 0ull;
+  }
   if (tid == 0) s_bad = 0;
   __syncthreads();
   // counts, and the trace preconditions the sequential kernel reports (nondecreasing ticks,
@@ -72,8 +81,19 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
     const int32_t g = A.region[tbase + i];
     const int64_t t = A.arrive[tbase + i];
     const int64_t tp = i > 0 ? A.arrive[tbase + i - 1] : INT64_MIN;
-    if (g < 0 || g >= B || A.req[tbase + i] < 0 || t > kMaxTick || t < tp) bad = true;
-    else atomicAdd(&s_cnt[g], 1u);
+    const int32_t q = A.req[tbase + i];
+    if (g < 0 || g >= B || q < 0 || t > kMaxTick || t < tp) {
+      bad = true;
+    } else {
+      atomicAdd(&s_cnt[g], 1u);
+      atomicMin(&s_t0[g], (unsigned long long)t);
+      atomicMax(&s_t1[g], (unsigned long long)t);
+      atomicAdd(&s_rq[g], (unsigned long long)q);
+    }
+  }
+  for (int j = tid; j < A.N; j += kSortThreads) {
+    const int32_t m = A.mips[(size_t)r * (size_t)A.node_stride + j];
+    atomicAdd(&s_mp[j / FOGNET_HIER_REGION_NODES], (unsigned long long)(m > 0 ? m : 1));
   }
   if (bad) s_bad = 1;
   __syncthreads();
@@ -82,6 +102,23 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
     return;
   }
   int32_t* const seg = W.seg + (size_t)r * (size_t)(B + 1);
+  if (tid < B) {
+    // dispatch key: the region's estimated load, rho = (requirements / mean MIPS) seconds of service
+    // over (span x nodes); a lighter region decides in more, shorter runs (one per publish at
+    // the lightest), so its wavefront runs longer: the region wavefronts are dispatched lightest
+    // first (region_order_kernel), longest first.  Only the schedule changes, never a result.
+    const int nb = min(FOGNET_HIER_REGION_NODES, A.N - tid * FOGNET_HIER_REGION_NODES);
+    const uint32_t n = s_cnt[tid];
+    uint32_t key = 255u;  // (no publish: last)
+    if (n > 0u) {
+      const double span = (double)(s_t1[tid] - s_t0[tid]) * 1e-12 + 1e-3;
+      const double svc = (double)s_rq[tid] / ((double)s_mp[tid] / (double)nb);
+      const double rho = svc / (span * (double)nb);
+      const double q = 8.0 * log2(rho > 1e-30 ? rho : 1e-30) + 128.0;
+      key = (uint32_t)(q < 0.0 ? 0.0 : (q > 254.0 ? 254.0 : q));
+    }
+    W.okey[(size_t)r * B + tid] = key;
+  }
   if (tid == 0) {
     uint32_t acc = 0u;
     for (int b = 0; b < B; ++b) {
@@ -127,6 +164,28 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
   }
 }
 
+// ---- region_order_kernel: the region wavefronts' dispatch order, by key (one block; counting
+// sort, any order within a key)
+constexpr int kOrderThreads = 1024;
+__global__ __launch_bounds__(kOrderThreads) void region_order_kernel(int32_t n, RegionWs W) {
+  __shared__ uint32_t s_h[256];
+  const int tid = threadIdx.x;
+  if (tid < 256) s_h[tid] = 0u;
+  __syncthreads();
+  for (int i = tid; i < n; i += kOrderThreads) atomicAdd(&s_h[W.okey[i] & 255u], 1u);
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0u;
+    for (int k = 0; k < 256; ++k) {
+      const uint32_t c = s_h[k];
+      s_h[k] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += kOrderThreads) W.perm[atomicAdd(&s_h[W.okey[i] & 255u], 1u)] = i;
+}
+
 // ---- replay_region_kernel
 // Run horizon offset of a node (replay.hip horizon_all_in): with every pending
 // task arrived before its head completes, the node's next advert carries
@@ -143,7 +202,8 @@ __device__ __forceinline__ uint32_t w_offset(const WideNode& h, int64_t dl) {
 // 4 waves per SIMD (<= 128 VGPRs); 10 KiB of LDS per wavefront (view ticks and horizon offsets).
 __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, RegionWs W) {
   const int B = W.B;
-  const int r = blockIdx.x / B, b = blockIdx.x - (blockIdx.x / B) * B;
+  const int item = W.perm[blockIdx.x];  // (region_order_kernel's dispatch order)
+  const int r = item / B, b = item - (item / B) * B;
   const int rb = r * B + b;  // (r, b)'s region record and busy view
   const int lane = threadIdx.x;
   const int T = A.T, N = A.N;
@@ -721,6 +781,9 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
 hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s) {
   hipLaunchKernelGGL(region_sort_kernel, dim3(a.R), dim3(kSortThreads), 0, s, a, w);
   hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(region_order_kernel, dim3(1), dim3(kOrderThreads), 0, s, (int32_t)(a.R * w.B), w);
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w);
   e = hipGetLastError();
