@@ -474,7 +474,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       // one wavefront per (replication, region) while no region escalates (replay_region.hip), the
       // statistics pass, then the sequential wide kernel for the replications some region handed back.
       // workspace: [hand-over counter | list [R] | quit flags [R] | region records [R][B] | segment offsets
-      // [R][B+1] | dispatch keys [R][B] | dispatch order [R*B] | entries [R][T] | node records [R][N] | busy view [R][B][1024] | region-sorted trace and
+      // [R][B+1] | dispatch keys [R][B] | dispatch order [R*B] | node tails [R][N][2] | entries [R][T] | node records [R][N] | busy view [R][B][1024] | region-sorted trace and
       // outputs [R][T]]; the hand-over launch reuses the space from the entries on (stream order: after the
       // finish kernel has read the node records and the sorted outputs), with one workspace slot per
       // handed-over replication up to kWideFallbackSlots (an escalation-heavy job replays its hand-overs
@@ -485,7 +485,8 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       const size_t o_seg = o_rec + align256((size_t)a.R * (size_t)B * sizeof(fognet::RegionRec));
       const size_t o_ok = o_seg + align256((size_t)a.R * (size_t)(B + 1) * sizeof(int32_t));
       const size_t o_perm = o_ok + align256((size_t)a.R * (size_t)B * sizeof(uint32_t));
-      const size_t o_e = o_perm + align256((size_t)a.R * (size_t)B * sizeof(int32_t));
+      const size_t o_tails = o_perm + align256((size_t)a.R * (size_t)B * sizeof(int32_t));
+      const size_t o_e = o_tails + align256((size_t)a.R * (size_t)a.N * 2 * sizeof(int64_t));
       const size_t o_nd = o_e + align256(RT * sizeof(fognet::WideEntry));
       const size_t o_vb = o_nd + align256((size_t)a.R * (size_t)a.N * sizeof(fognet::WideNode));
       const size_t o_sa = o_vb + align256((size_t)a.R * (size_t)B * FOGNET_HIER_REGION_NODES * sizeof(uint32_t));
@@ -516,6 +517,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       w.seg = reinterpret_cast<int32_t*>(base + o_seg);
       w.okey = reinterpret_cast<uint32_t*>(base + o_ok);
       w.perm = reinterpret_cast<int32_t*>(base + o_perm);
+      w.tails = reinterpret_cast<int64_t*>(base + o_tails);
       w.s_arr = reinterpret_cast<int64_t*>(base + o_sa);
       w.s_req = reinterpret_cast<int32_t*>(base + o_sq);
       w.inv = reinterpret_cast<int32_t*>(base + o_inv);

@@ -359,6 +359,9 @@ struct RegionWs {
   uint8_t* o_status; //        writes them to the caller's arrays in trace order)
   int64_t* o_start;
   int64_t* o_done;
+  int64_t* tails;  // [R][N][2] every node's tail completion tick (INT64_MIN: no task) and service seconds (tl_C):
+                   // written at the region pass's start, at each write-back of a lane's cached record and at its
+                   // end, so the finish kernel reads 16 B per node instead of the 64-B records
   uint32_t* okey;  // [R][B] dispatch key of each (replication, region): estimated load, quantised (region_sort_kernel)
   int32_t* perm;   // [R * B] the region wavefronts' dispatch order: lightest estimated load first (region_order_kernel)
   int32_t B;       // regions: ceil(N / FOGNET_HIER_REGION_NODES)

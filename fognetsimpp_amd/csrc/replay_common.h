@@ -541,7 +541,7 @@ __device__ __forceinline__ bool apply_wide_advert(WideNode& h, const WideEntry* 
 
 // ---------------------------------------------------------------- a11 energy over node records
 // E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12) with B_j = node j's service seconds
-// (its tail's cumulative sum, nd[j].tl_C), each operation separately rounded, summed in node
+// (its tail's cumulative sum, tl_C), each operation separately rounded, summed in node
 // order (0, 1, ..., N-1) by one wavefront (all 64 lanes active; the sum is returned in every
 // lane).  kDepth chunks of 64 nodes have their loads issued before the first of them is summed:
 // the sum is one dependent chain, so the record and power loads must not each wait in it.  Each
@@ -550,8 +550,11 @@ __device__ __forceinline__ bool apply_wide_advert(WideNode& h, const WideEntry* 
 // VGPRs; taking each term with v_readlane put an SGPR hand-off into every add (~80 cycles per
 // node at C5's 10,000 nodes).
 template <int kDepth = 8>
-__device__ __forceinline__ double energy_sum_wave(const WideNode* nd, const double* p_busy, const double* p_idle,
-                                                  int N, int64_t H, double* out_row, int lane, double* s_buf) {
+// tlc: node j's service seconds at tlc[j * stride] (the records' tl_C: stride 8 over WideNode;
+// the region pass's compact tails: stride 2).
+__device__ __forceinline__ double energy_sum_wave(const uint64_t* tlc, int stride, const double* p_busy,
+                                                  const double* p_idle, int N, int64_t H, double* out_row, int lane,
+                                                  double* s_buf) {
   double sum = 0.0;
   for (int c0 = 0; c0 < N; c0 += kDepth * kWave) {
     double en[kDepth];
@@ -560,7 +563,7 @@ __device__ __forceinline__ double energy_sum_wave(const WideNode* nd, const doub
       const int j = c0 + u * kWave + lane;
       en[u] = 0.0;
       if (j < N) {
-        const int64_t B = (int64_t)nd[j].tl_C;
+        const int64_t B = (int64_t)tlc[(size_t)j * (size_t)stride];
         const double eb = mul_rn(p_busy[j], (double)B);
         const double idle = __ddiv_rn((double)(H - B * kTicksPerSecond), 1e12);
         en[u] = add_rn(eb, mul_rn(p_idle[j], idle));

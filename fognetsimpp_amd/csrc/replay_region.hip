@@ -62,8 +62,7 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
   __shared__ uint32_t s_cnt[kWave];             // per region: count, then the next free position
   __shared__ uint32_t s_wc[kSortWaves][kWave];  // per wave and region: the tile's publishes
   __shared__ int s_bad;
-  // the dispatch key's inputs per region: publishes, first and last tick, requirements, node MIPS
-  __shared__ uint32_t s_n[kWave];
+  // the dispatch key's inputs per region (besides its count): first and last tick, requirements, node MIPS
   __shared__ unsigned long long s_t0[kWave], s_t1[kWave], s_rq[kWave], s_mp[kWave];
   if (tid < kWave) {
     s_cnt[tid] = 0u;
@@ -213,6 +212,13 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   const size_t tbase = (size_t)r * (size_t)T;
   WideEntry* const e = W.e + tbase;  // indexed by sorted position
   WideNode* const nd = W.nd + (size_t)r * (size_t)N;
+  int64_t* const tails = W.tails + 2 * (size_t)r * (size_t)N;
+  // node j's tail (completion, service seconds) for the finish kernel: a node's tail changes only
+  // when a run is pushed onto it, i.e. while it is a lane's cached node
+  auto write_tail = [&](int j, const WideNode& h) {
+    tails[2 * (size_t)j] = h.tl >= 0 ? h.tl_done : INT64_MIN;
+    tails[2 * (size_t)j + 1] = (int64_t)h.tl_C;
+  };
   const int32_t* const seg = W.seg + (size_t)r * (size_t)(B + 1);
   const int64_t arrive0 = T > 0 ? A.arrive[tbase] : kNever;
   uint32_t err = __hip_atomic_load(W.quit + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0
@@ -247,6 +253,8 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
       const int64_t d = A.dl[nbase + j], u = A.ul[nbase + j], ia = A.init[nbase + j];
       bad |= (m <= 0) | (d < 0) | (u < 0) | (d > kMaxTick) | (u > kMaxTick) | (ia < u) | (ia >= arrive0);
       nd[j] = WideNode{-1, -1, 0, -1, 0, 0u, 0, 0, 0u, 0u, 0u};
+      tails[2 * (size_t)j] = INT64_MIN;  // (no task yet)
+      tails[2 * (size_t)j + 1] = 0;
     }
   }
   // the lane's earliest advert (slot ms) and smallest view key (busy << 32 | j)
@@ -300,7 +308,10 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   int64_t c_dl = 0, c_ul = 0;
   auto cache_node = [&](uint32_t kk, int kl) {
     if (lane == kl && (int)kk != cj) {
-      if (cj >= 0) nd[cj] = ch;
+      if (cj >= 0) {
+        nd[cj] = ch;
+        write_tail(cj, ch);
+      }
       cj = (int)kk;
       ch = nd[kk];
       c_dv = udiv_magic((uint32_t)A.mips[nbase + kk]);
@@ -574,7 +585,10 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
       W.o_done[o] = q_done;
     }
   }
-  if (cj >= 0) nd[cj] = ch;
+  if (cj >= 0) {
+    nd[cj] = ch;
+    write_tail(cj, ch);
+  }
 #ifdef FOGNET_REGION_PROF
   pr[11] = clock64() - pt0;
   if (lane == 0 && (blockIdx.x < 3 || blockIdx.x % 997 == 7))
@@ -640,25 +654,25 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   fognet_rep_stats* const S = A.out_stats + r;
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)A.T;
-  const WideNode* const nd = W.nd + (size_t)r * (size_t)N;
   for (int h = tid; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kFinThreads) s_hist[h] = 0u;
   s_abt[tid] = INT64_MAX;
   s_abk[tid] = INT32_MAX;
-  // busy seconds and the last completion from the node tails (2 records in flight per thread)
+  // busy seconds and the last completion from the node tails (the region pass's compact copy,
+  // 16 B per node; four in flight per thread)
+  const int64_t* const tails = W.tails + 2 * (size_t)r * (size_t)N;
   Acc a = acc_identity();
-  for (int j0 = tid; j0 < N; j0 += 2 * kFinThreads) {
-    WideNode x[2];
+  for (int j0 = tid; j0 < N; j0 += 4 * kFinThreads) {
+    int64_t td[4], tc[4];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int j = j0 + u * kFinThreads;
-      x[u] = j < N ? nd[j] : WideNode{-1, -1, 0, -1, 0, 0u, 0, 0, 0u, 0u, 0u};
+      td[u] = j < N ? tails[2 * (size_t)j] : INT64_MIN;
+      tc[u] = j < N ? tails[2 * (size_t)j + 1] : 0;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (x[u].tl >= 0) {
-        a.busy += x[u].tl_C;
-        a.last = max(a.last, x[u].tl_done);
-      }
+    for (int u = 0; u < 4; ++u) {
+      a.busy += (uint64_t)tc[u];
+      a.last = max(a.last, td[u]);
     }
   }
   a = wave_merge(a);
@@ -685,7 +699,8 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
     if (false) {  // timing probe only
 #endif
       const int64_t H = n > 0 ? s_last : 0;
-      const double sum = energy_sum_wave(nd, A.p_busy + nbase, A.p_idle + nbase, N, H,
+      const double sum = energy_sum_wave(reinterpret_cast<const uint64_t*>(tails) + 1, 2, A.p_busy + nbase,
+                                         A.p_idle + nbase, N, H,
                                          A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, tid, s_ebuf);
       if (tid == 0) s_energy = sum;
     }

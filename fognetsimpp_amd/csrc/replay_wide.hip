@@ -1204,7 +1204,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     __syncthreads();  // (the records written back above by their owner lanes are read by others)
     // per node j (lane j % 64 here), then summed in node order 64 at a time
     const int64_t H = n_done > 0 ? acc.last : 0;
-    const double sum = energy_sum_wave(nd, A.p_busy + nbase, A.p_idle + nbase, N, H,
+    static_assert(sizeof(WideNode) % sizeof(uint64_t) == 0 && offsetof(WideNode, tl_C) % sizeof(uint64_t) == 0, "tl_C stride");
+    const double sum = energy_sum_wave(reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(nd) + offsetof(WideNode, tl_C)),
+                                       (int)(sizeof(WideNode) / sizeof(uint64_t)), A.p_busy + nbase, A.p_idle + nbase, N, H,
                                        A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, lane,
                                        reinterpret_cast<double*>(L.g_nxt));  // (the group minima are dead here)
     if (lane == 0) S->energy_j = sum;
