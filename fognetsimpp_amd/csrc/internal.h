@@ -101,6 +101,15 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   return readlane_u32(v, 0) + readlane_u32(v, 16) + readlane_u32(v, 32) + readlane_u32(v, 48);
 }
 
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+  v += dpp_u64<0xB1>(v);
+  v += dpp_u64<0x4E>(v);
+  v += dpp_u64<0x141>(v);
+  v += dpp_u64<0x140>(v);
+  return (uint64_t)readlane_i64((int64_t)v, 0) + (uint64_t)readlane_i64((int64_t)v, 16) +
+         (uint64_t)readlane_i64((int64_t)v, 32) + (uint64_t)readlane_i64((int64_t)v, 48);
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 
 struct U4 {

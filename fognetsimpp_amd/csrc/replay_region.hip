@@ -62,20 +62,17 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
   __shared__ uint32_t s_cnt[kWave];             // per region: count, then the next free position
   __shared__ uint32_t s_wc[kSortWaves][kWave];  // per wave and region: the tile's publishes
   __shared__ int s_bad;
-  // the dispatch key's inputs per region (besides its count): first and last tick, requirements, node MIPS
-  __shared__ unsigned long long s_t0[kWave], s_t1[kWave], s_rq[kWave], s_mp[kWave];
-  if (tid < kWave) {
-    s_cnt[tid] = 0u;
-    s_t0[tid] = ~0ull;
-    s_t1[tid] = 0ull;
-    s_rq[tid] = 0ull;
-    s_mp[tid] = 0ull;
-  }
+  // the dispatch key's inputs: the replication's requirement and MIPS totals (per-wave partials),
+  // each region's first sorted position
+  __shared__ unsigned long long s_rq[kSortWaves], s_mp[kSortWaves];
+  __shared__ uint32_t s_seg[kWave + 1];
+  if (tid < kWave) s_cnt[tid] = 0u;
   if (tid == 0) s_bad = 0;
   __syncthreads();
   // counts, and the trace preconditions the sequential kernel reports (nondecreasing ticks,
   // requirement >= 0, ticks < 2^61, a region of the node set): a violation hands r over
   bool bad = false;
+  uint64_t rq = 0u, mp = 0u;
   for (int i = tid; i < T; i += kSortThreads) {
     const int32_t g = A.region[tbase + i];
     const int64_t t = A.arrive[tbase + i];
@@ -85,14 +82,18 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
       bad = true;
     } else {
       atomicAdd(&s_cnt[g], 1u);
-      atomicMin(&s_t0[g], (unsigned long long)t);
-      atomicMax(&s_t1[g], (unsigned long long)t);
-      atomicAdd(&s_rq[g], (unsigned long long)q);
+      rq += (uint32_t)q;
     }
   }
   for (int j = tid; j < A.N; j += kSortThreads) {
     const int32_t m = A.mips[(size_t)r * (size_t)A.node_stride + j];
-    atomicAdd(&s_mp[j / FOGNET_HIER_REGION_NODES], (unsigned long long)(m > 0 ? m : 1));
+    mp += (uint32_t)(m > 0 ? m : 1);
+  }
+  rq = wave_sum_u64(rq);
+  mp = wave_sum_u64(mp);
+  if (lane == 0) {
+    s_rq[wv] = rq;
+    s_mp[wv] = mp;
   }
   if (bad) s_bad = 1;
   __syncthreads();
@@ -101,32 +102,17 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
     return;
   }
   int32_t* const seg = W.seg + (size_t)r * (size_t)(B + 1);
-  if (tid < B) {
-    // dispatch key: the region's estimated load, rho = (requirements / mean MIPS) seconds of service
-    // over (span x nodes); a lighter region decides in more, shorter runs (one per publish at
-    // the lightest), so its wavefront runs longer: the region wavefronts are dispatched lightest
-    // first (region_order_kernel), longest first.  Only the schedule changes, never a result.
-    const int nb = min(FOGNET_HIER_REGION_NODES, A.N - tid * FOGNET_HIER_REGION_NODES);
-    const uint32_t n = s_cnt[tid];
-    uint32_t key = 255u;  // (no publish: last)
-    if (n > 0u) {
-      const double span = (double)(s_t1[tid] - s_t0[tid]) * 1e-12 + 1e-3;
-      const double svc = (double)s_rq[tid] / ((double)s_mp[tid] / (double)nb);
-      const double rho = svc / (span * (double)nb);
-      const double q = 8.0 * log2(rho > 1e-30 ? rho : 1e-30) + 128.0;
-      key = (uint32_t)(q < 0.0 ? 0.0 : (q > 254.0 ? 254.0 : q));
-    }
-    W.okey[(size_t)r * B + tid] = key;
-  }
   if (tid == 0) {
     uint32_t acc = 0u;
     for (int b = 0; b < B; ++b) {
       const uint32_t c = s_cnt[b];
       s_cnt[b] = acc;
       seg[b] = (int32_t)acc;
+      s_seg[b] = acc;
       acc += c;
     }
     seg[B] = (int32_t)acc;
+    s_seg[B] = acc;
   }
   // tiles of kSortThreads publishes: a publish's position = its region's next free position + the
   // publishes of its region in earlier waves of the tile + those in earlier lanes of its wave
@@ -160,6 +146,29 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
       s_cnt[tid] += c;
     }
     __syncthreads();
+  }
+  if (tid < B) {
+    // dispatch key: the region's estimated load, rho = (its publishes x the replication's mean
+    // service seconds) over (its span x its nodes), from its first and last sorted publish; a
+    // lighter region decides in more, shorter runs (one per publish at the lightest), so its
+    // wavefront runs longer: the region wavefronts are dispatched lightest first
+    // (region_order_kernel), i.e. longest first.  Only the schedule changes, never a result.
+    const int nb = min(FOGNET_HIER_REGION_NODES, A.N - tid * FOGNET_HIER_REGION_NODES);
+    const uint32_t p0 = s_seg[tid], n = s_seg[tid + 1] - p0;
+    uint32_t key = 255u;  // (no publish: last)
+    if (n > 0u) {
+      uint64_t rqt = 0u, mpt = 0u;
+      for (int w = 0; w < kSortWaves; ++w) {
+        rqt += s_rq[w];
+        mpt += s_mp[w];
+      }
+      const double svc = ((double)rqt / (double)(T > 0 ? T : 1)) / ((double)mpt / (double)A.N);
+      const double span = (double)(W.s_arr[tbase + p0 + n - 1] - W.s_arr[tbase + p0]) * 1e-12 + 1e-3;
+      const double rho = (double)n * svc / (span * (double)nb);
+      const double q = 8.0 * log2(rho > 1e-30 ? rho : 1e-30) + 128.0;
+      key = (uint32_t)(q < 0.0 ? 0.0 : (q > 254.0 ? 254.0 : q));
+    }
+    W.okey[(size_t)r * B + tid] = key;
   }
 }
 
