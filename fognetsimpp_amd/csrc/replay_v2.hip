@@ -52,6 +52,12 @@ constexpr uint8_t kListNone = 0, kListLocal = 1, kListForwarded = 2;
 // 10-ms adverts between two MIPS changes: about half of all FES events.
 constexpr bool kPhantomAdverts = true;
 
+// replay_v2_kernel<NPL>: from this many nodes per lane on, a node's state is split
+// (the per-slot earliest event in VGPRs, the record indexed by slot; see the kernel)
+#ifndef FOGNET_V2_COLD_NPL
+#define FOGNET_V2_COLD_NPL 8
+#endif
+
 // Batched timer firings (replay_v2_rows_kernel).  A node's firing that releases
 // nothing (ComputeBrokerApp2.cc:222-245 finds no expired reservation, or the
 // self-message is ADVERTISEMIPS) touches only its node: it sends the advert
@@ -150,6 +156,17 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
   const int64_t stop = A.stop_tick[r];
 
   V2Node nd[NPL];
+  // NPL >= 8 (N > 256): a node's whole state does not fit in VGPRs next to the
+  // others', so it is split.  Every step's scan reads, for every slot, the node's
+  // earliest event (tick, sequence, source) and the broker's view of it: those stay
+  // in VGPRs (static slot index); the rest of the node's state is touched only by
+  // the handler of an event of that node (wave-uniform slot ws), so `nd` is indexed
+  // by ws directly and goes to scratch, read by one handler per step instead of by
+  // every step's scan.  NPL <= 4 keeps everything in VGPRs (static slot loops).
+  constexpr bool kCold = NPL >= FOGNET_V2_COLD_NPL;
+  int64_t h_tick[kCold ? NPL : 1];
+  uint64_t h_seq[kCold ? NPL : 1];
+  int32_t h_src[kCold ? NPL : 1], h_view[kCold ? NPL : 1];
   bool bad = !(stop <= kMaxV2Tick) || !(rtx >= 0.0) || rt_ticks > kMaxV2Tick;
 #pragma unroll
   for (int s = 0; s < NPL; ++s) {
@@ -180,6 +197,59 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       x.t_seq = (uint64_t)j;
     }
   }
+  // a node's earliest event: its self-message, its next task arrival, its next message at the broker
+  auto key_of = [](const V2Node& x, int64_t& kt, uint64_t& ks, int32_t& ksrc) {
+    kt = kNever;
+    ks = ~0ull;
+    ksrc = 0;
+    if (x.t_sched) {
+      kt = x.t_tick;
+      ks = x.t_seq;
+      ksrc = 1;
+    }
+    if (x.in_n && earlier(x.in_hd.tick, x.in_hd.seq, kt, ks)) {
+      kt = x.in_hd.tick;
+      ks = x.in_hd.seq;
+      ksrc = 2;
+    }
+    if (x.out_n && earlier(x.out_hd.tick, x.out_hd.seq, kt, ks)) {
+      kt = x.out_hd.tick;
+      ks = x.out_hd.seq;
+      ksrc = 3;
+    }
+  };
+  // refresh slot ws's VGPR copy from its record (kCold; the owner lane, after its handler)
+  auto refresh = [&](int ws) {
+    if constexpr (kCold) {
+      int64_t kt;
+      uint64_t ks;
+      int32_t ksrc;
+      const V2Node& x = nd[ws];
+      key_of(x, kt, ks, ksrc);
+      const int32_t v = x.view;
+#pragma unroll
+      for (int s2 = 0; s2 < NPL; ++s2) {
+        if (s2 == ws) {
+          h_tick[s2] = kt;
+          h_seq[s2] = ks;
+          h_src[s2] = ksrc;
+          h_view[s2] = v;
+        }
+      }
+    }
+  };
+  if constexpr (kCold) {
+#pragma unroll
+    for (int s = 0; s < NPL; ++s) {
+      key_of(nd[s], h_tick[s], h_seq[s], h_src[s]);
+      h_view[s] = nd[s].view;
+    }
+  }
+  // the broker's view of slot s (this lane's node s * 64 + lane)
+  auto view_of = [&](int s) -> int32_t {
+    if constexpr (kCold) return h_view[s];
+    else return nd[s].view;
+  };
 
   // ---- broker (wave-uniform)
   int32_t pool = A.broker_mips[r];
@@ -206,24 +276,33 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
     int csl = 0;  // its slot
 #pragma unroll
     for (int s = 0; s < NPL; ++s) {
-      const V2Node& x = nd[s];
-      if (x.t_sched && earlier(x.t_tick, x.t_seq, ct, cs)) {
-        ct = x.t_tick;
-        cs = x.t_seq;
-        src = 1;
-        csl = s;
-      }
-      if (x.in_n && earlier(x.in_hd.tick, x.in_hd.seq, ct, cs)) {
-        ct = x.in_hd.tick;
-        cs = x.in_hd.seq;
-        src = 2;
-        csl = s;
-      }
-      if (x.out_n && earlier(x.out_hd.tick, x.out_hd.seq, ct, cs)) {
-        ct = x.out_hd.tick;
-        cs = x.out_hd.seq;
-        src = 3;
-        csl = s;
+      if constexpr (kCold) {
+        if (h_src[s] && earlier(h_tick[s], h_seq[s], ct, cs)) {
+          ct = h_tick[s];
+          cs = h_seq[s];
+          src = h_src[s];
+          csl = s;
+        }
+      } else {
+        const V2Node& x = nd[s];
+        if (x.t_sched && earlier(x.t_tick, x.t_seq, ct, cs)) {
+          ct = x.t_tick;
+          cs = x.t_seq;
+          src = 1;
+          csl = s;
+        }
+        if (x.in_n && earlier(x.in_hd.tick, x.in_hd.seq, ct, cs)) {
+          ct = x.in_hd.tick;
+          cs = x.in_hd.seq;
+          src = 2;
+          csl = s;
+        }
+        if (x.out_n && earlier(x.out_hd.tick, x.out_hd.seq, ct, cs)) {
+          ct = x.out_hd.tick;
+          cs = x.out_hd.seq;
+          src = 3;
+          csl = s;
+        }
       }
     }
     const int64_t m_tick =
@@ -299,37 +378,41 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
         }
       } else {
         // the LAST node whose advertised MIPS exceeds node 0's (:241-248), else node 0
-        const int32_t v0 = (int32_t)readlane_u32((uint32_t)nd[0].view, 0);
+        const int32_t v0 = (int32_t)readlane_u32((uint32_t)view_of(0), 0);
         uint32_t last = 0u;
 #pragma unroll
         for (int s = 0; s < NPL; ++s) {
           const int j = s * kWave + lane;
-          if (j < N && j >= 1 && nd[s].view > v0) last = (uint32_t)j;
+          if (j < N && j >= 1 && view_of(s) > v0) last = (uint32_t)j;
         }
         k = (int32_t)~wave_min_u32(~last);
         const int kl = k & (kWave - 1), ks = k / kWave;
         int32_t vk = 0;
 #pragma unroll
         for (int s = 0; s < NPL; ++s)
-          if (s == ks) vk = (int32_t)readlane_u32((uint32_t)nd[s].view, kl);
+          if (s == ks) vk = (int32_t)readlane_u32((uint32_t)view_of(s), kl);
         lmark = kListForwarded;  // :255-260, before the MIPS check
         if (req < vk) {          // :262-270: FognetMsgTask to node k
           status = FOGNET_V2_ST_FORWARDED;
           ++st.n_forwarded;
           if (lane == kl) {
-#pragma unroll
-            for (int s = 0; s < NPL; ++s) {
-              if (s == ks) {
-                V2Node& x = nd[s];
-                const V2Msg m = {now + x.dl, seq, req, t};
-                if (x.in_n == Q) {
-                  bad = true;
-                } else {
-                  P.inq[qrow(s) + ((x.in_h + x.in_n) & qm)] = m;
-                  if (x.in_n == 0u) x.in_hd = m;
-                  ++x.in_n;
-                }
+            auto push = [&](V2Node& x, int s) {
+              const V2Msg m = {now + x.dl, seq, req, t};
+              if (x.in_n == Q) {
+                bad = true;
+              } else {
+                P.inq[qrow(s) + ((x.in_h + x.in_n) & qm)] = m;
+                if (x.in_n == 0u) x.in_hd = m;
+                ++x.in_n;
               }
+            };
+            if constexpr (kCold) {
+              push(nd[ks], ks);
+              refresh(ks);
+            } else {
+#pragma unroll
+              for (int s = 0; s < NPL; ++s)
+                if (s == ks) push(nd[s], s);
             }
           }
           ++seq;
@@ -380,19 +463,23 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       if (wsrc == 3) {
         // a node -> broker message reaches the broker (BrokerBaseApp2.cc:128-154)
         int32_t mk = 0, mv = 0;
-#pragma unroll
-        for (int s = 0; s < NPL; ++s) {
-          if (s == ws) {
-            mk = (int32_t)readlane_u32((uint32_t)nd[s].out_hd.kind, w);
-            mv = (int32_t)readlane_u32((uint32_t)nd[s].out_hd.val, w);
-            if (lane == w) {
-              V2Node& x = nd[s];
-              ++x.out_h;
-              --x.out_n;
-              if (x.out_n) x.out_hd = P.outq[qrow(s) + (x.out_h & qm)];
-              if (mk == kMsgAdvert) x.view = mv;  // setMips (:132)
-            }
+        auto receive = [&](V2Node& x, int s) {
+          mk = (int32_t)readlane_u32((uint32_t)x.out_hd.kind, w);
+          mv = (int32_t)readlane_u32((uint32_t)x.out_hd.val, w);
+          if (lane == w) {
+            ++x.out_h;
+            --x.out_n;
+            if (x.out_n) x.out_hd = P.outq[qrow(s) + (x.out_h & qm)];
+            if (mk == kMsgAdvert) x.view = mv;  // setMips (:132)
           }
+        };
+        if constexpr (kCold) {
+          receive(nd[ws], ws);
+          if (lane == w) refresh(ws);
+        } else {
+#pragma unroll
+          for (int s = 0; s < NPL; ++s)
+            if (s == ws) receive(nd[s], s);
         }
         if (mk == kMsgAck6) {  // relay and erase the request if it is still listed (:145-153)
           bool relayed = false;
@@ -409,11 +496,7 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
         int32_t o_task = -1;   // task whose result changed
         uint32_t o_what = 0u;  // 1 released, 2 accepted, 3 rejected
         uint64_t my_seq = seq;
-        if (lane == w) {
-#pragma unroll
-          for (int s = 0; s < NPL; ++s) {
-            if (s != ws) continue;
-            V2Node& x = nd[s];
+        auto handle = [&](V2Node& x, int s) {
             V2Msg* const outq = P.outq + qrow(s);
             if (wsrc == 1) {
               x.t_sched = false;
@@ -480,6 +563,15 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
                 o_what = 3u;  // TaskAck(false) (:299-306)
               }
             }
+        };
+        if (lane == w) {
+          if constexpr (kCold) {
+            handle(nd[ws], ws);
+            refresh(ws);
+          } else {
+#pragma unroll
+            for (int s = 0; s < NPL; ++s)
+              if (s == ws) handle(nd[s], s);
           }
         }
         if (ballot(bad)) {

@@ -11,6 +11,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fognetsimpp_amd import _abi  # noqa: E402
+if os.environ.get("FOGNET_LIB"):  # a variant build (tools/build_variant.sh)
+    _abi.LIB_PATH = os.environ["FOGNET_LIB"]
 import fognetsimpp_amd as fa  # noqa: E402
 from fognetsimpp_amd import formats  # noqa: E402
 
