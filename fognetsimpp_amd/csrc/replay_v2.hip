@@ -1373,8 +1373,12 @@ hipError_t launch_replay_v2(const fognet_v2_in& in, const fognet_v2_out& out, vo
     hipLaunchKernelGGL(replay_v2_kernel<4>, dim3(in.R), dim3(kWave), 0, s, a);
   else if (in.N <= 512)
     hipLaunchKernelGGL(replay_v2_kernel<8>, dim3(in.R), dim3(kWave), 0, s, a);
-  else
+  else if (in.N <= 1024)
     hipLaunchKernelGGL(replay_v2_kernel<16>, dim3(in.R), dim3(kWave), 0, s, a);
+  else if (in.N <= 2048)
+    hipLaunchKernelGGL(replay_v2_kernel<32>, dim3(in.R), dim3(kWave), 0, s, a);
+  else
+    hipLaunchKernelGGL(replay_v2_kernel<64>, dim3(in.R), dim3(kWave), 0, s, a);
   return hipGetLastError();
 }
 

@@ -314,7 +314,7 @@ typedef struct fognet_user_stats {
  * requiredTime and runs a 10-ms advert/release timer (ComputeBrokerApp2.cc:
  * 202-318).  Deadlines are doubles compared with simTime().dbl() = ticks *
  * 1e-12, exactly as the reference does (their rounding decides releases). */
-#define FOGNET_V2_MAX_NODES 1024 /* node j on lane j % 64, slot j / 64 (up to 16 per lane) */
+#define FOGNET_V2_MAX_NODES 4096 /* node j on lane j % 64, slot j / 64 (up to 64 per lane) */
 
 typedef enum fognet_v2_task_status {
     FOGNET_V2_ST_LOCAL = 3,      /* reserved in the broker's own pool (pubAck 3)                   */
