@@ -1,6 +1,6 @@
 #!/bin/bash
-# One GPU call of round 5: steps named in STEPS (space-separated), each under its own time limit,
-# stopping at the first failure.  Outputs under gpurun_out/r5/.
+# One GPU call: steps named in STEPS (space-separated), each under its own time limit,
+# stopping at the first failure.  Outputs under gpurun_out/$ROUND (default r6).
 #   tests:<pytest -k expr>   GPU tests matching the expression
 #   suite                    the whole GPU suite
 #   bench:<name>:<args>      one bench.py line (args with '+' for spaces) -> <name>.json
@@ -9,7 +9,7 @@
 #                            KTKERNEL=<kernel>: also the kernel_profile sidecar bench.py quotes)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r5; mkdir -p $O
+O=gpurun_out/${ROUND:-r6}; mkdir -p $O
 export TMPDIR=/tmp
 for s in $STEPS; do
   echo "== $s $(date +%T)"
