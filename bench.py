@@ -40,6 +40,7 @@ kept (no trace and no per-task output in memory).
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -358,8 +359,10 @@ def main():
 def rocprof_kernel_avg(args, line):
     """The committed rocprofv3 average launch of the dominant kernel for this exact workload
     (profiles/kernel_profile_<workload>[_<policy>|_<recipe>].json, written by tools/kprof_sidecar.py from a
-    kernel trace of the bench command itself): quoted only when its config equals this line's and the
-    average does not exceed this run's ms_per_step."""
+    kernel trace of the bench command itself).  Quoted only when the profiled run loaded the very library
+    this run loaded (sha256 of the .so: a profile of another build is never quoted), its config
+    equals this line's, and the average does not exceed the profiled run's own ms_per_step; both runs'
+    ms_per_step are printed, so a box-to-box difference shows instead of rejecting the profile."""
     tag = args.workload + ("" if args.policy in (None, "EXT_HIER" if args.workload == "c5" else "REF_V3")
                            else f"_{args.policy}") + ("_saturate" if getattr(args, "c5_recipe", "light") == "saturate"
                                                      and args.workload == "c5" else "")
@@ -370,10 +373,16 @@ def rocprof_kernel_avg(args, line):
         side = json.load(open(path))
     except ValueError:
         return {"kernel_avg_ms_rocprof": None}
-    if side.get("config") != line["config"] or side["avg_ms"] > line["ms_per_step"]:
-        return {"kernel_avg_ms_rocprof": None, "rocprof_profile_rejected": os.path.relpath(path, ROOT)}
-    return {"kernel_avg_ms_rocprof": side["avg_ms"], "rocprof_profile": os.path.relpath(path, ROOT),
-            "rocprof_command": side["command"], "rocprof_tree": side.get("tree")}
+    rel = os.path.relpath(path, ROOT)
+    with open(_abi.LIB_PATH, "rb") as f:
+        lib_sha = hashlib.sha256(f.read()).hexdigest()
+    if side.get("lib_sha256") != lib_sha:
+        return {"kernel_avg_ms_rocprof": None, "rocprof_profile_other_build": rel}
+    if side.get("config") != line["config"] or side["avg_ms"] > side["ms_per_step"]:
+        return {"kernel_avg_ms_rocprof": None, "rocprof_profile_rejected": rel}
+    return {"kernel_avg_ms_rocprof": side["avg_ms"], "rocprof_profile": rel,
+            "rocprof_ms_per_step": side["ms_per_step"], "ms_per_step_this_run": line["ms_per_step"],
+            "rocprof_command": side["command"], "rocprof_lib_sha256": lib_sha[:16]}
 
 
 def bench_c4(args, ctx, dev, dist, world, rank):

@@ -4,12 +4,15 @@ The profile must come from the bench command itself (same workload, same sizes, 
 steps/warm-up): this tool takes the bench's own JSON line from that profiled run and the
 tools/kstats.py summary of its kernel trace (warm-up dispatches skipped), picks the dominant
 kernel, and refuses to write a sidecar whose average launch exceeds the run's ms_per_step
-(a profile of another tree or other sizes cannot be the one the line quotes).
+(a profile of another tree or other sizes cannot be the one the line quotes).  It records the
+sha256 of the library the profiled run loaded (--lib): bench.py quotes the sidecar only for a
+run of that same binary (a stale profile of an older, faster build is never quoted).
 
   python tools/kprof_sidecar.py <bench log or json> <kstats.csv> --kernel <name prefix> \
       --cmd "<the profiled command>" --out profiles/kernel_profile_<workload>.json"""
 import argparse
 import csv
+import hashlib
 import json
 import re
 import sys
@@ -23,6 +26,7 @@ def main():
     ap.add_argument("--cmd", required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--tree", default=None, help="the commit the profiled tree was built from")
+  ap.add_argument("--lib", default="fognetsimpp_amd/libfognet_hip.so", help="the library the profiled run loaded")
     a = ap.parse_args()
     line = [ln for ln in open(a.bench) if ln.startswith("{")][-1]
     b = json.loads(line)
@@ -38,7 +42,8 @@ def main():
             "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6,
             "skipped_warmup": int(r.get("SkippedWarmup") or 0), "steps": b["steps"], "warmup": b["warmup"],
             "ms_per_step": b["ms_per_step"], "kernel_avg_ms_hip_events": b["roofline"].get("kernel_avg_ms"),
-            "config": b["config"], "stats_csv": a.kstats, "tree": a.tree}
+            "config": b["config"], "stats_csv": a.kstats, "tree": a.tree,
+            "lib_sha256": hashlib.sha256(open(a.lib, "rb").read()).hexdigest()}
     json.dump(side, open(a.out, "w"), indent=1)
     print(json.dumps({k: side[k] for k in ("kernel", "calls", "avg_ms", "ms_per_step", "kernel_avg_ms_hip_events")}))
 
