@@ -30,10 +30,19 @@ struct fognet_ctx {
   size_t host_stage_bytes = 0;
   // EXT_HIER path choice (fognet_hier_path_stats): the hand-over count of the last region pass,
   // copied back into pinned memory on the launch stream and read once its event has passed
-  int32_t* hier_host = nullptr;  // [0] handed-over replications, [1] R of that launch
+  // One measurement at a time: the count is paired with the shape and stream of the
+  // launch it measured, and its decision applies only to later launches of that same shape and stream.
+  struct HierShape {
+    int32_t R, T, N;
+    void* stream;
+    bool operator==(const HierShape& o) const { return R == o.R && T == o.T && N == o.N && stream == o.stream; }
+  };
+  int32_t* hier_host = nullptr;  // [0] handed-over replications of the measured launch
   hipEvent_t hier_ev = nullptr;
   bool hier_pending = false;
-  bool hier_seq = false;  // the last measured region pass handed most replications over
+  HierShape hier_pend_shape{};  // the launch being measured
+  bool hier_seq = false;  // the last measured region pass (of hier_seq_shape) handed most replications over
+  HierShape hier_seq_shape{};
   int hier_seq_runs = 0;  // launches sent straight to the sequential replay since that measurement
   int64_t hier_region_launches = 0, hier_seq_launches = 0;
   std::string err;
@@ -455,13 +464,16 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     const int32_t B = (a.N + FOGNET_HIER_REGION_NODES - 1) / FOGNET_HIER_REGION_NODES;
     const bool hier_split = a.policy == FOGNET_POLICY_EXT_HIER && !a.down && !stats_only && a.T > 0 && B >= 2;
     bool regions = hier_split && use_regions();
+    const fognet_ctx::HierShape shape{a.R, a.T, a.N, stream};
     if (regions && regions_auto()) {
       // the last region pass's hand-over count, if it has reached the host (never waited for)
       if (c->hier_pending && hipEventQuery(c->hier_ev) == hipSuccess) {
         c->hier_pending = false;
-        c->hier_seq = 2 * (int64_t)c->hier_host[0] > (int64_t)c->hier_host[1];
+        c->hier_seq = 2 * (int64_t)c->hier_host[0] > (int64_t)c->hier_pend_shape.R;
+        c->hier_seq_shape = c->hier_pend_shape;
         c->hier_seq_runs = 0;
       }
+      if (c->hier_seq && !(c->hier_seq_shape == shape)) c->hier_seq = false;  // another job: measure it
       if (c->hier_seq && c->hier_seq_runs < kHierReprobe) {
         regions = false;  // most replications escalated: the region pass would only be replayed again
         ++c->hier_seq_runs;
@@ -532,12 +544,14 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       if (regions_only()) return FOGNET_OK;
       e = fognet::launch_replay_wide(a, base + o_e, slots, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(c, e, "wide hand-over launch");
-      if (regions_auto()) {  // the hand-over count back to the host, asynchronously
-        if (!c->hier_host && hipHostMalloc((void**)&c->hier_host, 2 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
+      if (regions_auto() && !c->hier_pending) {  // the hand-over count back to the host, asynchronously
+        // (while a measurement is in flight, later launches are not measured: its pinned slot and event
+        // stay paired with the launch that issued them)
+        if (!c->hier_host && hipHostMalloc((void**)&c->hier_host, sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
           c->hier_host = nullptr;
         if (!c->hier_ev && hipEventCreateWithFlags(&c->hier_ev, hipEventDisableTiming) != hipSuccess) c->hier_ev = nullptr;
         if (c->hier_host && c->hier_ev) {
-          c->hier_host[1] = a.R;
+          c->hier_pend_shape = shape;
           e = hipMemcpyAsync(c->hier_host, a.wide_count, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream);
           if (e == hipSuccess) e = hipEventRecord(c->hier_ev, (hipStream_t)stream);
           if (e != hipSuccess) return hip_fail(c, e, "hand-over count copy");

@@ -97,11 +97,14 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
   }
   if (bad) s_bad = 1;
   __syncthreads();
+  int32_t* const seg = W.seg + (size_t)r * (size_t)(B + 1);
   if (s_bad) {
     if (tid == 0) __hip_atomic_store(W.quit + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the dispatch inputs stay defined: empty segments, dispatched last
+    if (tid <= B) seg[tid] = 0;
+    if (tid < B) W.okey[(size_t)r * B + tid] = 255u;
     return;
   }
-  int32_t* const seg = W.seg + (size_t)r * (size_t)(B + 1);
   if (tid == 0) {
     uint32_t acc = 0u;
     for (int b = 0; b < B; ++b) {

@@ -1127,6 +1127,47 @@ def test_v2_random_matches_oracle(ctx, seed, N, R):
     assert_v2_parity(g, o)
 
 
+def test_v2_widest_node_set_reserves_on_high_slots(ctx):
+    """N = 4096 (replay_v2_kernel<64>: 64 nodes per lane, per-node records in scratch) with R = 4 and
+    traces long enough for reservations, rejections and releases on the high slots: node 0 advertises
+    the smallest MIPS, so BrokerBaseApp2's "last node whose MIPS exceeds node 0's" (BrokerBaseApp2.cc:
+    241-248) lands at j >= 2048.  Equal to the oracle DES."""
+    R, N, T = 4, 4096, 400
+    tr, broker, stop, rt = v2_random(61, R, N, T)
+    tr["mips"][:, 0] = 500
+    tr["mips"][:, -64:] = 1500  # the last few nodes beat node 0 in every replication
+    tr["req"] = (tr["req"] % 400).astype(np.int32)  # small requirements: several reservations per node at once
+    rt = np.array([0.01, 0.02, 0.05, 0.05])
+    g = run_v2_gpu(ctx, tr, broker, stop, rt, qcap=256)
+    o = ol.run_v2(tr["arrive"], tr["req"], broker, tr["mips"], tr["dl"], tr["ul"], tr["first_adv"], stop, rt,
+                  threads=4)
+    assert (o["stats"]["status"] == 0).all()
+    assert_v2_parity(g, o)
+    fwd = g["node"][np.isin(g["status"], [_abi.V2_ST_ACCEPTED, _abi.V2_ST_REJECTED])]
+    assert fwd.size > 0 and fwd.min() >= 2048
+    assert (g["stats"]["n_accepted"] > 0).all() and (g["stats"]["n_released_node"] > 0).all()
+
+
+def test_v2_widest_node_set_capacity_refused(ctx):
+    """N = 4096 with a reservation list of capacity 16 and long requiredTimes: the replications whose
+    node holds more than 16 reservations at once are refused (FOGNET_ERR_CAPACITY, the queues never
+    wrap); a replication that stays within the capacity is still equal to the oracle DES."""
+    R, N, T = 3, 4096, 300
+    tr, broker, stop, rt = v2_random(62, R, N, T)
+    tr["mips"][:, 0] = 500
+    tr["mips"][:, -64:] = 1500
+    tr["req"] = (tr["req"] % 20 + 1).astype(np.int32)
+    rt = np.array([0.5, 0.5, 0.001])  # replication 2: each reservation released before the next arrives
+    broker = np.zeros(R, np.int32)  # no broker pool: every publish is forwarded
+    g = run_v2_gpu(ctx, tr, broker, stop, rt, qcap=16)
+    st = g["stats"]["status"]
+    assert (st[:2] == _abi.FOGNET_ERR_CAPACITY).all()
+    o = ol.run_v2(tr["arrive"][2:], tr["req"][2:], broker[2:], tr["mips"][2:], tr["dl"][2:], tr["ul"][2:],
+                  tr["first_adv"][2:], stop[2:], rt[2:], threads=1)
+    assert st[2] == 0 and (o["stats"]["status"] == 0).all()
+    assert_v2_parity({k: v[2:] for k, v in g.items()}, o)
+
+
 @pytest.mark.parametrize("env", [("FOGNET_V2_ROW", "32"), ("FOGNET_V2_ACTIVE", "4")])
 @pytest.mark.parametrize("N", [5, 16])
 def test_v2_two_rows_per_wave_at_small_n(ctx, monkeypatch, N, env):
@@ -1622,6 +1663,11 @@ def test_c5_ext_hier_automatic_path(monkeypatch, c5_saturated):
     mg, sc = fa.c5_params(np.arange(R), N)
     light = fa.generate_trace(c, 0x5EED0005, R, T, N, mg, sc)
     light["region"] = fa.mobility_regions(light["arrive"], N)
+    # another job (shape) on the same context is measured afresh, not sent to the sequential replay on the
+    # strength of the saturated job's count (the decision is paired with the launch it measured)
+    fa.run_batch(c, light, policy="EXT_HIER", hier_threshold_s=60, hier_up_tick=20 * 10**9)
+    torch.cuda.synchronize()
+    assert c.hier_path_stats() == (2, 1)
     c2 = fa.Context(0)
     for _ in range(2):
         fa.run_batch(c2, light, policy="EXT_HIER", hier_threshold_s=60, hier_up_tick=20 * 10**9)
