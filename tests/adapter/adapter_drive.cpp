@@ -20,7 +20,7 @@ static int g_last_port = -1;
 static int g_sent = 0;
 SimTime simTime() {
     SimTime t;
-    t.raw = g_now;
+    t.raw_ = g_now;
     return t;
 }
 void UDPSocket::sendTo(cPacket *msg, L3Address, int destPort) {

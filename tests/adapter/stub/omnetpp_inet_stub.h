@@ -18,8 +18,9 @@ namespace inet {
 typedef int64_t int64;
 
 struct SimTime {
-    int64 raw = 0;  // 1e-12 s
-    double dbl() const { return (double)raw * 1e-12; }
+    int64 raw_ = 0;  // 1e-12 s
+    double dbl() const { return (double)raw_ * 1e-12; }
+    int64 raw() const { return raw_; }
 };
 SimTime simTime();  // the driver's clock
 
@@ -38,12 +39,27 @@ class cRuntimeError : public std::runtime_error {
     }
 };
 
-class cMessage {
+class cObject {
+  public:
+    virtual ~cObject() {}
+};
+
+class cMessage : public cObject {
     std::string name;
+    SimTime created = simTime();
+    cObject *ctrl = nullptr;
+    short kind = 0;
   public:
     explicit cMessage(const char *n = nullptr) : name(n ? n : "") {}
-    virtual ~cMessage() {}
+    virtual ~cMessage() { delete ctrl; }
     const char *getName() const { return name.c_str(); }
+    SimTime getCreationTime() const { return created; }
+    cObject *getControlInfo() const { return ctrl; }
+    void setControlInfo(cObject *c) { ctrl = c; }
+    bool isSelfMessage() const { return false; }
+    short getKind() const { return kind; }
+    void setKind(short k) { kind = k; }
+    void stubSetCreationTime(int64 t) { created.raw_ = t; }  // stub only: the driver's sender clock
 };
 
 class cPacket : public cMessage {
@@ -62,6 +78,15 @@ class L3Address {
     uint32_t raw() const { return a; }
 };
 
+// INET 3.3 UDPDataIndication (the control info of a received datagram)
+class UDPDataIndication : public cObject {
+    L3Address src;
+  public:
+    explicit UDPDataIndication(L3Address a) : src(a) {}
+    L3Address getSrcAddr() const { return src; }
+};
+inline bool operator==(const L3Address &a, const L3Address &b) { return a.raw() == b.raw(); }
+
 class UDPSocket {
   public:
     void sendTo(cPacket *msg, L3Address destAddr, int destPort);  // the driver's network
@@ -69,23 +94,28 @@ class UDPSocket {
 
 class cPar {
     long v = 0;
+    std::string str;
   public:
     explicit cPar(long x = 0) : v(x) {}
     operator int() const { return (int)v; }
     operator long() const { return v; }
+    const char *stringValue() const { return str.c_str(); }
+    void stubSet(const std::string &x) { str = x; }
 };
 
 enum { INITSTAGE_LOCAL = 0, NUM_INIT_STAGES = 12 };
 
 class ApplicationBase {
   protected:
-    cPar parHipDevice;
+    cPar parHipDevice, parTraceFile;
     virtual void initialize(int stage) {}
     virtual void handleMessageWhenUp(cMessage *msg) = 0;
+    virtual void finish() {}
   public:
     virtual ~ApplicationBase() {}
-    cPar &par(const char *) { return parHipDevice; }
+    cPar &par(const char *name) { return std::string(name) == "traceFile" ? parTraceFile : parHipDevice; }
     int getId() const { return 7; }
+    std::string getFullPath() const { return "FogNet.broker.udpApp[0]"; }
 };
 
 // generated message classes (opp_string fields: const char * getters/setters)
@@ -105,6 +135,19 @@ class MqttMsgPublish : public cPacket {
     void setMIPSRequired(int m) { MIPSRequired = m; }
     double getRequiredTime() const { return requiredTime; }
     void setRequiredTime(double t) { requiredTime = t; }
+};
+
+// src/mqttapp/mqttMessages/MqttMsgPuback.msg: the acks a node sends (status 4 queued, 5 assigned,
+// 6 performed) and the broker relays (BrokerBaseApp3.cc:164-198)
+class MqttMsgPuback : public cPacket {
+    std::string messageID;
+    int status = 0;
+  public:
+    explicit MqttMsgPuback(const char *n = nullptr) : cPacket(n) {}
+    const char *getMessageID() const { return messageID.c_str(); }
+    void setMessageID(const char *s) { messageID = s; }
+    int getStatus() const { return status; }
+    void setStatus(int x) { status = x; }
 };
 
 class FognetMsgAdvertiseMIPS : public cPacket {

@@ -1,10 +1,13 @@
-"""The OMNeT++ adapters (integration/BrokerBaseAppHip.{h,cc,ned} for the v3
+"""The OMNeT++ modules (integration/BrokerBaseAppHip.{h,cc,ned} for the v3
 broker, integration/BrokerBaseApp2Hip.{h,cc,ned} for the v2 broker C1's ini
-selects) are real code: they type-check against a minimal
-stub of the OMNeT++ / INET identifiers they touch (tests/adapter/stub: the
-reference's member names, types and access, BrokerBaseApp3.h:24-64,
-BrokerBaseApp2.h:27-60), and on a GPU a driver feeds each adverts and
-publishes and checks every offloaded task against the oracle."""
+selects; integration/BrokerBaseAppRec.{h,cc,ned}, the trace
+exporter, §2) are real code: they type-check against a minimal stub of the
+OMNeT++ / INET identifiers they touch (tests/adapter/stub: the reference's
+member names, types and access, BrokerBaseApp3.h:24-64, BrokerBaseApp2.h:27-60),
+and drivers feed each the broker's message stream: the adapters' offloaded
+tasks are checked against the oracle on a GPU, the exporter's trace against the
+ground truth it was recorded from and its replay (oracle, and the device on a
+GPU) against the ground truth's decisions."""
 import os
 import subprocess
 
@@ -15,7 +18,8 @@ INC = ["-I", os.path.join(ROOT, "tests", "adapter", "stub"), "-I", os.path.join(
        "-I", os.path.join(ROOT, "integration")]
 
 
-ADAPTERS = {"v3": ("BrokerBaseAppHip.cc", "adapter_drive"), "v2": ("BrokerBaseApp2Hip.cc", "adapter2_drive")}
+ADAPTERS = {"v3": ("BrokerBaseAppHip.cc", "adapter_drive"), "v2": ("BrokerBaseApp2Hip.cc", "adapter2_drive"),
+            "rec": ("BrokerBaseAppRec.cc", "recorder_drive")}
 
 
 @pytest.mark.parametrize("which", sorted(ADAPTERS))
@@ -62,4 +66,26 @@ def test_v2_adapter_forwards_like_the_reference_on_gpu(tmp_path):
     p = subprocess.run([build_driver(tmp_path, "v2")], capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "adapter2: all checks passed" in p.stdout
+    print(p.stdout)
+
+
+def test_recorder_trace_equals_what_the_broker_saw(tmp_path):
+    """BrokerBaseAppRec records the QoS-1 publishes (QoS-0 ones left out) and the node table (CONNECT
+    order, first-advert MIPS and tick, ul from the advert's creation, dl from the first status-4/5 ack)
+    and writes them at finish(); the trace read back equals the ground truth it was recorded from, and
+    the oracle's replay of it reproduces the ground truth's decisions, ticks and statistics (CPU)."""
+    p = subprocess.run([build_driver(tmp_path, "rec"), str(tmp_path / "rec.fogntrc"), "--no-gpu"],
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "recorder: all checks passed" in p.stdout
+
+
+@pytest.mark.gpu
+def test_recorder_trace_replays_on_gpu(tmp_path):
+    """The exporter's trace through fognet_run_batch on the device: every decision, status, start and
+    completion tick and the statistics record equal the ground truth (identical inputs on both paths)."""
+    p = subprocess.run([build_driver(tmp_path, "rec"), str(tmp_path / "rec.fogntrc")], capture_output=True,
+                       text=True, timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "recorder: all checks passed" in p.stdout
     print(p.stdout)
