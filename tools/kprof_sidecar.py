@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--cmd", required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--tree", default=None, help="the commit the profiled tree was built from")
-  ap.add_argument("--lib", default="fognetsimpp_amd/libfognet_hip.so", help="the library the profiled run loaded")
+    ap.add_argument("--lib", default="fognetsimpp_amd/libfognet_hip.so", help="the library the profiled run loaded")
     a = ap.parse_args()
     line = [ln for ln in open(a.bench) if ln.startswith("{")][-1]
     b = json.loads(line)
