@@ -12,7 +12,7 @@
  * tests and no result files for the v3 modules.  This restatement is therefore
  * pinned only by hand-traced known-answer vectors derived from the reference
  * source (tests/golden/kat_*.json) — formally "parity unpinned" against an
- * executable reference.  See DESIGN.md §Oracle.
+ * executable reference.  See DESIGN.md §2.
  */
 #ifndef FOGNET_ORACLE_H
 #define FOGNET_ORACLE_H

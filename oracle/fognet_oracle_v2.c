@@ -18,7 +18,7 @@
  * Deadlines are doubles as in the reference: Request.requiredTime =
  * simTime().dbl() + requiredTime, compared with simTime().dbl(); OMNeT++ 4.6
  * computes dbl() as t * 1e-12 (int64 ticks times the double scale).  That
- * rounding decides some releases (DESIGN.md §10).
+ * rounding decides some releases (DESIGN.md §9).
  */
 #include <pthread.h>
 #include <stdlib.h>

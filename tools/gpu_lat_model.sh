@@ -1,5 +1,5 @@
 #!/bin/bash
-# Inputs of the C3 latency-floor model (DESIGN.md §4.6): the one-wave instruction-class latencies
+# Inputs of the C3 latency-floor model (DESIGN.md §4.3): the one-wave instruction-class latencies
 # (build/live/lat_probe, tools/lat_probe.hip) and the replay-only instruction mix at one wave per SIMD
 # (R = 1024, FOGNET_STAGES=replay: no statistics pass) from two rocprofv3 PMC passes.
 set -o pipefail

@@ -1,6 +1,6 @@
 // lat_probe.hip -- per-instruction-class latencies of ONE wave alone on a SIMD
-// (gfx950), the inputs of the C3 latency-floor model (DESIGN.md §4.6).
-// Diagnostics only: built by tools/build_lat_probe.sh into build/live/, never
+// (gfx950), the inputs of the C3 latency-floor model (DESIGN.md §4.3).
+// Diagnostics only: built by `hipcc --offload-arch=gfx950 -O2 -o build/live/lat_probe tools/lat_probe.hip`, never
 // linked into the library.  Each probe runs a chain of dependent instructions
 // (inline asm, so the compiler adds nothing between them), timed with
 // s_memtime (shader clock), and prints cycles per link.
