@@ -924,6 +924,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           max_pend = max(max_pend, tot);
           n_done += 1;
           jp += 1;
+          WTM(3)  // (profile builds: the escalation's pending bookkeeping counts as "record")
           continue;
         }
         // a direct task: the pending escalated tasks that reach k no later than it go first
