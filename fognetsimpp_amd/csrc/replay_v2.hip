@@ -70,6 +70,12 @@ constexpr bool kPhantomAdverts = true;
 // two sequence numbers its rank among them gives.  At C1 most events are such
 // firings (five nodes, a 10-ms timer, a publish every 50 ms).
 constexpr bool kBatchFirings = true;
+// The same batches in replay_v2_kernel<NPL> (N > 32), the firings ranked by a bitonic
+// sort in LDS (FOGNET_V2_NPL_BATCH=0: one event per step, for A/B timing)
+#ifndef FOGNET_V2_NPL_BATCH
+#define FOGNET_V2_NPL_BATCH 1
+#endif
+constexpr bool kBatchNpl = FOGNET_V2_NPL_BATCH != 0;
 constexpr int32_t kNoAdvert = INT32_MIN;  // no advert sent yet (the broker's view starts at MIPS 0)
 
 struct V2Msg {  // a message in flight: arrival tick, insertion sequence, payload
@@ -250,6 +256,37 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
     if constexpr (kCold) return h_view[s];
     else return nd[s].view;
   };
+  // f(node, slot) over this lane's slots (all, or those of the bit mask m): a
+  // counted loop over the scratch records (kCold; one copy of f), else unrolled
+  // over the register-resident ones
+  auto for_slots = [&](auto&& f) {
+    if constexpr (kCold) {
+#pragma unroll 1
+      for (int s = 0; s < NPL; ++s) f(nd[s], s);
+    } else {
+#pragma unroll
+      for (int s = 0; s < NPL; ++s) f(nd[s], s);
+    }
+  };
+  auto for_slots_in = [&](uint64_t m, auto&& f) {
+    if constexpr (kCold) {
+      for (; m; m &= m - 1ull) {
+        const int s = (int)__builtin_ctzll(m);
+        f(nd[s], s);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < NPL; ++s)
+        if ((m >> s) & 1ull) f(nd[s], s);
+    }
+  };
+  // batch ranks (kBatchFirings): the batch's firings as (tick, seq << 13 | releases << 12 |
+  // node) sorted in LDS; then each firing's sequence-number offset, by node (aliasing the
+  // ticks, dead once sorted)
+  __shared__ int64_t s_bt[NPL * kWave];
+  __shared__ uint64_t s_bk[NPL * kWave];
+  uint32_t* const s_off = reinterpret_cast<uint32_t*>(s_bt);
+  static_assert(NPL * kWave <= (1 << 12), "node index in 12 bits of the batch key");
 
   // ---- broker (wave-uniform)
   int32_t pool = A.broker_mips[r];
@@ -334,6 +371,186 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       kind = 3;
     }
     if (kind == 0 || e_tick >= stop) break;  // nothing left, or the sim-time-limit
+
+    // ---- a batch (kBatchFirings, the rows kernel's rule over NPL nodes per lane).  When
+    // the earliest event is a node's timer firing or a message reaching the broker, every
+    // node's next firing and every node -> broker message before H -- the earliest task
+    // arrival, publish or broker RELEASERESOURCE: the events that draw sequence numbers
+    // and touch a node or the request list -- are handled in this one step.  A firing
+    // touches only its node and draws two sequence numbers (three when it releases a
+    // reservation: its status-6 ack's first), a message draws none and touches only the
+    // broker's view or, for an ack, its request's list entry, so they commute; each
+    // firing takes the numbers its (tick, sequence) rank among the batch's firings gives
+    // (a bitonic sort of the batch in LDS), and each node's messages are popped in its
+    // FIFO's order (its own firing's advert included when it lands before H).
+    if (kBatchNpl && kind == 1 && (int)readlane_u32((uint32_t)src, w) != 2) {
+      int64_t ht = kNever;
+      uint64_t hs = ~0ull;
+      for_slots([&](V2Node& x, int) {
+        if (x.in_n && earlier(x.in_hd.tick, x.in_hd.seq, ht, hs)) {
+          ht = x.in_hd.tick;
+          hs = x.in_hd.seq;
+        }
+      });
+      int64_t H_t = (int64_t)wave_min_u64((uint64_t)ht);
+      uint64_t H_s = wave_min_u64(ht == H_t ? hs : ~0ull);
+      if (next < T && earlier(p_tick, (uint64_t)N + (uint64_t)next, H_t, H_s)) {
+        H_t = p_tick;
+        H_s = (uint64_t)N + (uint64_t)next;
+      }
+      if (b_sched && earlier(b_tick, b_seq, H_t, H_s)) {
+        H_t = b_tick;
+        H_s = b_seq;
+      }
+      // the batch's firings (bit s: slot s), and those that release a reservation
+      // (ComputeBrokerApp2.cc:222-226: the oldest, when its deadline < now)
+      uint64_t cm = 0ull, rm = 0ull;
+      for_slots([&](V2Node& x, int s) {
+        if (x.t_sched && x.t_tick < stop && earlier(x.t_tick, x.t_seq, H_t, H_s)) {
+          cm |= 1ull << s;
+          if (x.t_kind == kKindRelease && x.rs_n) {
+            const V2Res h = P.res[qrow(s) + (x.rs_h & qm)];
+            if (h.deadline < dbl(x.t_tick)) rm |= 1ull << s;
+          }
+        }
+      });
+      const uint32_t c = (uint32_t)__popcll(cm);
+      const uint32_t c_incl = wave_scan_add_u32(c);
+      const uint32_t n = readlane_u32(c_incl, kWave - 1);
+      if (seq >= (1ull << 50)) {  // (the sort key keeps the sequence in 51 bits)
+        err = FOGNET_ERR_CAPACITY;
+        break;
+      }
+      uint32_t p = c_incl - c;
+      for_slots_in(cm, [&](V2Node& x, int s) {
+        s_bt[p] = x.t_tick;
+        s_bk[p] = (x.t_seq << 13) | (((rm >> s) & 1ull) << 12) | (uint64_t)(s * kWave + lane);
+        ++p;
+      });
+      uint32_t n2 = 1u;
+      while (n2 < n) n2 <<= 1;
+      for (uint32_t i = n + (uint32_t)lane; i < n2; i += kWave) {
+        s_bt[i] = INT64_MAX;
+        s_bk[i] = ~0ull;
+      }
+      __syncthreads();
+      for (uint32_t k = 2u; k <= n2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0u; j >>= 1) {
+          for (uint32_t i = (uint32_t)lane; i < n2; i += kWave) {
+            const uint32_t q = i ^ j;
+            if (q > i) {
+              const int64_t ti = s_bt[i], tq = s_bt[q];
+              const uint64_t ki = s_bk[i], kq = s_bk[q];
+              const bool gt = ti > tq || (ti == tq && ki > kq);
+              if (gt == ((i & k) == 0u)) {
+                s_bt[i] = tq;
+                s_bt[q] = ti;
+                s_bk[i] = kq;
+                s_bk[q] = ki;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      // sorted position i draws from seq + 2 i + (releasing firings before it)
+      uint32_t n_relb = 0u;
+      for (uint32_t b0 = 0u; b0 < n; b0 += kWave) {
+        const uint32_t i = b0 + (uint32_t)lane;
+        const uint64_t kx = i < n ? s_bk[i] : 0ull;
+        const uint32_t rl = i < n ? (uint32_t)(kx >> 12) & 1u : 0u;
+        const uint32_t incl = wave_scan_add_u32(rl);
+        if (i < n) s_off[kx & 0xFFFu] = 2u * i + n_relb + incl - rl;
+        n_relb += readlane_u32(incl, kWave - 1);
+      }
+      __syncthreads();
+      const uint32_t tot = 2u * n + n_relb;
+      uint32_t n_rel = 0u;
+      bool has_last = false;
+      int64_t lt_t = 0;
+      uint64_t lt_s = 0ull;
+      for_slots_in(cm, [&](V2Node& x, int s) {
+        const uint32_t off = s_off[s * kWave + lane];
+        const bool rel = (rm >> s) & 1ull;
+        uint64_t sq = seq + off;
+        const int64_t ft = x.t_tick;
+        const uint64_t fs = x.t_seq;
+        V2Msg* const outq = P.outq + qrow(s);
+        auto push_out = [&](const V2Msg& m) {
+          if (x.out_n == Q) {
+            bad = true;
+          } else {
+            outq[(x.out_h + x.out_n) & qm] = m;
+            if (x.out_n == 0u) x.out_hd = m;
+            ++x.out_n;
+          }
+        };
+        if (rel) {  // releaseResource: the oldest reservation, acked with status 6 (:225-235)
+          const V2Res h = P.res[qrow(s) + (x.rs_h & qm)];
+          x.mips += h.req;  // :226
+          ++x.rs_h;
+          --x.rs_n;
+          O.done_tick[tbase + h.task] = ft;
+          ++n_rel;
+          push_out(V2Msg{ft + x.ul, sq++, kMsgAck6, h.task});
+        }
+        // advertiseMIPS (:202-220): advert, then the self-message again 0.01 s later
+        if (kPhantomAdverts && x.mips == x.last_sent && earlier(x.ph_tick, x.ph_seq, ft, fs)) {
+          x.ph_tick = ft + x.ul;
+          x.ph_seq = sq++;
+          x.ph_cnt += x.ph_tick < stop ? 1u : 0u;
+        } else {
+          push_out(V2Msg{ft + x.ul, sq++, kMsgAdvert, x.mips});
+          x.last_sent = x.mips;
+        }
+        x.t_sched = true;
+        x.t_tick = ft + kAdvertPeriod;
+        x.t_seq = sq++;
+        if (off + (rel ? 3u : 2u) == tot) {  // the batch's last firing
+          has_last = true;
+          lt_t = ft;
+          lt_s = fs;
+        }
+      });
+      // node -> broker messages before H (BrokerBaseApp2.cc:128-154), per node in FIFO order
+      uint32_t n_arr = 0u, n_rl = 0u;
+      for_slots([&](V2Node& x, int s) {
+        while (x.out_n && x.out_hd.tick < stop && earlier(x.out_hd.tick, x.out_hd.seq, H_t, H_s)) {
+          if (x.out_hd.kind == kMsgAdvert) {
+            x.view = x.out_hd.val;  // setMips (:132)
+          } else if (list[x.out_hd.val] == kListForwarded) {  // ack 6: relay, erase if still listed
+            list[x.out_hd.val] = kListNone;
+            ++n_rl;
+          }
+          ++x.out_h;
+          --x.out_n;
+          if (x.out_n) x.out_hd = P.outq[qrow(s) + (x.out_h & qm)];
+          ++n_arr;
+        }
+      });
+      if constexpr (kCold) {
+#pragma unroll
+        for (int s = 0; s < NPL; ++s) {
+          key_of(nd[s], h_tick[s], h_seq[s], h_src[s]);
+          h_view[s] = nd[s].view;
+        }
+      }
+      st.events += (int64_t)n + (int64_t)wave_sum_u32(n_arr);
+      st.n_released_node += (int64_t)wave_sum_u32(n_rel);
+      st.n_relayed += (int64_t)wave_sum_u32(n_rl);
+      seq += tot;
+      if (n) {  // where an error ends the replication: the batch's last firing
+        const int wl = (int)__builtin_ctzll(ballot(has_last));
+        end_tick = readlane_i64(lt_t, wl);
+        end_seq = (uint64_t)readlane_i64((int64_t)lt_s, wl);
+      }
+      if (ballot(bad)) {
+        err = FOGNET_ERR_CAPACITY;
+        break;
+      }
+      continue;
+    }
+
     const int64_t now = e_tick;
     ++st.events;
     end_tick = e_tick;
