@@ -70,6 +70,13 @@ constexpr bool kPhantomAdverts = true;
 // two sequence numbers its rank among them gives.  At C1 most events are such
 // firings (five nodes, a 10-ms timer, a publish every 50 ms).
 constexpr bool kBatchFirings = true;
+// Periods per node in one rows-kernel batch (at most 3 * kBatchGens * 16 sequence
+// numbers per 16-lane row and batch)
+#ifndef FOGNET_V2_BATCH_GENS
+#define FOGNET_V2_BATCH_GENS 5
+#endif
+constexpr int kBatchGens = FOGNET_V2_BATCH_GENS;
+static_assert(kBatchGens >= 1 && kBatchGens <= 24, "release mask and the row broadcast's packing");
 // The same batches in replay_v2_kernel<NPL> (N > 32), the firings ranked by a bitonic
 // sort in LDS (FOGNET_V2_NPL_BATCH=0: one event per step, for A/B timing)
 #ifndef FOGNET_V2_NPL_BATCH
@@ -1077,17 +1084,13 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
       }
       VTM(0)
       const bool cand = t_sched && t_tick < stop && earlier32(t_tick, t_seq, H_t, H_s);
-      // (a firing that releases a reservation, ComputeBrokerApp2.cc:222-245, also
-      // touches only its node: one more sequence number, its status-6 ack's)
-      const bool rel = cand && t_kind == kKindRelease && rs_n && rs_hd.deadline < dbl(t_tick);
-      const bool inb = cand;
       // messages reaching the broker before H: adverts set the view, status-6 acks
       // relay and erase their request (BrokerBaseApp2.cc:128-154); they draw no
       // number and touch neither a node nor what a firing reads
       const bool arr = out_n && out_hd.tick < stop && earlier32(out_hd.tick, out_hd.seq, H_t, H_s);
       VTM(1)
       const uint32_t rowm = (uint32_t)((1ull << kRowLanes) - 1ull);
-      const uint32_t rowb = (uint32_t)(ballot(inb) >> (lane & ~(kRowLanes - 1))) & rowm;
+      const uint32_t rowb = (uint32_t)(ballot(cand) >> (lane & ~(kRowLanes - 1))) & rowm;
       const bool rowa = ((ballot(arr) >> (lane & ~(kRowLanes - 1))) & rowm) != 0ull;
       if (rowb && seq >= kSeqLimit) {
         err = FOGNET_ERR_CAPACITY;  // (32-bit insertion sequence)
@@ -1095,77 +1098,151 @@ __global__ __launch_bounds__(64) void replay_v2_rows_kernel(V2Args P) {
         batched = true;
       } else if (rowb || rowa) {
         batched = true;
-        // the firings' order (tick, then insertion sequence): each draws two
-        // sequence numbers (its advert's, its next firing's), three when it releases
-        // (its ack's first); `off` counts those the firings before it draw
-        uint32_t off = 0u, tot = 0u;
-        const uint32_t hi_rel = (uint32_t)((uint64_t)t_tick >> 32) | (rel ? 0x80000000u : 0u);  // (ticks < 2^53)
-        for (uint32_t m = rowb; m; m &= m - 1u) {
+        // Several periods per node (kBatchGens).  No task reaches a node before H, so
+        // node j's firings in the batch are t_j + g P (g < G_j; every firing re-arms
+        // 0.01 s later, ComputeBrokerApp2.cc:219), cut at H and, so that the batch is a
+        // prefix of the FES order, at the row's first firing + kBatchGens periods.
+        int64_t Hc_t = H_t;
+        uint32_t Hc_s = H_s;
+        if (rowb) {
+          const int64_t cap =
+              (int64_t)row_min_u64<kRowLanes>((uint64_t)(cand ? t_tick : kNever)) + kBatchGens * kAdvertPeriod;
+          if (cap < Hc_t) {
+            Hc_t = cap;
+            Hc_s = 0u;  // (nothing at the cut's tick)
+          }
+        }
+        // a later period's sequence number is drawn in the batch, after every pending
+        // one, so at the cut's own tick only a first firing can precede it
+        uint32_t G = 0u;
+        if (cand) {
+          int64_t tg = t_tick;
+          while (G < (uint32_t)kBatchGens && tg < stop && (tg < Hc_t || (G == 0u && tg == Hc_t && t_seq < Hc_s))) {
+            ++G;
+            tg += kAdvertPeriod;
+          }
+        }
+        // the periods that release a reservation (:222-226: the oldest, when its
+        // deadline < now), peeked from the FIFO before any is popped
+        uint32_t rmask = 0u;
+        if (G && t_kind == kKindRelease && rs_n) {
+          uint32_t k = 0u;
+          V2Res h = rs_hd;
+          for (uint32_t g = 0u; g < G && k < rs_n; ++g) {
+            if (h.deadline < dbl(t_tick + (int64_t)g * kAdvertPeriod)) {
+              rmask |= 1u << g;
+              ++k;
+              if (k < rs_n) {
+                if (k == 1u) {
+                  h = rs_nx;
+                } else {
+                  h = res[(rs_h + k) & qm];
+                  sync_vm();
+                }
+              }
+            }
+          }
+        }
+        // The firings' order is (tick, period, first firing's sequence): at one tick a
+        // first firing (pending sequence) precedes every later period (drawn in the
+        // batch), and later periods of two nodes keep the order of their firings one
+        // period before, down to the period where one of them is a first firing.  Each
+        // firing draws two sequence numbers (its advert's, its next firing's), three
+        // when it releases (its ack's first); off[g] counts those the firings before
+        // period g of this node draw: node i's firings before it are its periods
+        // g' < g + ceil((t_j - t_i) / P) (+1 for a same-tick one that precedes).
+        uint32_t off[kBatchGens];
+#pragma unroll
+        for (int g = 0; g < kBatchGens; ++g) off[g] = 0u;
+        uint32_t tot = 0u;
+        const uint32_t grow = (uint32_t)(ballot(G != 0u) >> (lane & ~(kRowLanes - 1))) & rowm;
+        const uint32_t gr = G | (rmask << 8);
+        for (uint32_t m = grow; m; m &= m - 1u) {
           const int w = (int)__builtin_ctz(m);
-          const uint32_t hw = row_bcast_u32<kRowLanes>(hi_rel, w);
-          const int64_t tw = (int64_t)(((uint64_t)(hw & 0x7FFFFFFFu) << 32) |
-                                       row_bcast_u32<kRowLanes>((uint32_t)(uint64_t)t_tick, w));
+          const uint32_t gw = row_bcast_u32<kRowLanes>(gr, w);
+          const int64_t tw = (int64_t)row_bcast_u64<kRowLanes>((uint64_t)t_tick, w);
           const uint32_t sw = row_bcast_u32<kRowLanes>(t_seq, w);
-          const uint32_t dw = (hw >> 31) ? 3u : 2u;
-          off += earlier32(tw, sw, t_tick, t_seq) ? dw : 0u;
-          tot += dw;
+          const int Gw = (int)(gw & 0xFFu);
+          const uint32_t rw = gw >> 8;
+          tot += 2u * (uint32_t)Gw + (uint32_t)__builtin_popcount(rw);
+          if (G) {
+            const int64_t d = t_tick - tw;  // |d| < kBatchGens P: exact in double
+            int cd = (int)ceil((double)d / 1e10);
+            if ((int64_t)cd * kAdvertPeriod == d && (cd < 0 || (cd == 0 && sw < t_seq))) ++cd;
+#pragma unroll
+            for (int g = 0; g < kBatchGens; ++g) {
+              const int c = min(max(g + cd, 0), Gw);
+              off[g] += 2u * (uint32_t)c + (uint32_t)__builtin_popcount(rw & ((1u << c) - 1u));
+            }
+          }
+        }
+        if ((uint64_t)seq + tot > (uint64_t)kSeqLimit) {
+          err = FOGNET_ERR_CAPACITY;  // (32-bit insertion sequence)
+          fin = true;
+          G = 0u;
         }
         bool has_last = false;
         uint32_t n_rel = 0u;
-        if (inb) {
-          uint32_t sq = seq + off;
-          if (rel) {  // releaseResource: the oldest reservation, acked with status 6 (:225-235)
-            const V2Res h = rs_hd;
-            mips += h.req;  // :226
-            ++rs_h;
-            --rs_n;
-            rs_hd = rs_nx;
-            if (rs_n >= 2u) {
-              rs_nx = res[(rs_h + 1u) & qm];
-              sync_vm();
+#pragma unroll
+        for (int g = 0; g < kBatchGens; ++g) {
+          if ((uint32_t)g < G) {
+            uint32_t sq = seq + off[g];
+            const bool rl = (rmask >> g) & 1u;
+            if (rl) {  // releaseResource: the oldest reservation, acked with status 6 (:225-235)
+              const V2Res h = rs_hd;
+              mips += h.req;  // :226
+              ++rs_h;
+              --rs_n;
+              rs_hd = rs_nx;
+              if (rs_n >= 2u) {
+                rs_nx = res[(rs_h + 1u) & qm];
+                sync_vm();
+              }
+              const V2MsgR m = {t_tick + ul, sq++, kMsgAck6, h.task, 0};
+              if (out_n == Q) bad = true;
+              else {
+                if (out_n == 0u) out_hd = m;
+                else if (out_n == 1u) out_nx = m;
+                else outq[(out_h + out_n) & qm] = m;
+                ++out_n;
+              }
+              O.done_tick[tbase + h.task] = t_tick;
+              ++n_rel;
             }
-            const V2MsgR m = {t_tick + ul, sq++, kMsgAck6, h.task, 0};
-            if (out_n == Q) bad = true;
-            else {
-              if (out_n == 0u) out_hd = m;
-              else if (out_n == 1u) out_nx = m;
-              else outq[(out_h + out_n) & qm] = m;
-              ++out_n;
+            if (kPhantomAdverts && mips == last_sent && earlier32(ph_tick, ph_seq, t_tick, t_seq)) {
+              // carries the value of the node's previous advert (kPhantomAdverts)
+              ph_tick = t_tick + ul;
+              ph_seq = sq;
+              ph_cnt += ph_tick < stop ? 1u : 0u;
+            } else {
+              const V2MsgR m = {t_tick + ul, sq, kMsgAdvert, mips, 0};
+              last_sent = mips;
+              if (out_n == Q) bad = true;
+              else {
+                if (out_n == 0u) out_hd = m;
+                else if (out_n == 1u) out_nx = m;
+                else outq[(out_h + out_n) & qm] = m;
+                ++out_n;
+              }
             }
-            O.done_tick[tbase + h.task] = t_tick;
-            n_rel = 1u;
+            if (off[g] + (rl ? 3u : 2u) == tot) {  // the batch's last firing (where an error would end the replication)
+              has_last = true;
+              end_tick = t_tick;
+              end_seq = t_seq;
+            }
+            t_tick += kAdvertPeriod;
+            t_seq = sq + 1u;
           }
-          if (kPhantomAdverts && mips == last_sent && earlier32(ph_tick, ph_seq, t_tick, t_seq)) {
-            // carries the value of the node's previous advert (kPhantomAdverts)
-            ph_tick = t_tick + ul;
-            ph_seq = sq;
-            ph_cnt += ph_tick < stop ? 1u : 0u;
-          } else {
-            const V2MsgR m = {t_tick + ul, sq, kMsgAdvert, mips, 0};
-            last_sent = mips;
-            if (out_n == Q) bad = true;
-            else {
-              if (out_n == 0u) out_hd = m;
-              else if (out_n == 1u) out_nx = m;
-              else outq[(out_h + out_n) & qm] = m;
-              ++out_n;
-            }
-          }
-          has_last = off + (rel ? 3u : 2u) == tot;  // the batch's last firing (where an error would end the replication)
-          end_tick = t_tick;
-          end_seq = t_seq;
-          t_tick += kAdvertPeriod;
-          t_seq = sq + 1u;
         }
-        const uint32_t nfire = (uint32_t)__builtin_popcount(rowb);
-        if (rowb) {
+        const uint32_t nfire = (uint32_t)row_sum_i64<kRowLanes>((int64_t)G);
+        if (nfire) {
           end_tick = (int64_t)row_min_u64<kRowLanes>((uint64_t)(has_last ? end_tick : kNever));
           end_seq = row_min_u32<kRowLanes>(has_last ? end_seq : ~0u);
         }
         // the messages (a queued advert of this batch's firings included: its arrival
         // commutes with them too)
         uint32_t n_arr = 0u, n_rl = 0u;
-        while (out_n && out_hd.tick < stop && earlier32(out_hd.tick, out_hd.seq, H_t, H_s)) {
+        while (!fin && out_n && out_hd.tick < stop && earlier32(out_hd.tick, out_hd.seq, H_t, H_s)) {
           if (out_hd.kind == kMsgAdvert) {
             view = out_hd.val;  // setMips (:132)
           } else if (list[out_hd.val] == kListForwarded) {  // ack 6: relay, erase if still listed (:145-153)
