@@ -113,8 +113,10 @@ int prepare(fognet_ctx* c, const fognet_batch_in* in, fognet::ReplayArgs* a, boo
   if (!in) return fail(c, FOGNET_ERR_ARG, "null batch");
   if (in->R < 0 || in->T < 0 || in->N < 0) return fail(c, FOGNET_ERR_ARG, "negative R/T/N");
   if (in->N == 0) return fail(c, FOGNET_ERR_NO_NODES, "N == 0 (BrokerBaseApp3.cc:268 reads brokers[0])");
-  if (in->N > fognet::kWideMaxNodes)
-    return fail(c, FOGNET_ERR_UNSUPPORTED, "N > 65536 (the wide replay kernel keeps 28 B of group minima per 16 nodes in LDS)");
+  if (in->N > fognet::kWideBigMaxNodes)
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "N > 1048576 (the wide replay kernel's active-group mask: 16 words per lane)");
+  if (in->policy == FOGNET_POLICY_EXT_HIER && in->N > fognet::kWideMaxNodes)
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "EXT_HIER with N > 65536 (more than 64 regions of 1,024 nodes)");
   if (in->policy != FOGNET_POLICY_REF_V3 && in->policy != FOGNET_POLICY_EXT_LAT && in->policy != FOGNET_POLICY_EXT_HIER)
     return fail(c, FOGNET_ERR_UNSUPPORTED, "unknown policy");
   if (in->policy == FOGNET_POLICY_EXT_HIER) {
@@ -203,9 +205,9 @@ bool use_inloop() {
 // still exact.  At most kWideFallbackSlots, and no more than fit in the ring
 // workspace the register kernel needs anyway (floor 1), so a replay that never
 // hands over allocates nothing extra.
-int32_t fallback_slots(int32_t R, int32_t T, int32_t N, size_t ring_bytes, bool gen) {
+int32_t fallback_slots(int32_t R, int32_t T, int32_t N, size_t ring_bytes, bool gen, int policy) {
   int32_t slots = R < kWideFallbackSlots ? R : kWideFallbackSlots;
-  const size_t per = fognet::replay_wide_workspace_bytes(1, T, N, gen);
+  const size_t per = fognet::replay_wide_workspace_bytes(1, T, N, gen, policy);
   const size_t fit = per ? ring_bytes / per : (size_t)slots;
   if ((size_t)slots > fit) slots = fit < 1 ? 1 : (int32_t)fit;
   return slots;
@@ -510,7 +512,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       const size_t o_od = o_ost + align256(RT * sizeof(int64_t));
       const size_t body = o_od + RT * sizeof(int64_t) - o_e;
       const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
-      const size_t fb = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
+      const size_t fb = fognet::replay_wide_workspace_bytes(slots, a.T, a.N, false, a.policy);
       rc = ensure(c, (void**)&c->ring, &c->ring_bytes, o_e + (body > fb ? body : fb), "region replay workspace");
       if (rc) return rc;
       unsigned char* const base = reinterpret_cast<unsigned char*>(c->ring);
@@ -560,7 +562,7 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       }
       return FOGNET_OK;
     }
-    const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N);
+    const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N, false, a.policy);
     rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ws, "wide replay workspace");
     if (rc) return rc;
     e = fognet::launch_replay_wide(a, c->ring, a.R, (hipStream_t)stream);
@@ -577,8 +579,8 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     // replay of the handed-over replications once the register kernel is done (stream order)]
     // + for a statistics-only replay the per-task outputs the fused statistics epilogue reads back
     const size_t ring_bytes = (size_t)a.R * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingWord);
-    const int32_t slots = fallback_slots(a.R, a.T, a.N, ring_bytes, false);
-    const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N);
+    const int32_t slots = fallback_slots(a.R, a.T, a.N, ring_bytes, false, a.policy);
+    const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N, false, a.policy);
     const size_t o_board = align256(256 + (size_t)a.R * sizeof(int32_t));
     const size_t head = o_board + fognet::kBoardWords * sizeof(uint32_t);
     const size_t body = ring_bytes > fb_bytes ? ring_bytes : fb_bytes;
@@ -658,7 +660,7 @@ int fognet_run_generated_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t 
   if (a.out_energy && !a.p_busy) return fail(c, FOGNET_ERR_ARG, "node_energy_j needs the power model (p_busy_w/p_idle_w)");
   hipError_t e;
   if (use_wide(a.N) || long_run || a.policy == FOGNET_POLICY_EXT_HIER) {
-    const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N, true);
+    const size_t ws = fognet::replay_wide_workspace_bytes(a.R, a.T, a.N, true, a.policy);
     rc = ensure(c, (void**)&c->ring, &c->ring_bytes, ws, "wide replay workspace");
     if (rc) return rc;
     e = fognet::launch_replay_wide(a, c->ring, a.R, (hipStream_t)stream);
@@ -669,8 +671,8 @@ int fognet_run_generated_dev(fognet_ctx* c, const fognet_gen_params* p, int64_t 
   const int64_t resident = (int64_t)c->cus * fognet::kGenWavesPerCu;
   a.gen_slots = (int32_t)(a.R < resident ? a.R : resident);
   const size_t ring_bytes = (size_t)a.gen_slots * (size_t)a.N * ((size_t)1 << a.q_log2) * sizeof(fognet::RingWord);
-  const int32_t slots = fallback_slots(a.R, a.T, a.N, ring_bytes, true);
-  const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N, true);
+  const int32_t slots = fallback_slots(a.R, a.T, a.N, ring_bytes, true, a.policy);
+  const size_t fb_bytes = fognet::replay_wide_workspace_bytes(slots, a.T, a.N, true, a.policy);
   const size_t head = align256(256 + (size_t)a.R * sizeof(int32_t));
   rc = ensure(c, (void**)&c->ring, &c->ring_bytes, head + (ring_bytes > fb_bytes ? ring_bytes : fb_bytes),
               "ring workspace");

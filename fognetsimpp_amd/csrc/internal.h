@@ -336,11 +336,14 @@ static_assert(sizeof(WideNode) == 64, "wide node record is one 64-B line");
 // advert, its node, the smallest view key and run-horizon bound (28 B) + the histogram; the
 // per-node view (next advert tick, advertised busy) is in HBM.
 constexpr int kWideGroupSlots = 16;
-constexpr int kWideMaxNodes = 65536;  // LDS: 115 KiB of group minima
+constexpr int kWideMaxNodes = 65536;  // LDS: 115 KiB of group minima (FOGNET_POLICY_EXT_HIER's limit)
+// Above kWideMaxNodes the flat policies keep the group minima in HBM (2 KiB per group of
+// 1,024 nodes per workspace slot), up to:
+constexpr int kWideBigMaxNodes = 1 << 20;
 size_t replay_wide_lds_bytes(int32_t N);
 // workspace: R*T WideEntry followed by R*N WideNode
-// (+ R*N generated node parameters in generated mode)
-size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen = false);
+// (+ R*N generated node parameters in generated mode, + the HBM group minima above kWideMaxNodes)
+size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen, int policy);
 // slots: workspace slots (workgroups).  With a.wide_list unset, slots == R and
 // workgroup r replays replication r; with it set, the workgroups take the
 // listed replications in turn (slots <= R bounds the workspace).

@@ -97,6 +97,12 @@ struct WideLds {
 // overflow list (WideWs::ov_off, see flush_pending).
 constexpr int kHierPending = kWave;
 
+// Group minima in LDS up to 64 groups per lane (N <= 65,536, kWideMaxNodes); the flat
+// policies above that (BIG) keep them in HBM, up to kWideBigMaxNodes (kGWords mask words).
+constexpr int kWideLdsGroups = 64;
+constexpr int kGWords = kWideBigMaxNodes / (kWave * kWideGroupSlots * 64);
+static_assert(kGWords <= 32, "the summary of non-zero mask words is 32 bits");
+
 // This lane's view in HBM: slot s (node s * 64 + lane) at [s].
 struct WideView {
   int64_t* nxt;    // [G * kWideGroupSlots]
@@ -175,15 +181,48 @@ __device__ __forceinline__ uint64_t lane_min_key(const WideLds& L, int lane) {
   return mk;
 }
 
-// The same over the groups with a pending advert only (bit g of ga; G <= 64): the
-// other groups hold kNever in both minima.
-__device__ __forceinline__ void lane_min_nxt_w_m(const WideLds& L, int lane, uint64_t ga, int64_t& mn, int& mj,
-                                                 int64_t& mw) {
+// The lane's groups with a pending advert (the lane minima and the run horizon visit only
+// these).  Up to 64 groups per lane (N <= 65,536): a bit mask in a register.  Above (BIG,
+// the flat policies up to kWideBigMaxNodes, the group minima in HBM): kGWords mask words
+// per lane in LDS ([word][lane]) and a register summary of the non-zero words.
+template <bool BIG>
+struct GroupSet {
+  uint64_t m = 0ull;        // !BIG: bit g
+  uint32_t sum = 0u;        // BIG: bit w: word w is not zero
+  uint64_t* wl = nullptr;   // BIG: this lane's words, wl[w * kWave]
+  __device__ __forceinline__ void set(int g, bool on) {
+    if constexpr (!BIG) {
+      m = on ? m | (1ull << g) : m & ~(1ull << g);
+    } else {
+      const int w = g >> 6;
+      uint64_t x = wl[w * kWave];
+      x = on ? x | (1ull << (g & 63)) : x & ~(1ull << (g & 63));
+      wl[w * kWave] = x;
+      sum = x ? sum | (1u << w) : sum & ~(1u << w);
+    }
+  }
+  template <class F>
+  __device__ __forceinline__ void each(F&& f) const {
+    if constexpr (!BIG) {
+      for (uint64_t x = m; x; x &= x - 1ull) f((int)__builtin_ctzll(x));
+    } else {
+      for (uint32_t s = sum; s; s &= s - 1u) {
+        const int w = (int)__builtin_ctz(s);
+        for (uint64_t x = wl[w * kWave]; x; x &= x - 1ull) f(w * 64 + (int)__builtin_ctzll(x));
+      }
+    }
+  }
+};
+
+// The same over the groups with a pending advert only: the other groups hold kNever in
+// both minima.
+template <bool BIG>
+__device__ __forceinline__ void lane_min_nxt_w_m(const WideLds& L, int lane, const GroupSet<BIG>& ga, int64_t& mn,
+                                                 int& mj, int64_t& mw) {
   mn = kNever;
   mj = lane;
   mw = kNever;
-  for (uint64_t m = ga; m; m &= m - 1ull) {
-    const int g = (int)__builtin_ctzll(m);
+  ga.each([&](int g) {
     const int64_t x = L.g_nxt[g * kWave + lane];
     const int jj = L.g_j[g * kWave + lane];
     const int64_t w = L.g_w[g * kWave + lane];
@@ -192,20 +231,21 @@ __device__ __forceinline__ void lane_min_nxt_w_m(const WideLds& L, int lane, uin
       mj = jj;
     }
     mw = w < mw ? w : mw;
-  }
+  });
 }
-__device__ __forceinline__ void lane_min_nxt_m(const WideLds& L, int lane, uint64_t ga, int64_t& mn, int& mj) {
+template <bool BIG>
+__device__ __forceinline__ void lane_min_nxt_m(const WideLds& L, int lane, const GroupSet<BIG>& ga, int64_t& mn,
+                                               int& mj) {
   mn = kNever;
   mj = lane;
-  for (uint64_t m = ga; m; m &= m - 1ull) {
-    const int g = (int)__builtin_ctzll(m);
+  ga.each([&](int g) {
     const int64_t x = L.g_nxt[g * kWave + lane];
     const int jj = L.g_j[g * kWave + lane];
     if (x < mn) {
       mn = x;
       mj = jj;
     }
-  }
+  });
 }
 
 __device__ __forceinline__ void lane_min(const WideLds& L, int lane, int64_t& mn, int& mj, uint64_t& mk) {
@@ -241,13 +281,20 @@ __device__ __forceinline__ int64_t node_w(const WideNode& h, int64_t nxt, int64_
 
 // Workspace layout (launch_replay_wide, replay_wide_workspace_bytes).
 struct WideWs {
-  size_t e_off, nd_off, nxt_off, busy_off, w_off, dv_off, gm_off, gd_off, gu_off, ov_off, bytes;
+  size_t e_off, nd_off, nxt_off, busy_off, w_off, dv_off, gm_off, gd_off, gu_off, ov_off, gx_off, bytes;
 };
+
+// BIG (group minima in HBM): per workspace slot [G][64] of g_nxt, g_key, g_w (8 B), g_j,
+// g_msk (4 B): 2 KiB per group
+constexpr size_t kGxGroupBytes = (size_t)kWave * (3 * sizeof(int64_t) + 2 * sizeof(int32_t));
+__host__ __device__ __forceinline__ bool wide_big(int32_t N, bool force) {
+  return force || wide_groups(N) > kWideLdsGroups;
+}
 
 __host__ __device__ __forceinline__ size_t align64(size_t x) { return (x + 63) & ~(size_t)63; }
 
 // gen: + the generated node parameters (MIPS, dl, ul) of each slot
-__host__ __device__ __forceinline__ WideWs wide_ws(int32_t R, int32_t T, int32_t N, bool gen) {
+__host__ __device__ __forceinline__ WideWs wide_ws(int32_t R, int32_t T, int32_t N, bool gen, bool big) {
   const size_t SP = (size_t)wide_groups(N) * kWideGroupSlots;  // view slots per lane
   WideWs w;
   w.e_off = 0;
@@ -262,7 +309,8 @@ __host__ __device__ __forceinline__ WideWs wide_ws(int32_t R, int32_t T, int32_t
   w.gu_off = align64(w.gd_off + RN * sizeof(int64_t));
   // EXT_HIER: the pending-escalation overflow list, [R][T] task indices
   w.ov_off = align64(w.gu_off + RN * sizeof(int64_t));
-  w.bytes = align64(w.ov_off + (size_t)R * (size_t)T * sizeof(int32_t));
+  w.gx_off = align64(w.ov_off + (size_t)R * (size_t)T * sizeof(int32_t));
+  w.bytes = align64(w.gx_off + (big ? (size_t)R * (size_t)wide_groups(N) * kGxGroupBytes : 0));
   return w;
 }
 
@@ -274,49 +322,53 @@ struct GenNodes {
   uint64_t* dv;
 };
 
-template <int POL>
+template <int POL, bool BIG>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
                                                 int64_t* VN, uint32_t* VB, int64_t* VW, GenNodes GN, int32_t* OV,
-                                                unsigned char* w_lds);
+                                                unsigned char* GX, unsigned char* w_lds);
 
 // One replication per workgroup (r = blockIdx.x), or, with A.wide_list set,
 // the replications the register kernel handed over, taken in turn by the
 // workgroups (workspace slot = blockIdx.x); every workgroup leaves when the
 // list (complete before this launch, stream order) is exhausted.
-template <int POL>
+template <int POL, bool BIG>
 __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry* E, WideNode* ND, int64_t* VN,
-                                                         uint32_t* VB, int64_t* VW, GenNodes GN, int32_t* OV) {
+                                                         uint32_t* VB, int64_t* VW, GenNodes GN, int32_t* OV,
+                                                         unsigned char* GX) {
   extern __shared__ __align__(16) unsigned char w_lds[];
   if (A.wide_list == nullptr) {
-    replay_wide_rep<POL>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, VW, GN, OV, w_lds);
+    replay_wide_rep<POL, BIG>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, VW, GN, OV, GX, w_lds);
     return;
   }
   const int n = *A.wide_count;
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
-    replay_wide_rep<POL>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, VW, GN, OV, w_lds);
+    replay_wide_rep<POL, BIG>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, VW, GN, OV, GX, w_lds);
     __syncthreads();  // LDS reuse by the next replication
   }
 }
 
 // Replication r with workspace slot wr.
-template <int POL>
+template <int POL, bool BIG>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
                                                 int64_t* VN, uint32_t* VB, int64_t* VW, GenNodes GN, int32_t* OV,
-                                                unsigned char* w_lds) {
+                                                unsigned char* GX, unsigned char* w_lds) {
   constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
   constexpr bool kHier = POL == FOGNET_POLICY_EXT_HIER;
+  static_assert(!(BIG && kHier), "EXT_HIER keeps its regions (groups) in LDS");
   constexpr bool kPerPublish = kExt || kHier;  // the decision depends on the publish itself
   const int lane = threadIdx.x;
   const int T = A.T, N = A.N;
   WideLds L;
   L.G = wide_groups(N);
-  L.g_nxt = reinterpret_cast<int64_t*>(w_lds);
+  // group minima: LDS, or (BIG) this workspace slot's [G][64] arrays in HBM
+  unsigned char* const gbase = BIG ? GX + (size_t)wr * (size_t)L.G * kGxGroupBytes : w_lds;
+  L.g_nxt = reinterpret_cast<int64_t*>(gbase);
   L.g_key = reinterpret_cast<uint64_t*>(L.g_nxt + L.G * kWave);
   L.g_w = reinterpret_cast<int64_t*>(L.g_key + L.G * kWave);
   L.g_j = reinterpret_cast<int32_t*>(L.g_w + L.G * kWave);
-  L.hist = reinterpret_cast<uint32_t*>(L.g_j + L.G * kWave);
+  L.hist = BIG ? reinterpret_cast<uint32_t*>(w_lds) : reinterpret_cast<uint32_t*>(L.g_j + L.G * kWave);
   L.reg_key = reinterpret_cast<uint64_t*>(L.hist + FOGNET_HIST_METRICS * FOGNET_HIST_BINS);
-  L.p_t = reinterpret_cast<int64_t*>(L.reg_key + L.G);
+  L.p_t = reinterpret_cast<int64_t*>(L.reg_key + (BIG ? 0 : L.G));
   L.p_a = L.p_t + kHierPending;
   L.p_i = reinterpret_cast<int32_t*>(L.p_a + kHierPending);
   L.p_k = L.p_i + kHierPending;
@@ -327,7 +379,9 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   L.q_dn = L.q_st + kWave;
   L.q_i = reinterpret_cast<int32_t*>(L.q_dn + kWave);
   L.q_sS = reinterpret_cast<uint32_t*>(L.q_i + kWave);
-  L.g_msk = L.q_sS + kWave;
+  L.g_msk = BIG ? reinterpret_cast<uint32_t*>(L.g_j + L.G * kWave) : L.q_sS + kWave;
+  // BIG: the active-group mask words after the other LDS arrays ([kGWords][64])
+  uint64_t* const gw_lds = reinterpret_cast<uint64_t*>(BIG ? reinterpret_cast<unsigned char*>(L.q_sS + kWave) : w_lds);
   const int SP = L.G * kWideGroupSlots;
   const WideView V{VN + ((size_t)wr * kWave + lane) * SP, VB + ((size_t)wr * kWave + lane) * SP,
                    VW + ((size_t)wr * kWave + lane) * SP};
@@ -403,7 +457,11 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   int mj;
   uint64_t mk;
   lane_min(L, lane, mn, mj, mk);
-  uint64_t gact = 0ull;  // the lane's groups with a pending advert (lane minima visit only these)
+  GroupSet<BIG> gact;  // the lane's groups with a pending advert (lane minima visit only these)
+  if constexpr (BIG) {
+    gact.wl = gw_lds + lane;
+    for (int w = 0; w < kGWords; ++w) gact.wl[w * kWave] = 0ull;
+  }
   int64_t mw = kNever;  // REF_V3 run horizon: this lane's smallest node_w
   Acc acc = acc_identity();
   AbortPt ab = abort_none();  // the reference's abort point (replay_common.h)
@@ -533,7 +591,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         V.nxt[kk / kWave] = x;
         if (x != kNever) {
           L.g_msk[g * kWave + lane] |= 1u << ((kk / kWave) % kWideGroupSlots);
-          gact |= 1ull << g;
+          gact.set(g, true);
         }
         if (x < L.g_nxt[g * kWave + lane]) {
           L.g_nxt[g * kWave + lane] = x;
@@ -798,7 +856,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           }
           L.g_nxt[g * kWave + lane] = gmn;
           L.g_j[g * kWave + lane] = gmn == kNever ? lane : wnode<kHier>(g * kWideGroupSlots + gsi, lane);
-          gact = (gm & 0xFFFFu) != 0u ? gact | (1ull << g) : gact & ~(1ull << g);
+          gact.set(g, (gm & 0xFFFFu) != 0u);
           if constexpr (!kPerPublish) {
             L.g_w[g * kWave + lane] = gmw;
             lane_min_nxt_w_m(L, lane, gact, mn, mj, mw);  // (one LDS pass for both lane minima)
@@ -963,15 +1021,14 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
         // a group whose nodes all have larger indices than k, with busy_b = 0, never matters
         const uint32_t busy_b = (uint32_t)(k_key >> 32);
         int64_t e_lane = kNever;
-        for (uint64_t m = gact; m; m &= m - 1ull) {
-          const int g = (int)__builtin_ctzll(m);
+        gact.each([&](int g) {
           const uint32_t thr = busy_b - (((uint32_t)(g * kWave * kWideGroupSlots) + (uint32_t)lane > k) ? 1u : 0u);
-          if (thr == 0xFFFFFFFFu) continue;  // (busy_b = 0 and every node of the group after k)
+          if (thr == 0xFFFFFFFFu) return;  // (busy_b = 0 and every node of the group after k)
           const int64_t gx = L.g_nxt[g * kWave + lane], gw = L.g_w[g * kWave + lane];
           int64_t bnd = gx;
           if (thr < (1u << 21) && (uint64_t)(gw - gx) > (uint64_t)ticks_of(thr)) bnd = gw - ticks_of(thr);
           e_lane = bnd < e_lane ? bnd : e_lane;
-        }
+        });
         int64_t E = (int64_t)wave_min_u64((uint64_t)e_lane);
         if (npend0 > 0) {  // k's own next advert changes its key
           const int64_t hd_done_k = readlane_i64(ch.hd_done, kl);
@@ -1089,7 +1146,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           V.nxt[k / kWave] = x;
           if (x != kNever) {
             L.g_msk[g * kWave + lane] |= 1u << ((k / kWave) % kWideGroupSlots);
-            gact |= 1ull << g;
+            gact.set(g, true);
           }
           if (x < L.g_nxt[g * kWave + lane]) {
             L.g_nxt[g * kWave + lane] = x;
@@ -1209,7 +1266,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     const double sum = energy_sum_wave(reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(nd) + offsetof(WideNode, tl_C)),
                                        (int)(sizeof(WideNode) / sizeof(uint64_t)), A.p_busy + nbase, A.p_idle + nbase, N, H,
                                        A.out_energy ? A.out_energy + (size_t)r * (size_t)N : nullptr, lane,
-                                       reinterpret_cast<double*>(L.g_nxt));  // (the group minima are dead here)
+                                       // (LDS the loop no longer reads: the group minima or, BIG, the group mask words)
+                                       reinterpret_cast<double*>(BIG ? reinterpret_cast<unsigned char*>(gw_lds) : w_lds));
     if (lane == 0) S->energy_j = sum;
   }
   if (hist) {
@@ -1219,29 +1277,50 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   }
 }
 
-template <int POL>
+template <int POL, bool BIG>
 void launch_wide_pol(const ReplayArgs& a, int32_t slots, WideEntry* e, WideNode* nd, int64_t* vn, uint32_t* vb,
-                     int64_t* vw, GenNodes gn, int32_t* ov, size_t lds, hipStream_t s) {
+                     int64_t* vw, GenNodes gn, int32_t* ov, unsigned char* gx, size_t lds, hipStream_t s) {
   if (lds > 65536)  // above the default dynamic-LDS limit (N > ~51,000 nodes; gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&replay_wide_kernel<POL>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&replay_wide_kernel<POL, BIG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((replay_wide_kernel<POL>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb, vw, gn, ov);
+  hipLaunchKernelGGL((replay_wide_kernel<POL, BIG>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb, vw, gn, ov,
+                     gx);
+}
+
+// FOGNET_WIDE_BIG=1: the HBM group minima at any N (the flat policies; parity tests of both layouts)
+bool wide_force_big() {
+  const char* f = getenv("FOGNET_WIDE_BIG");
+  return f && f[0] == '1';
+}
+
+
+// (big: wide_big -- the group minima in HBM, the active-group mask words in LDS)
+size_t wide_lds_bytes(int32_t N, bool big) {
+  const size_t G = (size_t)wide_groups(N);
+  const size_t rest = FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t) +
+                      kHierPending * (2 * sizeof(int64_t) + 3 * sizeof(int32_t)) +
+                      kWave * (4 * sizeof(int64_t) + 2 * sizeof(int32_t));
+  if (big) return rest + (size_t)kGWords * kWave * sizeof(uint64_t);
+  return G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int64_t) + sizeof(int32_t)) + rest +
+         G * sizeof(uint64_t) + G * kWave * sizeof(uint32_t);
 }
 
 }  // namespace
 
-size_t replay_wide_lds_bytes(int32_t N) {
-  const size_t G = (size_t)wide_groups(N);
-  return G * kWave * (sizeof(int64_t) + sizeof(uint64_t) + sizeof(int64_t) + sizeof(int32_t)) +
-         FOGNET_HIST_METRICS * FOGNET_HIST_BINS * sizeof(uint32_t) + G * sizeof(uint64_t) +
-         kHierPending * (2 * sizeof(int64_t) + 3 * sizeof(int32_t)) + kWave * (4 * sizeof(int64_t) + 2 * sizeof(int32_t)) +
-         G * kWave * sizeof(uint32_t);
+size_t replay_wide_lds_bytes(int32_t N) { return wide_lds_bytes(N, wide_big(N, false)); }
+
+// (the EXT_HIER regions stay groups in LDS: N <= kWideMaxNodes, never BIG)
+static bool wide_big_for(int32_t N, int policy) {
+  return policy != FOGNET_POLICY_EXT_HIER && wide_big(N, wide_force_big());
 }
 
-size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen) { return wide_ws(R, T, N, gen).bytes; }
+size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen, int policy) {
+  return wide_ws(R, T, N, gen, wide_big_for(N, policy)).bytes;
+}
 
 hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slots, hipStream_t s) {
-  const WideWs w = wide_ws(slots, a.T, a.N, a.gen_on != 0);
+  const bool big = wide_big_for(a.N, a.policy);
+  const WideWs w = wide_ws(slots, a.T, a.N, a.gen_on != 0, big);
   unsigned char* const base = static_cast<unsigned char*>(workspace);
   WideEntry* const e = reinterpret_cast<WideEntry*>(base + w.e_off);
   WideNode* const nd = reinterpret_cast<WideNode*>(base + w.nd_off);
@@ -1251,13 +1330,20 @@ hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slot
   const GenNodes gn{reinterpret_cast<int32_t*>(base + w.gm_off), reinterpret_cast<int64_t*>(base + w.gd_off),
                     reinterpret_cast<int64_t*>(base + w.gu_off), reinterpret_cast<uint64_t*>(base + w.dv_off)};
   int32_t* const ov = reinterpret_cast<int32_t*>(base + w.ov_off);
-  const size_t lds = replay_wide_lds_bytes(a.N);
-  if (a.policy == FOGNET_POLICY_EXT_LAT)
-    launch_wide_pol<FOGNET_POLICY_EXT_LAT>(a, slots, e, nd, vn, vb, vw, gn, ov, lds, s);
-  else if (a.policy == FOGNET_POLICY_EXT_HIER)
-    launch_wide_pol<FOGNET_POLICY_EXT_HIER>(a, slots, e, nd, vn, vb, vw, gn, ov, lds, s);
-  else
-    launch_wide_pol<FOGNET_POLICY_REF_V3>(a, slots, e, nd, vn, vb, vw, gn, ov, lds, s);
+  unsigned char* const gx = base + w.gx_off;
+  const size_t lds = wide_lds_bytes(a.N, big);
+  if (a.policy == FOGNET_POLICY_EXT_LAT) {
+    if (big)
+      launch_wide_pol<FOGNET_POLICY_EXT_LAT, true>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, lds, s);
+    else
+      launch_wide_pol<FOGNET_POLICY_EXT_LAT, false>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, lds, s);
+  } else if (a.policy == FOGNET_POLICY_EXT_HIER) {
+    launch_wide_pol<FOGNET_POLICY_EXT_HIER, false>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, lds, s);
+  } else if (big) {
+    launch_wide_pol<FOGNET_POLICY_REF_V3, true>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, lds, s);
+  } else {
+    launch_wide_pol<FOGNET_POLICY_REF_V3, false>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, lds, s);
+  }
   return hipGetLastError();
 }
 

@@ -71,7 +71,7 @@ typedef enum fognet_status {
     FOGNET_ERR_CAPACITY = 7,    /* v2 queue_capacity exceeded; a decision whose smallest advertised busy
                                    time is 2^32 - 1 s or more (the view keeps 32 bits, saturated: larger
                                    values only lose); EXT_LAT: an advertised busy time of 2^24 s or more */
-    FOGNET_ERR_UNSUPPORTED = 8, /* configuration not implemented (e.g. N > 65,536, unknown policy)     */
+    FOGNET_ERR_UNSUPPORTED = 8, /* configuration not implemented (e.g. N > 2^20, unknown policy)     */
     FOGNET_REF_ABORTED = 9,     /* replication status under FOGNET_FLAG_REF_ABORT: the reference run ends
                                    at a queueTime emission that overflows (ComputeBrokerApp3.cc:238; see
                                    "Reference signal values"); outputs are still written in full     */

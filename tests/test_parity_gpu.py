@@ -359,9 +359,16 @@ def test_precondition_errors(ctx, bad, N):
 
 
 def test_unsupported_sizes(ctx):
-    tr = tg.make_batch(5, 1, 65537, 10)  # kWideMaxNodes: the wide kernel's LDS group minima
+    """The wide kernel's limits: N <= 2^20 for the flat policies (its active-group mask words),
+    N <= 65,536 for EXT_HIER (64 regions of 1,024 nodes); refused loudly above."""
+    tr = tg.make_batch(5, 1, (1 << 20) + 1, 4)
     with pytest.raises(fa.FognetError) as e:
         run_gpu(ctx, tr)
+    assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED
+    tr = tg.make_batch(5, 1, 65537, 10)
+    tr["region"] = np.zeros((1, 10), np.int32)
+    with pytest.raises(fa.FognetError) as e:
+        run_gpu_full(ctx, tr, policy="EXT_HIER")
     assert e.value.code == _abi.FOGNET_ERR_UNSUPPORTED
 
 
@@ -880,7 +887,8 @@ def test_ext_lat_latency_bound(ctx):
 # on node 0 for the whole trace; light loads spread decisions over many nodes.
 @pytest.mark.parametrize("N,T,R,rho", [(257, 2000, 3, 0.8), (700, 3000, 3, 0.01), (4096, 4000, 2, 0.01),
                                        (12288, 3000, 1, 0.002), (20000, 1500, 1, 0.001),
-                                       (65536, 1200, 1, 0.0005)])  # the advertised limit (82 KiB of LDS)
+                                       (65536, 1200, 1, 0.0005),  # the last N with the group minima in LDS
+                                       (70000, 1200, 2, 0.0005), (262144, 400, 1, 0.0002)])  # in HBM (BIG)
 def test_wide_matches_oracle(ctx, N, T, R, rho):
     tr = tg.make_batch(0x5EED0005 + N, R, N, T, rho=rho, lat_scale=10)
     pb, pi = fa.power_model(tr["mips"])
@@ -893,6 +901,36 @@ def test_wide_matches_oracle(ctx, N, T, R, rho):
     np.testing.assert_array_equal(g["energy"], o["node_energy"])
     assert g["stats"].tobytes() == o["stats"].tobytes()
     np.testing.assert_array_equal(g["hist"], o["hist"].sum(axis=0))
+
+
+@pytest.mark.parametrize("policy,N,down", [("REF_V3", 700, False), ("REF_V3", 10_000, False), ("EXT_LAT", 3000, False),
+                                           ("REF_V3", 2000, True)])
+def test_wide_big_layout_equals_lds_layout(ctx, monkeypatch, policy, N, down):
+    """FOGNET_WIDE_BIG=1 keeps the wide kernel's group minima in HBM (the layout above N = 65,536)
+    at any N: every output, record and histogram equals the LDS layout's, and the oracle's."""
+    tr = tg.make_batch(0xB16 + N, 3, N, 2000, rho=0.01, lat_scale=10)
+    if down:
+        tr = with_crashes(tr, 5, 0.2)
+    lds = run_gpu_full(ctx, tr, policy=policy)
+    monkeypatch.setenv("FOGNET_WIDE_BIG", "1")
+    big = run_gpu_full(ctx, tr, policy=policy)
+    for k in ("node", "status", "start", "done", "hist"):
+        np.testing.assert_array_equal(big[k], lds[k], err_msg=k)
+    assert big["stats"].tobytes() == lds["stats"].tobytes()
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=3, hist=True,
+                     policy=ol.POLICIES[policy], down=tr.get("down"))
+    assert_parity(tr, big, o)
+
+
+def test_wide_ext_lat_above_65536_nodes(ctx):
+    """EXT_LAT (the north-star cost, every node's cost per publish) at N = 70,000: the group
+    minima in HBM; equal to the oracle."""
+    tr = tg.make_batch(0x7000, 1, 70_000, 300, sweep=True)
+    g = run_gpu_full(ctx, tr, policy="EXT_LAT")
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], policy=ol.POLICY_EXT_LAT,
+                     hist=True)
+    assert (o["stats"]["status"] == 0).all()
+    assert_parity(tr, g, o)
 
 
 @pytest.mark.parametrize("N", [1, 5, 64, 100, 256])
