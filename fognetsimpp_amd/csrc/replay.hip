@@ -799,6 +799,10 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   ch_stamp = ops;
   int64_t n_done = 0;
   uint32_t scan = 0u;  // profile builds: ring entries read by c_arrived (per lane)
+#if FOGNET_REPLAY_PROFILE == 3
+  // timeline probe (tools/c3_timeline.py): the wave's start, replay end and epilogue end (s_memtime)
+  const uint64_t tl_t0 = __builtin_amdgcn_s_memtime();
+#endif
 #if FOGNET_REPLAY_PROFILE == 2
   uint64_t p_t[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t p_start = __builtin_amdgcn_s_memtime();
@@ -1248,7 +1252,10 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
     S->resp_sq_hi = p_endh_same;
 #endif
   }
-#if !defined(FOGNET_REPLAY_PROFILE) || FOGNET_REPLAY_PROFILE == 0
+#if FOGNET_REPLAY_PROFILE == 3
+  const uint64_t tl_t1 = __builtin_amdgcn_s_memtime();
+#endif
+#if !defined(FOGNET_REPLAY_PROFILE) || FOGNET_REPLAY_PROFILE == 0 || FOGNET_REPLAY_PROFILE == 3
   if constexpr (INL) {
     if (A.out_stats && err != kNeedsWide) {
       // busy seconds, per-node service (energy) and `last` from the node
@@ -1272,6 +1279,18 @@ __device__ __forceinline__ void replay_body(const ReplayArgs& A, const int r, co
   } else if (A.fuse_stats && A.out_stats && err != kNeedsWide) {
     fused_stats_epilogue<NPL>(A, r, n_done, err, s_tld, s_tlC, s_ul, s_dl, s_ch,
                               reinterpret_cast<int64_t*>(kAbInDvm ? (void*)s_dvm : (void*)s_abx), lane);
+  }
+#endif
+#if FOGNET_REPLAY_PROFILE == 3
+  if constexpr (!GEN && !INL) {
+    const uint64_t tl_t2 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (lane == 0 && T >= 4) {  // (over the replication's first outputs: a timing probe only)
+      A.out_done[tbase + 0] = (int64_t)tl_t0;
+      A.out_done[tbase + 1] = (int64_t)tl_t1;
+      A.out_done[tbase + 2] = (int64_t)tl_t2;
+      A.out_done[tbase + 3] = (int64_t)board_slot();
+    }
   }
 #endif
 }
