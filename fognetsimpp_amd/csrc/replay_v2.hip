@@ -146,6 +146,17 @@ struct V2Node {
 // NPL nodes per lane (N <= 64 * NPL): node j on lane j % 64, slot j / 64, like
 // the v3 register kernel.  The slot is a compile-time index everywhere (static
 // loops select it), so the state stays in registers.
+// A lane's slots as a bit mask (bit s: slot s): 128 bits above 64 slots per lane.
+__device__ __forceinline__ int slot_ctz(uint64_t m) { return (int)__builtin_ctzll(m); }
+__device__ __forceinline__ int slot_ctz(unsigned __int128 m) {
+  const uint64_t lo = (uint64_t)m;
+  return lo ? (int)__builtin_ctzll(lo) : 64 + (int)__builtin_ctzll((uint64_t)(m >> 64));
+}
+__device__ __forceinline__ uint32_t slot_popc(uint64_t m) { return (uint32_t)__popcll(m); }
+__device__ __forceinline__ uint32_t slot_popc(unsigned __int128 m) {
+  return (uint32_t)__popcll((uint64_t)m) + (uint32_t)__popcll((uint64_t)(m >> 64));
+}
+
 template <int NPL>
 __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
   constexpr int kPad = NPL * kWave;  // queue rows per replication
@@ -177,6 +188,7 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
   // by ws directly and goes to scratch, read by one handler per step instead of by
   // every step's scan.  NPL <= 4 keeps everything in VGPRs (static slot loops).
   constexpr bool kCold = NPL >= FOGNET_V2_COLD_NPL;
+  using SlotMask = std::conditional_t<(NPL > 64), unsigned __int128, uint64_t>;
   int64_t h_tick[kCold ? NPL : 1];
   uint64_t h_seq[kCold ? NPL : 1];
   int32_t h_src[kCold ? NPL : 1], h_view[kCold ? NPL : 1];
@@ -275,25 +287,25 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       for (int s = 0; s < NPL; ++s) f(nd[s], s);
     }
   };
-  auto for_slots_in = [&](uint64_t m, auto&& f) {
+  auto for_slots_in = [&](SlotMask m, auto&& f) {
     if constexpr (kCold) {
-      for (; m; m &= m - 1ull) {
-        const int s = (int)__builtin_ctzll(m);
+      for (; m; m &= m - 1) {
+        const int s = slot_ctz(m);
         f(nd[s], s);
       }
     } else {
 #pragma unroll
       for (int s = 0; s < NPL; ++s)
-        if ((m >> s) & 1ull) f(nd[s], s);
+        if ((m >> s) & 1u) f(nd[s], s);
     }
   };
-  // batch ranks (kBatchFirings): the batch's firings as (tick, seq << 13 | releases << 12 |
+  // batch ranks (kBatchFirings): the batch's firings as (tick, seq << 14 | releases << 13 |
   // node) sorted in LDS; then each firing's sequence-number offset, by node (aliasing the
   // ticks, dead once sorted)
   __shared__ int64_t s_bt[NPL * kWave];
   __shared__ uint64_t s_bk[NPL * kWave];
   uint32_t* const s_off = reinterpret_cast<uint32_t*>(s_bt);
-  static_assert(NPL * kWave <= (1 << 12), "node index in 12 bits of the batch key");
+  static_assert(NPL * kWave <= (1 << 13), "node index in 13 bits of the batch key");
 
   // ---- broker (wave-uniform)
   int32_t pool = A.broker_mips[r];
@@ -411,27 +423,27 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       }
       // the batch's firings (bit s: slot s), and those that release a reservation
       // (ComputeBrokerApp2.cc:222-226: the oldest, when its deadline < now)
-      uint64_t cm = 0ull, rm = 0ull;
+      SlotMask cm = 0, rm = 0;
       for_slots([&](V2Node& x, int s) {
         if (x.t_sched && x.t_tick < stop && earlier(x.t_tick, x.t_seq, H_t, H_s)) {
-          cm |= 1ull << s;
+          cm |= (SlotMask)1 << s;
           if (x.t_kind == kKindRelease && x.rs_n) {
             const V2Res h = P.res[qrow(s) + (x.rs_h & qm)];
-            if (h.deadline < dbl(x.t_tick)) rm |= 1ull << s;
+            if (h.deadline < dbl(x.t_tick)) rm |= (SlotMask)1 << s;
           }
         }
       });
-      const uint32_t c = (uint32_t)__popcll(cm);
+      const uint32_t c = slot_popc(cm);
       const uint32_t c_incl = wave_scan_add_u32(c);
       const uint32_t n = readlane_u32(c_incl, kWave - 1);
-      if (seq >= (1ull << 50)) {  // (the sort key keeps the sequence in 51 bits)
+      if (seq >= (1ull << 49)) {  // (the sort key keeps the sequence in 50 bits)
         err = FOGNET_ERR_CAPACITY;
         break;
       }
       uint32_t p = c_incl - c;
       for_slots_in(cm, [&](V2Node& x, int s) {
         s_bt[p] = x.t_tick;
-        s_bk[p] = (x.t_seq << 13) | (((rm >> s) & 1ull) << 12) | (uint64_t)(s * kWave + lane);
+        s_bk[p] = (x.t_seq << 14) | ((uint64_t)((rm >> s) & 1u) << 13) | (uint64_t)(s * kWave + lane);
         ++p;
       });
       uint32_t n2 = 1u;
@@ -465,9 +477,9 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       for (uint32_t b0 = 0u; b0 < n; b0 += kWave) {
         const uint32_t i = b0 + (uint32_t)lane;
         const uint64_t kx = i < n ? s_bk[i] : 0ull;
-        const uint32_t rl = i < n ? (uint32_t)(kx >> 12) & 1u : 0u;
+        const uint32_t rl = i < n ? (uint32_t)(kx >> 13) & 1u : 0u;
         const uint32_t incl = wave_scan_add_u32(rl);
-        if (i < n) s_off[kx & 0xFFFu] = 2u * i + n_relb + incl - rl;
+        if (i < n) s_off[kx & 0x1FFFu] = 2u * i + n_relb + incl - rl;
         n_relb += readlane_u32(incl, kWave - 1);
       }
       __syncthreads();
@@ -478,7 +490,7 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       uint64_t lt_s = 0ull;
       for_slots_in(cm, [&](V2Node& x, int s) {
         const uint32_t off = s_off[s * kWave + lane];
-        const bool rel = (rm >> s) & 1ull;
+        const bool rel = ((rm >> s) & 1u) != 0;
         uint64_t sq = seq + off;
         const int64_t ft = x.t_tick;
         const uint64_t fs = x.t_seq;
@@ -1671,8 +1683,10 @@ hipError_t launch_replay_v2(const fognet_v2_in& in, const fognet_v2_out& out, vo
     hipLaunchKernelGGL(replay_v2_kernel<16>, dim3(in.R), dim3(kWave), 0, s, a);
   else if (in.N <= 2048)
     hipLaunchKernelGGL(replay_v2_kernel<32>, dim3(in.R), dim3(kWave), 0, s, a);
-  else
+  else if (in.N <= 4096)
     hipLaunchKernelGGL(replay_v2_kernel<64>, dim3(in.R), dim3(kWave), 0, s, a);
+  else
+    hipLaunchKernelGGL(replay_v2_kernel<128>, dim3(in.R), dim3(kWave), 0, s, a);
   return hipGetLastError();
 }
 

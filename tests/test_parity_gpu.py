@@ -1149,15 +1149,17 @@ def v2_random(seed, R, N, T):
 
 @pytest.mark.parametrize("seed,N,R", [(0, 1, 16), (1, 2, 16), (2, 5, 16), (3, 13, 16), (4, 64, 16), (5, 5, 16),
                                       (6, 16, 7), (7, 17, 5), (8, 3, 1), (9, 5, 13), (10, 65, 5), (11, 200, 4),
-                                      (12, 129, 3), (13, 300, 2), (14, 1024, 2), (15, 2048, 2), (16, 4096, 1)])
+                                      (12, 129, 3), (13, 300, 2), (14, 1024, 2), (15, 2048, 2), (16, 4096, 1),
+                                      (17, 4097, 1), (18, 8192, 2)])
 def test_v2_random_matches_oracle(ctx, seed, N, R):
     """N <= 16: replay_v2_rows_kernel<16> (four replications per wavefront, R not
     a multiple of four included); 17 <= N <= 32: replay_v2_rows_kernel<32> (two);
     N > 32: replay_v2_kernel<NPL> with node j on lane j % 64, slot j / 64 (NPL = 1,
-    2, 4, 8, 16, 32, 64: N <= 4096; the reference's loop takes any brokers.size(),
+    2, 4, 8, 16, 32, 64, 128: N <= 8192; the reference's loop takes any brokers.size(),
     BrokerBaseApp2.cc:241-248).  Every node's 10-ms timer fires throughout, so the
     wider node sets take shorter traces."""
-    tr, broker, stop, rt = v2_random(seed, R, N, 3000 if N <= 256 else 1500 if N <= 1024 else 400 if N <= 2048 else 200)
+    tr, broker, stop, rt = v2_random(seed, R, N, 3000 if N <= 256 else 1500 if N <= 1024 else 400 if N <= 2048 else
+                                     200 if N <= 4096 else 120)
     g = run_v2_gpu(ctx, tr, broker, stop, rt, qcap=4096)
     o = ol.run_v2(tr["arrive"], tr["req"], broker, tr["mips"], tr["dl"], tr["ul"], tr["first_adv"], stop, rt,
                   threads=8)
@@ -1165,12 +1167,14 @@ def test_v2_random_matches_oracle(ctx, seed, N, R):
     assert_v2_parity(g, o)
 
 
-def test_v2_widest_node_set_reserves_on_high_slots(ctx):
-    """N = 4096 (replay_v2_kernel<64>: 64 nodes per lane, per-node records in scratch) with R = 4 and
-    traces long enough for reservations, rejections and releases on the high slots: node 0 advertises
-    the smallest MIPS, so BrokerBaseApp2's "last node whose MIPS exceeds node 0's" (BrokerBaseApp2.cc:
-    241-248) lands at j >= 2048.  Equal to the oracle DES."""
-    R, N, T = 4, 4096, 400
+@pytest.mark.parametrize("N,T", [(4096, 400), (8192, 200)])
+def test_v2_widest_node_set_reserves_on_high_slots(ctx, N, T):
+    """N = 4096 (replay_v2_kernel<64>: 64 nodes per lane, per-node records in scratch) and N = 8192
+    (replay_v2_kernel<128>: the slot masks take 128 bits) with R = 4 and traces long enough for
+    reservations, rejections and releases on the high slots: node 0 advertises the smallest MIPS, so
+    BrokerBaseApp2's "last node whose MIPS exceeds node 0's" (BrokerBaseApp2.cc:241-248) lands at
+    j >= N / 2 (slots past 64 at N = 8192).  Equal to the oracle DES."""
+    R = 4
     tr, broker, stop, rt = v2_random(61, R, N, T)
     tr["mips"][:, 0] = 500
     tr["mips"][:, -64:] = 1500  # the last few nodes beat node 0 in every replication
@@ -1182,7 +1186,7 @@ def test_v2_widest_node_set_reserves_on_high_slots(ctx):
     assert (o["stats"]["status"] == 0).all()
     assert_v2_parity(g, o)
     fwd = g["node"][np.isin(g["status"], [_abi.V2_ST_ACCEPTED, _abi.V2_ST_REJECTED])]
-    assert fwd.size > 0 and fwd.min() >= 2048
+    assert fwd.size > 0 and fwd.min() >= N // 2
     assert (g["stats"]["n_accepted"] > 0).all() and (g["stats"]["n_released_node"] > 0).all()
 
 
@@ -1286,7 +1290,7 @@ def test_v2_errors(ctx):
               first_adv=np.zeros(0, np.int64))
     g = run_v2_gpu(ctx, tr, 100, 100 * MS)
     assert int(g["stats"]["status"][0]) == _abi.FOGNET_ERR_STATE
-    n = _abi.V2_MAX_NODES + 1  # (64 nodes per lane)
+    n = _abi.V2_MAX_NODES + 1  # (128 nodes per lane)
     big = dict(arrive=np.array([[10 * MS]]), req=np.array([[1]], np.int32), mips=np.full(n, 1000, np.int32),
                dl=np.ones(n, np.int64), ul=np.ones(n, np.int64), first_adv=np.ones(n, np.int64))
     with pytest.raises(fa.FognetError) as e:
