@@ -187,6 +187,13 @@ bool use_regions() {
   return f == nullptr || strcmp(f, "0") != 0;
 }
 bool regions_auto() { return getenv("FOGNET_HIER_REGIONS") == nullptr; }
+// FOGNET_HIER_RESUME=0: an escalated replication is replayed by the sequential kernel from the
+// start (and the automatic mode below chooses between the two paths); default: it continues from
+// its first escalated publish (replay_region.hip)
+bool use_resume() {
+  const char* f = getenv("FOGNET_HIER_RESUME");
+  return f == nullptr || strcmp(f, "0") != 0;
+}
 // automatic mode: after a region pass that handed most replications over, this many launches go
 // straight to the sequential replay before a region pass measures again
 constexpr int kHierReprobe = 15;
@@ -466,8 +473,11 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     const int32_t B = (a.N + FOGNET_HIER_REGION_NODES - 1) / FOGNET_HIER_REGION_NODES;
     const bool hier_split = a.policy == FOGNET_POLICY_EXT_HIER && !a.down && !stats_only && a.T > 0 && B >= 2;
     bool regions = hier_split && use_regions();
+    // resume (replay_region.hip): an escalated replication continues on the sequential kernel from
+    // its first escalated publish, so the region pass is never wasted and is always taken
+    const bool resume = regions && use_resume();
     const fognet_ctx::HierShape shape{a.R, a.T, a.N, stream};
-    if (regions && regions_auto()) {
+    if (regions && regions_auto() && !resume) {
       // the last region pass's hand-over count, if it has reached the host (never waited for)
       if (c->hier_pending && hipEventQuery(c->hier_ev) == hipSuccess) {
         c->hier_pending = false;
@@ -487,19 +497,22 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
     if (regions) {
       // one wavefront per (replication, region) while no region escalates (replay_region.hip), the
       // statistics pass, then the sequential wide kernel for the replications some region handed back.
-      // workspace: [hand-over counter | list [R] | quit flags [R] | region records [R][B] | segment offsets
-      // [R][B+1] | dispatch keys [R][B] | dispatch order [R*B] | node tails [R][N][2] | entries [R][T] | node records [R][N] | busy view [R][B][1024] | region-sorted trace and
-      // outputs [R][T]]; the hand-over launch reuses the space from the entries on (stream order: after the
-      // finish kernel has read the node records and the sorted outputs), with one workspace slot per
-      // handed-over replication up to kWideFallbackSlots (an escalation-heavy job replays its hand-overs
-      // side by side, as the sequential-only path does)
+      // workspace: [hand-over counter | list [R] | first escalations [R] | region records [R][B] | segment
+      // offsets [R][B+1] | dispatch keys [R][B] | dispatch order [R*B] | resume records [R] | node tails
+      // [R][N][2] | entries [R][T] | node records [R][N] | busy view [R][B][1024] | region-sorted trace and
+      // outputs [R][T] | sorted -> trace index [R][T]] + the hand-over launch's space, after it (resume: the
+      // wide kernel reads the region state), else from the entries on (stream order: after the finish
+      // kernel has read the node records and the sorted outputs), with one workspace slot per handed-over
+      // replication up to kWideFallbackSlots (an escalation-heavy job replays its hand-overs side by side,
+      // as the sequential-only path does)
       const size_t RT = (size_t)a.R * (size_t)a.T;
-      const size_t o_quit = align256(256 + (size_t)a.R * sizeof(int32_t));
-      const size_t o_rec = o_quit + align256((size_t)a.R * sizeof(int32_t));
+      const size_t o_esc = align256(256 + (size_t)a.R * sizeof(int32_t));
+      const size_t o_rec = o_esc + align256((size_t)a.R * sizeof(int32_t));
       const size_t o_seg = o_rec + align256((size_t)a.R * (size_t)B * sizeof(fognet::RegionRec));
       const size_t o_ok = o_seg + align256((size_t)a.R * (size_t)(B + 1) * sizeof(int32_t));
       const size_t o_perm = o_ok + align256((size_t)a.R * (size_t)B * sizeof(uint32_t));
-      const size_t o_tails = o_perm + align256((size_t)a.R * (size_t)B * sizeof(int32_t));
+      const size_t o_pacc = o_perm + align256((size_t)a.R * (size_t)B * sizeof(int32_t));
+      const size_t o_tails = o_pacc + align256((size_t)a.R * fognet::kRegionResumeBytes);
       const size_t o_e = o_tails + align256((size_t)a.R * (size_t)a.N * 2 * sizeof(int64_t));
       const size_t o_nd = o_e + align256(RT * sizeof(fognet::WideEntry));
       const size_t o_vb = o_nd + align256((size_t)a.R * (size_t)a.N * sizeof(fognet::WideNode));
@@ -510,24 +523,28 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       const size_t o_os = o_on + align256(RT * sizeof(int32_t));
       const size_t o_ost = o_os + align256(RT);
       const size_t o_od = o_ost + align256(RT * sizeof(int64_t));
-      const size_t body = o_od + RT * sizeof(int64_t) - o_e;
+      const size_t o_sidx = o_od + align256(RT * sizeof(int64_t));
+      const size_t body = o_sidx + align256(RT * sizeof(int32_t)) - o_e;
       const int32_t slots = a.R < kWideFallbackSlots ? a.R : kWideFallbackSlots;
       const size_t fb = fognet::replay_wide_workspace_bytes(slots, a.T, a.N, false, a.policy);
-      rc = ensure(c, (void**)&c->ring, &c->ring_bytes, o_e + (body > fb ? body : fb), "region replay workspace");
+      const size_t o_wide = resume ? o_e + body : o_e;
+      const size_t total = resume ? o_wide + fb : o_e + (body > fb ? body : fb);
+      rc = ensure(c, (void**)&c->ring, &c->ring_bytes, total, "region replay workspace");
       if (rc) return rc;
       unsigned char* const base = reinterpret_cast<unsigned char*>(c->ring);
       a.wide_count = reinterpret_cast<int32_t*>(base);
       a.wide_list = reinterpret_cast<int32_t*>(base + 256);
       e = hipMemsetAsync(a.wide_count, 0, sizeof(int32_t), (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(c, e, "hand-over counter");
-      e = hipMemsetAsync(base + o_quit, 0, (size_t)a.R * sizeof(int32_t), (hipStream_t)stream);
-      if (e != hipSuccess) return hip_fail(c, e, "region quit flags");
       fognet::RegionWs w;
       w.e = reinterpret_cast<fognet::WideEntry*>(base + o_e);
       w.nd = reinterpret_cast<fognet::WideNode*>(base + o_nd);
       w.rec = reinterpret_cast<fognet::RegionRec*>(base + o_rec);
       w.vb = reinterpret_cast<uint32_t*>(base + o_vb);
-      w.quit = reinterpret_cast<int32_t*>(base + o_quit);
+      w.esc = reinterpret_cast<int32_t*>(base + o_esc);  // (set by the sort kernel)
+      w.s_idx = reinterpret_cast<int32_t*>(base + o_sidx);
+      w.pacc = base + o_pacc;
+      w.pass = 1;
       w.seg = reinterpret_cast<int32_t*>(base + o_seg);
       w.okey = reinterpret_cast<uint32_t*>(base + o_ok);
       w.perm = reinterpret_cast<int32_t*>(base + o_perm);
@@ -541,12 +558,12 @@ static int stage(fognet_ctx* c, const fognet_batch_in* in, fognet_batch_out* out
       w.o_done = reinterpret_cast<int64_t*>(base + o_od);
       w.B = B;
       if (regions_only()) a.wide_list = nullptr;
-      e = fognet::launch_replay_region(a, w, (hipStream_t)stream);
+      e = fognet::launch_replay_region(a, w, resume && !regions_only(), (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(c, e, "region replay launch");
       if (regions_only()) return FOGNET_OK;
-      e = fognet::launch_replay_wide(a, base + o_e, slots, (hipStream_t)stream);
+      e = fognet::launch_replay_wide(a, base + o_wide, slots, (hipStream_t)stream, resume ? &w : nullptr);
       if (e != hipSuccess) return hip_fail(c, e, "wide hand-over launch");
-      if (regions_auto() && !c->hier_pending) {  // the hand-over count back to the host, asynchronously
+      if (regions_auto() && !resume && !c->hier_pending) {  // the hand-over count back to the host, asynchronously
         // (while a measurement is in flight, later launches are not measured: its pinned slot and event
         // stay paired with the launch that issued them)
         if (!c->hier_host && hipHostMalloc((void**)&c->hier_host, sizeof(int32_t), hipHostMallocDefault) != hipSuccess)

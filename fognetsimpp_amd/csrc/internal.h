@@ -344,11 +344,6 @@ size_t replay_wide_lds_bytes(int32_t N);
 // workspace: R*T WideEntry followed by R*N WideNode
 // (+ R*N generated node parameters in generated mode, + the HBM group minima above kWideMaxNodes)
 size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen, int policy);
-// slots: workspace slots (workgroups).  With a.wide_list unset, slots == R and
-// workgroup r replays replication r; with it set, the workgroups take the
-// listed replications in turn (slots <= R bounds the workspace).
-hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slots, hipStream_t s);
-
 // FOGNET_POLICY_EXT_HIER by region (replay_region.hip): one wavefront per
 // (replication, region) over the region's publishes while no escalation occurs;
 // then per replication the regions' records merged and the statistics pass, or
@@ -361,8 +356,17 @@ struct RegionWs {
   WideNode* nd;    // [R][N]
   RegionRec* rec;  // [R][B]
   uint32_t* vb;    // [R][B][16][64] advertised busy times (the region kernel's view, [slot][lane])
-  int32_t* quit;   // [R] zeroed before the launch: set when a region of r hands it back (or the trace is
-                   // invalid), so r's other region wavefronts stop early (the sequential kernel replays r)
+  // [R] the replication's first escalated publish (trace index), lowered by every region that meets
+  // one (atomic min); set to T by the sort kernel, 0 for anything the sequential kernel must replay
+  // from the start (an invalid trace, a saturated view, a service time past the pass's range).  A
+  // region wavefront of the first pass stops once its publishes are past it.
+  int32_t* esc;
+  int32_t* s_idx;  // [R][T] trace index of sorted position p (inv's inverse)
+  unsigned char* pacc;  // [R][kRegionResumeBytes] the statistics of the publishes before esc (finish kernel)
+  // 1: every replication, up to its first escalation (found on the way); 2: the escalated
+  // replications again, each region exactly up to esc (a first-pass wavefront may have run past
+  // it), so that the sequential wide kernel continues from that state (resume)
+  int32_t pass;
   int32_t* seg;    // [R][B + 1] region b's publishes are sorted positions [seg[b], seg[b + 1])
   int64_t* s_arr;  // [R][T] publish ticks, region-sorted (stable: trace order within a region)
   int32_t* s_req;  // [R][T] MIPSRequired, region-sorted
@@ -378,7 +382,18 @@ struct RegionWs {
   int32_t* perm;   // [R * B] the region wavefronts' dispatch order: lightest estimated load first (region_order_kernel)
   int32_t B;       // regions: ceil(N / FOGNET_HIER_REGION_NODES)
 };
-hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s);
+// sort + order + the first region pass; resume: + the second pass over the escalated replications;
+// then the finish kernel (statistics, hand-over list)
+hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, bool resume, hipStream_t s);
+constexpr size_t kRegionResumeBytes = 192;  // >= sizeof(Acc) + sizeof(AbortPt) (replay_common.h)
+
+// slots: workspace slots (workgroups).  With a.wide_list unset, slots == R and
+// workgroup r replays replication r; with it set, the workgroups take the
+// listed replications in turn (slots <= R bounds the workspace).  rw (EXT_HIER,
+// nullable): the region pass's workspace; a listed replication with 0 < rw->esc[r] < T
+// continues from the second pass's state at its first escalated publish.
+hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slots, hipStream_t s,
+                              const RegionWs* rw = nullptr);
 
 hipError_t launch_replay(const ReplayArgs& a, hipStream_t s);
 hipError_t launch_rep_stats(const ReplayArgs& a, hipStream_t s);

@@ -25,11 +25,17 @@
 //   * region_finish_kernel merges the regions' records, writes the outputs back
 //     in trace order and runs the statistics pass (the same Acc record,
 //     histogram and a11 energy as the wide kernel's inline statistics).
-// A replication in which any region meets an escalation (or anything else this
-// pass does not model: a saturated busy time, a service time past 2^22 s, an
-// invalid input) is replayed again from the start by the sequential wide
-// kernel (the hand-over list, like the register kernel's), which defines every
-// result of such a replication; nothing of this pass survives for it.
+// A replication in which a region meets an escalation is continued by the
+// sequential wide kernel from the publish that escalates (resume): the first
+// pass finds each replication's first escalated publish (every region stops once
+// its publishes are past the earliest found so far), a second pass replays the
+// escalated replications again with each region stopping exactly before it (a
+// first-pass wavefront may have run past it), the finish kernel completes the
+// publishes before it, and the wide kernel takes over that state (its node
+// records, chains and views, replay_wide.hip).  Anything else this pass does not
+// model (a saturated busy time, a service time past 2^22 s, an invalid input)
+// hands the replication to the wide kernel from the start, as does
+// FOGNET_HIER_RESUME=0 for every escalated one.
 #include "replay_common.h"
 
 namespace fognet {
@@ -49,7 +55,7 @@ constexpr uint32_t kRegWCap = 0xFFFFu;
 // (fognet_hip.h never returns it; under FOGNET_HIER_REGIONS=only the finish kernel
 // reports FOGNET_ERR_UNSUPPORTED instead).
 constexpr int32_t kRegionSeq = 0x53455121;
-constexpr int kQuitEvery = 4;  // chunks between polls of the replication's quit flag
+constexpr int kQuitEvery = 4;  // chunks between polls of the replication's first escalation (W.esc)
 
 // ---- region_sort_kernel: stable counting sort of one replication's publishes by region (one block)
 constexpr int kSortThreads = 1024;  // (a replication's 10,000 publishes in 10 tiles)
@@ -98,8 +104,9 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
   if (bad) s_bad = 1;
   __syncthreads();
   int32_t* const seg = W.seg + (size_t)r * (size_t)(B + 1);
+  // (no escalation found yet; an invalid trace: the sequential kernel replays r from the start)
+  if (tid == 0) __hip_atomic_store(W.esc + r, s_bad ? 0 : T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (s_bad) {
-    if (tid == 0) __hip_atomic_store(W.quit + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the dispatch inputs stay defined: empty segments, dispatched last
     if (tid <= B) seg[tid] = 0;
     if (tid < B) W.okey[(size_t)r * B + tid] = 255u;
@@ -139,6 +146,7 @@ __global__ __launch_bounds__(kSortThreads) void region_sort_kernel(ReplayArgs A,
       uint32_t pos = s_cnt[g] + rank;
       for (int w = 0; w < wv; ++w) pos += s_wc[w][g];
       W.inv[tbase + i] = (int32_t)pos;
+      W.s_idx[tbase + pos] = i;
       W.s_arr[tbase + pos] = A.arrive[tbase + i];
       W.s_req[tbase + pos] = A.req[tbase + i];
     }
@@ -233,10 +241,26 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   };
   const int32_t* const seg = W.seg + (size_t)r * (size_t)(B + 1);
   const int64_t arrive0 = T > 0 ? A.arrive[tbase] : kNever;
-  uint32_t err = __hip_atomic_load(W.quit + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0
-                     ? (uint32_t)kRegionSeq : (uint32_t)FOGNET_OK;  // (an invalid trace: see the sort)
+  const int32_t esc0 = __hip_atomic_load(W.esc + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the second pass replays only the replications the first found an escalation in (0 < esc < T);
+  // the others keep the first pass's state and records
+  if (W.pass == 2 && (esc0 <= 0 || esc0 >= T)) return;
+  // esc 0: an invalid trace (see the sort) or another region's failure: the sequential kernel replays r
+  uint32_t err = esc0 == 0 ? (uint32_t)kRegionSeq : (uint32_t)FOGNET_OK;
   const int s0 = err == FOGNET_OK ? seg[b] : 0;
-  const int nseg = err == FOGNET_OK ? seg[b + 1] - s0 : 0;  // this region's publishes
+  int nseg = err == FOGNET_OK ? seg[b + 1] - s0 : 0;  // this region's publishes
+  if (W.pass == 2) {  // those before the escalated publish: a prefix of the segment (trace order)
+    int lo = 0, hi = nseg;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (W.s_idx[tbase + s0 + mid] < esc0) lo = mid + 1;
+      else hi = mid;
+    }
+    nseg = lo;
+  }
+  // the first pass's finding for W.esc: the escalated publish's trace index, 0 for a failure the
+  // sequential kernel must replay from the start, -1 none (or a stop at another region's escalation)
+  int32_t esc_hit = -1;
 
   // ---- this lane's nodes (local l = s * 64 + lane) and their view ([slot][lane]: each lane
   // touches only its own column): next advert ticks and run-horizon offsets in LDS
@@ -308,7 +332,10 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
     }
   };
 
-  if (ballot(bad)) err = kRegionSeq;
+  if (ballot(bad)) {
+    err = kRegionSeq;
+    esc_hit = 0;
+  }
   uint32_t max_pend = 0u;
   int n_done = 0;
   // the node this lane pushed to last (the stale view keeps choosing it): its
@@ -353,9 +380,10 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
 #endif
 
   for (int c0 = 0; c0 < nseg && err == FOGNET_OK; c0 += kWave) {
-    // another region of r handed it back: the sequential kernel replays r from the start
-    if ((c0 & (kQuitEvery * kWave - 1)) == 0 && c0 > 0 &&
-        __hip_atomic_load(W.quit + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+    // first pass: this region's publishes are past r's first escalation found so far (another
+    // region's, or 0 for a failure), so nothing it decides from here on matters
+    if (W.pass == 1 && (c0 & (kQuitEvery * kWave - 1)) == 0 && c0 > 0 &&
+        W.s_idx[tbase + s0 + c0] >= __hip_atomic_load(W.esc + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
       err = kRegionSeq;
       break;
     }
@@ -421,6 +449,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
         }
         if (ballot(lbroken)) {
           err = FOGNET_ERR_INTERNAL;
+          esc_hit = 0;
           break;
         }
         PRT(8)
@@ -431,6 +460,8 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
         }
         if ((key >> 32) > (uint64_t)A.hier_thr || (key >> 32) >= kRegBusySat) {
           err = kRegionSeq;
+          // an escalation (publish s0 + c0 + jp), or a saturated view (the sequential kernel refuses it)
+          esc_hit = (key >> 32) >= kRegBusySat ? 0 : W.s_idx[tbase + s0 + c0 + jp];
           break;
         }
       }
@@ -506,6 +537,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
       // tick range (the wide kernel's kPastRange): the sequential kernel decides the replication
       if (ballot(in_run && (Cs >= kRegSCap || a > kMaxTick))) {
         err = kRegionSeq;
+        esc_hit = 0;
         break;
       }
       int64_t X = in_run ? a - ticks_of(Cs - S) : INT64_MIN;
@@ -515,6 +547,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
       const int64_t done = dmax + ticks_of(Cs);
       if (ballot(in_run && done > kMaxTick)) {
         err = kRegionSeq;
+        esc_hit = 0;
         break;
       }
       int64_t prev_done = base_done;
@@ -610,7 +643,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
 #endif
   const uint32_t mp = ~wave_min_u32(~max_pend);
   if (lane == 0) {
-    if (err != FOGNET_OK) __hip_atomic_store(W.quit + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (W.pass == 1 && esc_hit >= 0) atomicMin(W.esc + r, esc_hit);
     W.rec[rb] = RegionRec{n_done, (int32_t)mp, (int32_t)err, 0};
   }
 }
@@ -654,15 +687,20 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
     }
   }
   __syncthreads();
-  if (!s_ok) {  // the sequential replay overwrites the record
+  // resume (second pass run): the second pass replayed r up to its first escalated publish esc;
+  // the publishes before it are finished here, and the sequential kernel continues from esc
+  const int32_t esc = W.esc[r];
+  const bool part = W.pass == 2 && A.wide_list && esc > 0 && esc < A.T;
+  if (!s_ok || (part && s_done != esc)) {  // the sequential replay overwrites the record
     if (tid == 0) {
       // (FOGNET_HIER_REGIONS=only: no hand-over list, the replication stays unreplayed)
       A.out_stats[r].status = A.wide_list ? kRegionSeq : FOGNET_ERR_UNSUPPORTED;
+      if (W.pass == 2) W.esc[r] = 0;  // from the start
       if (A.wide_list) A.wide_list[atomicAdd(A.wide_count, 1)] = r;
     }
     return;
   }
-  const int n = s_done;  // == T
+  const int n = s_done;  // == T, or esc (part)
   fognet_rep_stats* const S = A.out_stats + r;
   const size_t nbase = (size_t)r * (size_t)A.node_stride;
   const size_t tbase = (size_t)r * (size_t)A.T;
@@ -705,8 +743,9 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
   if (tid < kWave) {
     // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12), summed in
     // node order (64 nodes at a time, then lane by lane) while waves 1-3 run the statistics pass
+    // (part: the sequential kernel sums it at the end)
 #ifndef FOGNET_FIN_NOENERGY
-    if (A.p_busy) {  // (an unused node's record has tl_C = 0)
+    if (A.p_busy && !part) {  // (an unused node's record has tl_C = 0)
 #else
     if (false) {  // timing probe only
 #endif
@@ -790,12 +829,21 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
     }
     t.busy = s_busy;  // (the node tails': the statistics pass adds none)
     t.last = s_last;
-    S->n_tasks = n;
-    S->max_pending = s_mp;
-    S->status = FOGNET_OK;
-    S->events = 2 * (int64_t)N + 4 * (int64_t)n;  // initial adverts + publish, arrival, release, advert per task
-    write_rep_stats(S, t, ab, A.ref_abort);
-    if (A.p_busy) S->energy_j = s_energy;
+    if (part) {  // the publishes before esc: the record the sequential kernel starts from
+      static_assert(sizeof(Acc) + sizeof(AbortPt) <= kRegionResumeBytes, "resume record");
+      unsigned char* const pr = W.pacc + (size_t)r * kRegionResumeBytes;
+      *reinterpret_cast<Acc*>(pr) = t;
+      *reinterpret_cast<AbortPt*>(pr + sizeof(Acc)) = ab;
+      S->status = kRegionSeq;
+      A.wide_list[atomicAdd(A.wide_count, 1)] = r;
+    } else {
+      S->n_tasks = n;
+      S->max_pending = s_mp;
+      S->status = FOGNET_OK;
+      S->events = 2 * (int64_t)N + 4 * (int64_t)n;  // initial adverts + publish, arrival, release, advert per task
+      write_rep_stats(S, t, ab, A.ref_abort);
+      if (A.p_busy) S->energy_j = s_energy;
+    }
   }
   if (A.hist) {
     for (int h = tid; h < FOGNET_HIST_METRICS * FOGNET_HIST_BINS; h += kFinThreads)
@@ -805,17 +853,26 @@ __global__ __launch_bounds__(kFinThreads) void region_finish_kernel(ReplayArgs A
 
 }  // namespace
 
-hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, hipStream_t s) {
-  hipLaunchKernelGGL(region_sort_kernel, dim3(a.R), dim3(kSortThreads), 0, s, a, w);
+hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, bool resume, hipStream_t s) {
+  RegionWs w1 = w;
+  w1.pass = 1;
+  hipLaunchKernelGGL(region_sort_kernel, dim3(a.R), dim3(kSortThreads), 0, s, a, w1);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(region_order_kernel, dim3(1), dim3(kOrderThreads), 0, s, (int32_t)(a.R * w.B), w);
+  hipLaunchKernelGGL(region_order_kernel, dim3(1), dim3(kOrderThreads), 0, s, (int32_t)(a.R * w.B), w1);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w);
+  hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w1);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(region_finish_kernel, dim3(a.R), dim3(kFinThreads), 0, s, a, w);
+  RegionWs w2 = w;
+  w2.pass = resume ? 2 : 1;  // (the finish kernel: whether the second pass ran)
+  if (resume) {  // the escalated replications again, each region exactly up to the first escalation
+    hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w2);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(region_finish_kernel, dim3(a.R), dim3(kFinThreads), 0, s, a, w2);
   return hipGetLastError();
 }
 

@@ -325,7 +325,7 @@ struct GenNodes {
 template <int POL, bool BIG>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
                                                 int64_t* VN, uint32_t* VB, int64_t* VW, GenNodes GN, int32_t* OV,
-                                                unsigned char* GX, unsigned char* w_lds);
+                                                unsigned char* GX, const RegionWs& RW, unsigned char* w_lds);
 
 // One replication per workgroup (r = blockIdx.x), or, with A.wide_list set,
 // the replications the register kernel handed over, taken in turn by the
@@ -334,15 +334,15 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 template <int POL, bool BIG>
 __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry* E, WideNode* ND, int64_t* VN,
                                                          uint32_t* VB, int64_t* VW, GenNodes GN, int32_t* OV,
-                                                         unsigned char* GX) {
+                                                         unsigned char* GX, RegionWs RW) {
   extern __shared__ __align__(16) unsigned char w_lds[];
   if (A.wide_list == nullptr) {
-    replay_wide_rep<POL, BIG>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, VW, GN, OV, GX, w_lds);
+    replay_wide_rep<POL, BIG>(A, blockIdx.x, blockIdx.x, E, ND, VN, VB, VW, GN, OV, GX, RW, w_lds);
     return;
   }
   const int n = *A.wide_count;
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
-    replay_wide_rep<POL, BIG>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, VW, GN, OV, GX, w_lds);
+    replay_wide_rep<POL, BIG>(A, A.wide_list[i], blockIdx.x, E, ND, VN, VB, VW, GN, OV, GX, RW, w_lds);
     __syncthreads();  // LDS reuse by the next replication
   }
 }
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(64) void replay_wide_kernel(ReplayArgs A, WideEntry
 template <int POL, bool BIG>
 __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int wr, WideEntry* E, WideNode* ND,
                                                 int64_t* VN, uint32_t* VB, int64_t* VW, GenNodes GN, int32_t* OV,
-                                                unsigned char* GX, unsigned char* w_lds) {
+                                                unsigned char* GX, const RegionWs& RW, unsigned char* w_lds) {
   constexpr bool kExt = POL == FOGNET_POLICY_EXT_LAT;
   constexpr bool kHier = POL == FOGNET_POLICY_EXT_HIER;
   static_assert(!(BIG && kHier), "EXT_HIER keeps its regions (groups) in LDS");
@@ -469,6 +469,75 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   int n_short = 0;         // tasks of this lane's nodes that never complete (node-down)
   int64_t prev_t = INT64_MIN;
   int n_done = 0;
+  // ---- EXT_HIER resume (replay_region.hip): a replication whose first escalated publish esc the
+  // region passes found continues from the second pass's state there -- node records and
+  // chains (sorted positions renamed to trace indices), advertised busy views, the finish
+  // kernel's statistics record of the publishes before esc -- at publish esc, as if this kernel
+  // had replayed them (until esc every decision is its region's, made from its region's view)
+  int c_first = 0;
+  if constexpr (kHier) {
+    const int32_t esc = RW.esc != nullptr && !gen ? RW.esc[r] : 0;
+    if (esc > 0 && esc < T && err == FOGNET_OK) {
+      c_first = esc;
+      const int32_t* const sidx = RW.s_idx + tbase;
+      auto ren = [&](int32_t x) -> int32_t { return x < 0 || x >= T ? x : sidx[x]; };
+      const WideEntry* const re = RW.e + tbase;
+      for (int p = lane; p < T; p += kWave) {  // the entries of the publishes before esc
+        const int32_t i = sidx[p];
+        if (i < esc) {
+          WideEntry x = re[p];
+          x.prev = ren(x.prev);
+          x.next = ren(x.next);
+          e[i] = x;
+        }
+      }
+      const WideNode* const rn = RW.nd + (size_t)r * (size_t)N;
+      const uint32_t* const rvb = RW.vb + (size_t)r * (size_t)RW.B * FOGNET_HIER_REGION_NODES;
+      for (int sj = 0; sj < SP; ++sj) {  // this lane's nodes: records and views
+        const int j = wnode<kHier>(sj, lane);
+        if (j >= N) continue;
+        WideNode h = rn[j];
+        h.hd = ren(h.hd);
+        h.tl = ren(h.tl);
+        h.hd_next = ren(h.hd_next);
+        nd[j] = h;
+        V.nxt[sj] = h.npend > 0 && h.hd_done != kNever ? h.hd_done + P_ul[j] : kNever;
+        V.busy[sj] = rvb[j];  // (region j / 1024, its node j % 1024 at [slot][lane] = j % 1024)
+      }
+      for (int g = 0; g < L.G; ++g) {  // the group minima (regions) from the lane's views
+        int64_t gmn = kNever;
+        int gsi = 0;
+        uint32_t gm = 0u;
+        for (int i = 0; i < kWideGroupSlots; ++i) {
+          const int64_t x = V.nxt[g * kWideGroupSlots + i];
+          gm |= (x != kNever ? 1u : 0u) << i;
+          gm |= (V.busy[g * kWideGroupSlots + i] != 0u ? 1u : 0u) << (16 + i);
+          if (x < gmn) {
+            gmn = x;
+            gsi = i;
+          }
+        }
+        L.g_nxt[g * kWave + lane] = gmn;
+        L.g_j[g * kWave + lane] = wnode<kHier>(g * kWideGroupSlots + (gmn == kNever ? 0 : gsi), lane);
+        L.g_msk[g * kWave + lane] = gm;
+        L.g_key[g * kWave + lane] = group_key<kHier>(V, lane, g);
+        gact.set(g, (gm & 0xFFFFu) != 0u);
+      }
+      if (lane == 0) {
+        const unsigned char* const pr = RW.pacc + (size_t)r * kRegionResumeBytes;
+        acc = *reinterpret_cast<const Acc*>(pr);
+        ab = *reinterpret_cast<const AbortPt*>(pr + sizeof(Acc));
+      }
+      const uint32_t mp_b = lane < RW.B ? (uint32_t)RW.rec[(size_t)r * RW.B + lane].max_pend : 0u;
+      const uint32_t mp_r = ~wave_min_u32(~mp_b);  // (all lanes: a cross-lane reduction)
+      max_pend = lane == 0 ? mp_r : 0u;
+      n_done = esc;
+      prev_t = A.arrive[tbase + esc - 1];
+      __threadfence_block();
+      __syncthreads();  // (the entries and records written above are read by their nodes' lanes)
+      lane_min(L, lane, mn, mj, mk);
+    }
+  }
   // the node this lane pushed to last: under the stale view the broker keeps
   // choosing it, so its record and parameters stay in registers between
   // pushes; nd[cj] in HBM is stale until the record is written back (when
@@ -711,7 +780,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   bool glob_valid = false;
 
   int64_t gen_t0 = 0;  // generated EXT_HIER: the first publish's tick (the mobility model's origin)
-  for (int c0 = 0; c0 < T && err == FOGNET_OK; c0 += kWave) {
+  for (int c0 = c_first; c0 < T && err == FOGNET_OK; c0 += kWave) {
     const int cnt = min(kWave, T - c0);
     const bool live = lane < cnt;
     // this chunk's pushed tasks, one per lane (publish c0 + lane): their
@@ -1279,12 +1348,13 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
 
 template <int POL, bool BIG>
 void launch_wide_pol(const ReplayArgs& a, int32_t slots, WideEntry* e, WideNode* nd, int64_t* vn, uint32_t* vb,
-                     int64_t* vw, GenNodes gn, int32_t* ov, unsigned char* gx, size_t lds, hipStream_t s) {
+                     int64_t* vw, GenNodes gn, int32_t* ov, unsigned char* gx, const RegionWs& rw, size_t lds,
+                     hipStream_t s) {
   if (lds > 65536)  // above the default dynamic-LDS limit (N > ~51,000 nodes; gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&replay_wide_kernel<POL, BIG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((replay_wide_kernel<POL, BIG>), dim3(slots), dim3(kWave), lds, s, a, e, nd, vn, vb, vw, gn, ov,
-                     gx);
+                     gx, rw);
 }
 
 // FOGNET_WIDE_BIG=1: the HBM group minima at any N (the flat policies; parity tests of both layouts)
@@ -1318,7 +1388,9 @@ size_t replay_wide_workspace_bytes(int32_t R, int32_t T, int32_t N, bool gen, in
   return wide_ws(R, T, N, gen, wide_big_for(N, policy)).bytes;
 }
 
-hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slots, hipStream_t s) {
+hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slots, hipStream_t s, const RegionWs* rwp) {
+  RegionWs rw{};  // (esc null: every listed replication starts from the beginning)
+  if (rwp && a.policy == FOGNET_POLICY_EXT_HIER) rw = *rwp;
   const bool big = wide_big_for(a.N, a.policy);
   const WideWs w = wide_ws(slots, a.T, a.N, a.gen_on != 0, big);
   unsigned char* const base = static_cast<unsigned char*>(workspace);
@@ -1334,15 +1406,15 @@ hipError_t launch_replay_wide(const ReplayArgs& a, void* workspace, int32_t slot
   const size_t lds = wide_lds_bytes(a.N, big);
   if (a.policy == FOGNET_POLICY_EXT_LAT) {
     if (big)
-      launch_wide_pol<FOGNET_POLICY_EXT_LAT, true>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, lds, s);
+      launch_wide_pol<FOGNET_POLICY_EXT_LAT, true>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, rw, lds, s);
     else
-      launch_wide_pol<FOGNET_POLICY_EXT_LAT, false>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, lds, s);
+      launch_wide_pol<FOGNET_POLICY_EXT_LAT, false>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, rw, lds, s);
   } else if (a.policy == FOGNET_POLICY_EXT_HIER) {
-    launch_wide_pol<FOGNET_POLICY_EXT_HIER, false>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, lds, s);
+    launch_wide_pol<FOGNET_POLICY_EXT_HIER, false>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, rw, lds, s);
   } else if (big) {
-    launch_wide_pol<FOGNET_POLICY_REF_V3, true>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, lds, s);
+    launch_wide_pol<FOGNET_POLICY_REF_V3, true>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, rw, lds, s);
   } else {
-    launch_wide_pol<FOGNET_POLICY_REF_V3, false>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, lds, s);
+    launch_wide_pol<FOGNET_POLICY_REF_V3, false>(a, slots, e, nd, vn, vb, vw, gn, ov, gx, rw, lds, s);
   }
   return hipGetLastError();
 }

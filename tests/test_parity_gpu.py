@@ -1454,9 +1454,11 @@ def test_hier_region_pass_and_handover(ctx, monkeypatch):
     while no region escalates) with the sequential hand-over: of six
     replications five never escalate (two regions, one of 6 nodes) and one does
     (297 escalated publishes in the oracle).  FOGNET_HIER_REGIONS=only shows the
-    region pass finishing exactly the five; the default (region pass + hand-over
-    of the sixth) and FOGNET_HIER_REGIONS=0 (sequential only) both equal the
-    oracle, records and job histogram included."""
+    region pass finishing exactly the five; the default (region pass + the sixth
+    continued by the sequential kernel from its first escalated publish), the
+    restart (FOGNET_HIER_RESUME=0: the sixth replayed from the start) and
+    FOGNET_HIER_REGIONS=0 (sequential only) all equal the oracle, records and job
+    histogram included."""
     tr = tg.make_batch(21, 6, 1030, 4000, rho=0.9)
     reg = np.zeros_like(tr["req"])
     reg[1::2, 1::2] = 1
@@ -1481,8 +1483,9 @@ def test_hier_region_pass_and_handover(ctx, monkeypatch):
     assert st[:5].tobytes() == o["stats"][:5].tobytes()
     np.testing.assert_array_equal(out.node_energy.cpu().numpy()[:5], o["node_energy"][:5])
     np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"][:5].sum(axis=0))
-    for mode in ("1", "0"):
-        monkeypatch.setenv("FOGNET_HIER_REGIONS", mode)
+    for mode in ("1", "1-restart", "0"):  # (1: the sixth resumed at its first escalated publish)
+        monkeypatch.setenv("FOGNET_HIER_REGIONS", mode.split("-")[0])
+        monkeypatch.setenv("FOGNET_HIER_RESUME", "0" if mode == "1-restart" else "1")
         out = fa.run_batch(ctx, d, **kw)
         torch.cuda.synchronize()
         g = dict(node=out.node.cpu().numpy(), status=out.status.cpu().numpy(), start=out.start_tick.cpu().numpy(),
@@ -1640,19 +1643,26 @@ def test_c5_saturated_trace_escalates_everywhere(c5_saturated):
     assert (o["stats"]["status"] == 0).all() and (o["stats"]["n_qtime_overflow"] == 0).all()
 
 
-@pytest.mark.parametrize("mode", ["1", "0", "only"])
+@pytest.mark.parametrize("mode", ["1", "1-restart", "0", "only"])
 def test_c5_ext_hier_escalations(ctx, monkeypatch, c5_saturated, mode):
     """EXT_HIER at the C5 topology WITH escalations: every
     output, record (a11 energy included), per-node energy and histogram bin
     against the oracle.  mode "1" (default): the region pass finishes the two
-    non-escalating replications and hands the six others to the sequential wide
-    kernel, which replays them from the start (regional argmin per region,
-    BrokerBaseApp3.cc:267-281; node FIFO of any length, ComputeBrokerApp3.cc:
-    305-309; escalated tasks of all ten rows); "0": the sequential kernel for all
-    eight; "only": the region pass alone -- the two finished replications equal
-    the oracle, the six others report FOGNET_ERR_UNSUPPORTED."""
+    non-escalating replications; the six others are replayed again by a second
+    region pass up to their first escalated publish (past publish 16,000 here),
+    whose state the sequential wide kernel continues from (resume: regional argmin
+    per region, BrokerBaseApp3.cc:267-281; node FIFO of any length,
+    ComputeBrokerApp3.cc:305-309; escalated tasks of all ten rows); "1-restart"
+    (FOGNET_HIER_RESUME=0): the sequential kernel replays the six from the start;
+    "0": the sequential kernel for all eight; "only": the region pass alone -- the
+    two finished replications equal the oracle, the six others report
+    FOGNET_ERR_UNSUPPORTED."""
     tr, o = c5_saturated
-    monkeypatch.setenv("FOGNET_HIER_REGIONS", mode)
+    monkeypatch.setenv("FOGNET_HIER_REGIONS", mode.split("-")[0])
+    if mode == "1-restart":
+        monkeypatch.setenv("FOGNET_HIER_RESUME", "0")
+    else:
+        monkeypatch.delenv("FOGNET_HIER_RESUME", raising=False)
     dev = torch.device("cuda", ctx.device)
     out = fa.run_batch(ctx, fa.as_device_trace(tr, dev), policy="EXT_HIER", hier_threshold_s=60,
                        hier_up_tick=20 * 10**9, hist=True)
@@ -1677,22 +1687,30 @@ def test_c5_ext_hier_escalations(ctx, monkeypatch, c5_saturated, mode):
     np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
 
 
-def test_c5_ext_hier_automatic_path(monkeypatch, c5_saturated):
-    """FOGNET_HIER_REGIONS unset (the default): the first launch takes the region
-    pass, which hands six of the eight replications over; once that count has
-    reached the host, the next launch goes straight to the sequential replay
-    (fognet_hier_path_stats); every output, record, per-node energy and histogram
-    equals the oracle on both launches.  A light C5 trace (no escalation) keeps the
-    region pass."""
+@pytest.mark.parametrize("resume", [True, False])
+def test_c5_ext_hier_automatic_path(monkeypatch, c5_saturated, resume):
+    """FOGNET_HIER_REGIONS unset (the default).  With resume (the default) every
+    launch takes the region pass: an escalated replication continues on the
+    sequential kernel from its first escalated publish, so the pass is never
+    wasted.  With FOGNET_HIER_RESUME=0 the first launch takes the region pass,
+    which hands six of the eight replications over; once that count has reached
+    the host, the next launch goes straight to the sequential replay
+    (fognet_hier_path_stats).  Every output, record, per-node energy and histogram
+    equals the oracle on both launches.  A light C5 trace (no escalation) keeps
+    the region pass."""
     tr, o = c5_saturated
     monkeypatch.delenv("FOGNET_HIER_REGIONS", raising=False)
+    if resume:
+        monkeypatch.delenv("FOGNET_HIER_RESUME", raising=False)
+    else:
+        monkeypatch.setenv("FOGNET_HIER_RESUME", "0")
     c = fa.Context(0)  # (a fresh context: the measurement is per context)
     dev = torch.device("cuda", c.device)
     d = fa.as_device_trace(tr, dev)
     for launch in range(2):
         out = fa.run_batch(c, d, policy="EXT_HIER", hier_threshold_s=60, hier_up_tick=20 * 10**9, hist=True)
         torch.cuda.synchronize()
-        assert c.hier_path_stats() == ((1, 0) if launch == 0 else (1, 1))
+        assert c.hier_path_stats() == ((1, 0) if launch == 0 else (2, 0) if resume else (1, 1))
         st = out.rep_stats()
         g = dict(node=out.node.cpu().numpy(), status=out.status.cpu().numpy(), start=out.start_tick.cpu().numpy(),
                  done=out.done_tick.cpu().numpy(), stats=st)
@@ -1709,7 +1727,7 @@ def test_c5_ext_hier_automatic_path(monkeypatch, c5_saturated):
     # strength of the saturated job's count (the decision is paired with the launch it measured)
     fa.run_batch(c, light, policy="EXT_HIER", hier_threshold_s=60, hier_up_tick=20 * 10**9)
     torch.cuda.synchronize()
-    assert c.hier_path_stats() == (2, 1)
+    assert c.hier_path_stats() == ((3, 0) if resume else (2, 1))
     c2 = fa.Context(0)
     for _ in range(2):
         fa.run_batch(c2, light, policy="EXT_HIER", hier_threshold_s=60, hier_up_tick=20 * 10**9)
