@@ -501,15 +501,16 @@ int fognet_sync(fognet_ctx *ctx);
 /* EXT_HIER with N > 1024 (more than one region), fognet_run_batch[_dev]: the path each
  * launch took (diagnostic).  A launch first replays every (replication, region) pair on
  * its own wavefront and hands a replication with any escalation to the sequential
- * replay, which replays it from the start (region_launches); or it runs the sequential
- * replay for every replication (sequential_launches).  Both give identical results.
- * FOGNET_HIER_REGIONS (environment): unset -- automatic: while the last region pass
+ * replay, which continues it from its first escalated publish (region_launches); or it
+ * runs the sequential replay for every replication (sequential_launches).  Both give
+ * identical results.  FOGNET_HIER_REGIONS (environment): unset or "1" -- the region pass;
+ * "0" -- always sequential; "only" -- the region pass without the hand-over (testing: a
+ * handed-over replication then reports FOGNET_ERR_UNSUPPORTED).  FOGNET_HIER_RESUME=0: the
+ * sequential replay restarts a handed-over replication from its first publish, and with
+ * FOGNET_HIER_REGIONS unset the path is chosen per launch: while the last region pass
  * whose hand-over count has reached the host (copied back asynchronously, read without
- * waiting) handed more than half of its replications over, the next launches go
- * straight to the sequential replay, with a region pass again every 16th launch to
- * re-measure; "1" -- always the region pass; "0" -- always sequential; "only" -- the
- * region pass without the hand-over (testing: a handed-over replication then reports
- * FOGNET_ERR_UNSUPPORTED). */
+ * waiting) handed more than half of its replications over, the next launches go straight
+ * to the sequential replay, with a region pass again every 16th launch to re-measure. */
 int fognet_hier_path_stats(const fognet_ctx *ctx, int64_t *region_launches, int64_t *sequential_launches);
 
 /* ---- Multi-GPU statistics exchange over RCCL (xGMI), SURVEY.md §8(b)
