@@ -219,6 +219,9 @@ __device__ __forceinline__ uint32_t w_offset(const WideNode& h, int64_t dl) {
 }
 
 // 4 waves per SIMD (<= 128 VGPRs); 10 KiB of LDS per wavefront (view ticks and horizon offsets).
+// PASS 1: every replication, up to its first escalation; 2: the escalated ones again, exactly up
+// to it (RegionWs::pass; two instantiations, so kernel traces tell the passes apart).
+template <int PASS>
 __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, RegionWs W) {
   const int B = W.B;
   const int item = W.perm[blockIdx.x];  // (region_order_kernel's dispatch order)
@@ -244,12 +247,12 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   const int32_t esc0 = __hip_atomic_load(W.esc + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the second pass replays only the replications the first found an escalation in (0 < esc < T);
   // the others keep the first pass's state and records
-  if (W.pass == 2 && (esc0 <= 0 || esc0 >= T)) return;
+  if (PASS == 2 && (esc0 <= 0 || esc0 >= T)) return;
   // esc 0: an invalid trace (see the sort) or another region's failure: the sequential kernel replays r
   uint32_t err = esc0 == 0 ? (uint32_t)kRegionSeq : (uint32_t)FOGNET_OK;
   const int s0 = err == FOGNET_OK ? seg[b] : 0;
   int nseg = err == FOGNET_OK ? seg[b + 1] - s0 : 0;  // this region's publishes
-  if (W.pass == 2) {  // those before the escalated publish: a prefix of the segment (trace order)
+  if (PASS == 2) {  // those before the escalated publish: a prefix of the segment (trace order)
     int lo = 0, hi = nseg;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
@@ -382,7 +385,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
   for (int c0 = 0; c0 < nseg && err == FOGNET_OK; c0 += kWave) {
     // first pass: this region's publishes are past r's first escalation found so far (another
     // region's, or 0 for a failure), so nothing it decides from here on matters
-    if (W.pass == 1 && (c0 & (kQuitEvery * kWave - 1)) == 0 && c0 > 0 &&
+    if (PASS == 1 && (c0 & (kQuitEvery * kWave - 1)) == 0 && c0 > 0 &&
         W.s_idx[tbase + s0 + c0] >= __hip_atomic_load(W.esc + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
       err = kRegionSeq;
       break;
@@ -643,7 +646,7 @@ __global__ __launch_bounds__(64, 4) void replay_region_kernel(ReplayArgs A, Regi
 #endif
   const uint32_t mp = ~wave_min_u32(~max_pend);
   if (lane == 0) {
-    if (W.pass == 1 && esc_hit >= 0) atomicMin(W.esc + r, esc_hit);
+    if (PASS == 1 && esc_hit >= 0) atomicMin(W.esc + r, esc_hit);
     W.rec[rb] = RegionRec{n_done, (int32_t)mp, (int32_t)err, 0};
   }
 }
@@ -862,13 +865,13 @@ hipError_t launch_replay_region(const ReplayArgs& a, const RegionWs& w, bool res
   hipLaunchKernelGGL(region_order_kernel, dim3(1), dim3(kOrderThreads), 0, s, (int32_t)(a.R * w.B), w1);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w1);
+  hipLaunchKernelGGL(replay_region_kernel<1>, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w1);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   RegionWs w2 = w;
   w2.pass = resume ? 2 : 1;  // (the finish kernel: whether the second pass ran)
   if (resume) {  // the escalated replications again, each region exactly up to the first escalation
-    hipLaunchKernelGGL(replay_region_kernel, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w2);
+    hipLaunchKernelGGL(replay_region_kernel<2>, dim3((unsigned)a.R * (unsigned)w.B), dim3(kWave), 0, s, a, w2);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -10,7 +10,7 @@ rm -rf gpurun_out/pmc; mkdir -p gpurun_out/pmc
 if [ "${WORKLOAD:-c3}" = c5 ]; then
   # POLICY=REF_V3: the flat broker (pmc_traffic_c5_REF_V3.json); default EXT_HIER (pmc_traffic_c5.json)
   BARGS="--workload c5 --policy ${POLICY:-EXT_HIER}"; DEC=10240000; CFG=1024,10000,10000
-  KERNEL=$([ "${POLICY:-EXT_HIER}" = EXT_HIER ] && echo replay_region_kernel || echo replay_wide_kernel)
+  KERNEL=$([ "${POLICY:-EXT_HIER}" = EXT_HIER ] && echo "replay_region_kernel<1>" || echo replay_wide_kernel)
   OUT=pmc_traffic_c5$([ "${POLICY:-EXT_HIER}" = EXT_HIER ] || echo _${POLICY}).json
 else
   BARGS=""; KERNEL=replay_kernel; DEC=409600000; OUT=pmc_traffic.json; CFG=4096,100000,256
