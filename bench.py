@@ -329,7 +329,9 @@ def main():
                                      "fognet_hier_path_stats)" if hier_esc and hier_esc["sequential_launches"] >= args.steps
                                      else "replay_region_kernel (one wavefront per regional broker) + "
                                      "region_finish_kernel (statistics pass)" +
-                                     (" + replay_wide_kernel (the sequential replay of the handed-back replications)"
+                                     (" + replay_region_kernel<2> and replay_wide_kernel (the escalated replications "
+                                      "replayed again up to their first escalated publish, then continued "
+                                      "sequentially from there)"
                                       if hier_esc and hier_esc["escalating_replications"] else ""))
                                     if args.policy == "EXT_HIER" and N > _abi.HIER_REGION_NODES
                                     else "replay_wide_kernel (statistics inline)" if N > 256
