@@ -134,7 +134,7 @@ class GenParams(C.Structure):
                 ("mean_gap_ticks", C.c_void_p), ("lat_scale", C.c_void_p)]
 
 
-V2_MAX_NODES = 8192
+V2_MAX_NODES = 16384
 V2_ST_LOCAL, V2_ST_FORWARDED, V2_ST_DROPPED, V2_ST_NO_NODES, V2_ST_ACCEPTED, V2_ST_REJECTED = 3, 4, 5, 6, 7, 8
 
 

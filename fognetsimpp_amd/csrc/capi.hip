@@ -838,7 +838,7 @@ int fognet_run_v2_dev(fognet_ctx* c, const fognet_v2_in* in, fognet_v2_out* out,
   if (!c || !in || !out) return FOGNET_ERR_ARG;
   if (in->R < 0 || in->T < 0 || in->N < 0) return fail(c, FOGNET_ERR_ARG, "negative R/T/N");
   if (in->N > FOGNET_V2_MAX_NODES)
-    return fail(c, FOGNET_ERR_UNSUPPORTED, "the v2 replay keeps at most 128 nodes per lane: N <= 8192");
+    return fail(c, FOGNET_ERR_UNSUPPORTED, "the v2 replay keeps at most 256 nodes per lane: N <= 16384");
   if (in->node_stride != 0 && in->node_stride != in->N) return fail(c, FOGNET_ERR_ARG, "node_stride must be 0 or N");
   const int q = in->queue_capacity ? in->queue_capacity : 256;
   if (q < 2 || (q & (q - 1)) != 0 || q > (1 << 16)) return fail(c, FOGNET_ERR_ARG, "queue_capacity must be a power of two in [2, 2^16]");

@@ -713,7 +713,7 @@ int run_v2(const Options& o, const Scenario& sc, int32_t T, const std::vector<in
            const std::vector<int32_t>& req, const std::vector<int64_t>& dl, const std::vector<int64_t>& ul,
            const std::vector<int64_t>& first_adv, const std::string& run_id) {
   const int32_t R = o.reps, N = (int32_t)sc.mips.size();
-  if (N > FOGNET_V2_MAX_NODES) die("BrokerBaseApp2 replays take at most 8192 fog nodes");
+  if (N > FOGNET_V2_MAX_NODES) die("BrokerBaseApp2 replays take at most 16384 fog nodes");
   hip_check(hipSetDevice(o.device), "hipSetDevice");
   fognet_ctx* ctx = nullptr;
   if (fognet_create(&ctx, o.device) != FOGNET_OK) die("fognet_create: no gfx950 device " + std::to_string(o.device));

@@ -146,16 +146,19 @@ struct V2Node {
 // NPL nodes per lane (N <= 64 * NPL): node j on lane j % 64, slot j / 64, like
 // the v3 register kernel.  The slot is a compile-time index everywhere (static
 // loops select it), so the state stays in registers.
-// A lane's slots as a bit mask (bit s: slot s): 128 bits above 64 slots per lane.
-__device__ __forceinline__ int slot_ctz(uint64_t m) { return (int)__builtin_ctzll(m); }
-__device__ __forceinline__ int slot_ctz(unsigned __int128 m) {
-  const uint64_t lo = (uint64_t)m;
-  return lo ? (int)__builtin_ctzll(lo) : 64 + (int)__builtin_ctzll((uint64_t)(m >> 64));
-}
-__device__ __forceinline__ uint32_t slot_popc(uint64_t m) { return (uint32_t)__popcll(m); }
-__device__ __forceinline__ uint32_t slot_popc(unsigned __int128 m) {
-  return (uint32_t)__popcll((uint64_t)m) + (uint32_t)__popcll((uint64_t)(m >> 64));
-}
+// A lane's slots as a bit mask (bit s: slot s), one 64-bit word per 64 slots.
+template <int W>
+struct SlotBits {
+  uint64_t w[W];
+  __device__ __forceinline__ void set(int s) { w[s >> 6] |= 1ull << (s & 63); }
+  __device__ __forceinline__ bool test(int s) const { return ((w[s >> 6] >> (s & 63)) & 1ull) != 0ull; }
+  __device__ __forceinline__ uint32_t popc() const {
+    uint32_t c = 0u;
+#pragma unroll
+    for (int i = 0; i < W; ++i) c += (uint32_t)__popcll(w[i]);
+    return c;
+  }
+};
 
 template <int NPL>
 __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
   // by ws directly and goes to scratch, read by one handler per step instead of by
   // every step's scan.  NPL <= 4 keeps everything in VGPRs (static slot loops).
   constexpr bool kCold = NPL >= FOGNET_V2_COLD_NPL;
-  using SlotMask = std::conditional_t<(NPL > 64), unsigned __int128, uint64_t>;
+  using SlotMask = SlotBits<(NPL + 63) / 64>;
   int64_t h_tick[kCold ? NPL : 1];
   uint64_t h_seq[kCold ? NPL : 1];
   int32_t h_src[kCold ? NPL : 1], h_view[kCold ? NPL : 1];
@@ -287,25 +290,33 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       for (int s = 0; s < NPL; ++s) f(nd[s], s);
     }
   };
-  auto for_slots_in = [&](SlotMask m, auto&& f) {
+  auto for_slots_in = [&](const SlotMask& m, auto&& f) {
     if constexpr (kCold) {
-      for (; m; m &= m - 1) {
-        const int s = slot_ctz(m);
-        f(nd[s], s);
+#pragma unroll 1
+      for (int i = 0; i < (NPL + 63) / 64; ++i) {
+        for (uint64_t x = m.w[i]; x; x &= x - 1ull) {
+          const int s = i * 64 + (int)__builtin_ctzll(x);
+          f(nd[s], s);
+        }
       }
     } else {
 #pragma unroll
       for (int s = 0; s < NPL; ++s)
-        if ((m >> s) & 1u) f(nd[s], s);
+        if (m.test(s)) f(nd[s], s);
     }
   };
-  // batch ranks (kBatchFirings): the batch's firings as (tick, seq << 14 | releases << 13 |
+  // batch ranks (kBatchFirings): the batch's firings as (tick, seq << 15 | releases << 14 |
   // node) sorted in LDS; then each firing's sequence-number offset, by node (aliasing the
-  // ticks, dead once sorted)
-  __shared__ int64_t s_bt[NPL * kWave];
-  __shared__ uint64_t s_bk[NPL * kWave];
-  uint32_t* const s_off = reinterpret_cast<uint32_t*>(s_bt);
-  static_assert(NPL * kWave <= (1 << 13), "node index in 13 bits of the batch key");
+  // ticks, dead once sorted: 32-bit offsets while the sort holds a firing per node, 16-bit
+  // above, where a batch is cut at kSortCap firings)
+  constexpr int kSortCap = NPL * kWave <= 8192 ? NPL * kWave : 4096;
+  using OffT = std::conditional_t<(kSortCap < NPL * kWave), uint16_t, uint32_t>;
+  __shared__ int64_t s_bt[kSortCap];
+  __shared__ uint64_t s_bk[kSortCap];
+  OffT* const s_off = reinterpret_cast<OffT*>(s_bt);
+  static_assert(NPL * kWave <= (1 << 14), "node index in 14 bits of the batch key");
+  static_assert(sizeof(OffT) * NPL * kWave <= sizeof(int64_t) * kSortCap, "offsets alias the sorted ticks");
+  static_assert(sizeof(OffT) == 4 || 3 * kSortCap < 65536, "16-bit offsets: 2 i + releases < 3 kSortCap");
 
   // ---- broker (wave-uniform)
   int32_t pool = A.broker_mips[r];
@@ -423,27 +434,67 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       }
       // the batch's firings (bit s: slot s), and those that release a reservation
       // (ComputeBrokerApp2.cc:222-226: the oldest, when its deadline < now)
-      SlotMask cm = 0, rm = 0;
+      SlotMask cm{}, rm{};
       for_slots([&](V2Node& x, int s) {
         if (x.t_sched && x.t_tick < stop && earlier(x.t_tick, x.t_seq, H_t, H_s)) {
-          cm |= (SlotMask)1 << s;
+          cm.set(s);
           if (x.t_kind == kKindRelease && x.rs_n) {
             const V2Res h = P.res[qrow(s) + (x.rs_h & qm)];
-            if (h.deadline < dbl(x.t_tick)) rm |= (SlotMask)1 << s;
+            if (h.deadline < dbl(x.t_tick)) rm.set(s);
           }
         }
       });
-      const uint32_t c = slot_popc(cm);
-      const uint32_t c_incl = wave_scan_add_u32(c);
-      const uint32_t n = readlane_u32(c_incl, kWave - 1);
-      if (seq >= (1ull << 49)) {  // (the sort key keeps the sequence in 50 bits)
+      uint32_t c = cm.popc();
+      uint32_t c_incl = wave_scan_add_u32(c);
+      uint32_t n = readlane_u32(c_incl, kWave - 1);
+      if constexpr (kSortCap < NPL * kWave) {
+        if (n > (uint32_t)kSortCap) {
+          // more firings than the LDS sort holds: the batch ends earlier, at the largest (tick,
+          // seq) bound H' with at most kSortCap firings before it (binary searches over the
+          // tick, then the sequence at that tick); the events from H' on are the next step's.
+          // At least the current event (a firing at e_tick, e_seq) stays before it.
+          auto before = [&](int64_t bt, uint64_t bs) -> uint32_t {
+            uint32_t k = 0u;
+            for_slots_in(cm, [&](V2Node& x, int) { k += earlier(x.t_tick, x.t_seq, bt, bs) ? 1u : 0u; });
+            return wave_sum_u32(k);
+          };
+          // before(lo, 0) == 0; before(hi, 0) >= n > cap (every firing of the batch is before stop)
+          int64_t lo = e_tick, hi = H_t < stop ? H_t + 1 : stop;
+          while (hi - lo > 1) {
+            const int64_t mid = lo + (hi - lo) / 2;
+            if (before(mid, 0ull) <= (uint32_t)kSortCap) lo = mid;
+            else hi = mid;
+          }
+          uint64_t slo = 0ull, shi = ~0ull;  // at tick lo: before(lo, ~0) covers every firing at lo
+          while (shi - slo > 1ull) {
+            const uint64_t mid = slo + (shi - slo) / 2ull;
+            if (before(lo, mid) <= (uint32_t)kSortCap) slo = mid;
+            else shi = mid;
+          }
+          H_t = lo;
+          H_s = slo;
+          SlotMask cm2{}, rm2{};
+          for_slots_in(cm, [&](V2Node& x, int s) {
+            if (earlier(x.t_tick, x.t_seq, H_t, H_s)) {
+              cm2.set(s);
+              if (rm.test(s)) rm2.set(s);
+            }
+          });
+          cm = cm2;
+          rm = rm2;
+          c = cm.popc();
+          c_incl = wave_scan_add_u32(c);
+          n = readlane_u32(c_incl, kWave - 1);
+        }
+      }
+      if (seq >= (1ull << 48)) {  // (the sort key keeps the sequence in 49 bits)
         err = FOGNET_ERR_CAPACITY;
         break;
       }
       uint32_t p = c_incl - c;
       for_slots_in(cm, [&](V2Node& x, int s) {
         s_bt[p] = x.t_tick;
-        s_bk[p] = (x.t_seq << 14) | ((uint64_t)((rm >> s) & 1u) << 13) | (uint64_t)(s * kWave + lane);
+        s_bk[p] = (x.t_seq << 15) | ((uint64_t)(rm.test(s) ? 1u : 0u) << 14) | (uint64_t)(s * kWave + lane);
         ++p;
       });
       uint32_t n2 = 1u;
@@ -477,9 +528,9 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       for (uint32_t b0 = 0u; b0 < n; b0 += kWave) {
         const uint32_t i = b0 + (uint32_t)lane;
         const uint64_t kx = i < n ? s_bk[i] : 0ull;
-        const uint32_t rl = i < n ? (uint32_t)(kx >> 13) & 1u : 0u;
+        const uint32_t rl = i < n ? (uint32_t)(kx >> 14) & 1u : 0u;
         const uint32_t incl = wave_scan_add_u32(rl);
-        if (i < n) s_off[kx & 0x1FFFu] = 2u * i + n_relb + incl - rl;
+        if (i < n) s_off[kx & 0x3FFFu] = (OffT)(2u * i + n_relb + incl - rl);
         n_relb += readlane_u32(incl, kWave - 1);
       }
       __syncthreads();
@@ -490,7 +541,7 @@ __global__ __launch_bounds__(64) void replay_v2_kernel(V2Args P) {
       uint64_t lt_s = 0ull;
       for_slots_in(cm, [&](V2Node& x, int s) {
         const uint32_t off = s_off[s * kWave + lane];
-        const bool rel = ((rm >> s) & 1u) != 0;
+        const bool rel = rm.test(s);
         uint64_t sq = seq + off;
         const int64_t ft = x.t_tick;
         const uint64_t fs = x.t_seq;
@@ -1685,8 +1736,10 @@ hipError_t launch_replay_v2(const fognet_v2_in& in, const fognet_v2_out& out, vo
     hipLaunchKernelGGL(replay_v2_kernel<32>, dim3(in.R), dim3(kWave), 0, s, a);
   else if (in.N <= 4096)
     hipLaunchKernelGGL(replay_v2_kernel<64>, dim3(in.R), dim3(kWave), 0, s, a);
-  else
+  else if (in.N <= 8192)
     hipLaunchKernelGGL(replay_v2_kernel<128>, dim3(in.R), dim3(kWave), 0, s, a);
+  else
+    hipLaunchKernelGGL(replay_v2_kernel<256>, dim3(in.R), dim3(kWave), 0, s, a);
   return hipGetLastError();
 }
 

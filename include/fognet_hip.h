@@ -314,11 +314,11 @@ typedef struct fognet_user_stats {
  * requiredTime and runs a 10-ms advert/release timer (ComputeBrokerApp2.cc:
  * 202-318).  Deadlines are doubles compared with simTime().dbl() = ticks *
  * 1e-12, exactly as the reference does (their rounding decides releases). */
-#define FOGNET_V2_MAX_NODES 8192 /* node j on lane j % 64, slot j / 64 (up to 128 per lane) */
+#define FOGNET_V2_MAX_NODES 16384 /* node j on lane j % 64, slot j / 64 (up to 256 per lane) */
 /* Device workspace of a v2 replay (fognet_run_v2_dev, allocated and kept by the context): 64 B per
  * (replication, node slot, queue entry) plus R * T B, i.e. R * S * queue_capacity * 64 B with S = N
  * rounded up to 64 x a power of two -- at N = 4096 and the default capacity 256, 64 MiB per replication
- * (128 MiB at N = 8192).  Above 256 nodes (NPL >= 8) each node's record lives in
+ * (128 MiB at N = 8192, 256 MiB at N = 16384).  Above 256 nodes (NPL >= 8) each node's record lives in
  * per-lane scratch memory. */
 
 typedef enum fognet_v2_task_status {

@@ -1150,16 +1150,17 @@ def v2_random(seed, R, N, T):
 @pytest.mark.parametrize("seed,N,R", [(0, 1, 16), (1, 2, 16), (2, 5, 16), (3, 13, 16), (4, 64, 16), (5, 5, 16),
                                       (6, 16, 7), (7, 17, 5), (8, 3, 1), (9, 5, 13), (10, 65, 5), (11, 200, 4),
                                       (12, 129, 3), (13, 300, 2), (14, 1024, 2), (15, 2048, 2), (16, 4096, 1),
-                                      (17, 4097, 1), (18, 8192, 2)])
+                                      (17, 4097, 1), (18, 8192, 2), (19, 8193, 1), (20, 16384, 1)])
 def test_v2_random_matches_oracle(ctx, seed, N, R):
     """N <= 16: replay_v2_rows_kernel<16> (four replications per wavefront, R not
     a multiple of four included); 17 <= N <= 32: replay_v2_rows_kernel<32> (two);
     N > 32: replay_v2_kernel<NPL> with node j on lane j % 64, slot j / 64 (NPL = 1,
-    2, 4, 8, 16, 32, 64, 128: N <= 8192; the reference's loop takes any brokers.size(),
+    2, 4, 8, 16, 32, 64, 128, 256: N <= 16384, the batches cut at 4,096 firings above 8,192; the
+    reference's loop takes any brokers.size(),
     BrokerBaseApp2.cc:241-248).  Every node's 10-ms timer fires throughout, so the
     wider node sets take shorter traces."""
     tr, broker, stop, rt = v2_random(seed, R, N, 3000 if N <= 256 else 1500 if N <= 1024 else 400 if N <= 2048 else
-                                     200 if N <= 4096 else 120)
+                                     200 if N <= 4096 else 120 if N <= 8192 else 60)
     g = run_v2_gpu(ctx, tr, broker, stop, rt, qcap=4096)
     o = ol.run_v2(tr["arrive"], tr["req"], broker, tr["mips"], tr["dl"], tr["ul"], tr["first_adv"], stop, rt,
                   threads=8)
@@ -1167,7 +1168,7 @@ def test_v2_random_matches_oracle(ctx, seed, N, R):
     assert_v2_parity(g, o)
 
 
-@pytest.mark.parametrize("N,T", [(4096, 400), (8192, 200)])
+@pytest.mark.parametrize("N,T", [(4096, 400), (8192, 200), (16384, 100)])
 def test_v2_widest_node_set_reserves_on_high_slots(ctx, N, T):
     """N = 4096 (replay_v2_kernel<64>: 64 nodes per lane, per-node records in scratch) and N = 8192
     (replay_v2_kernel<128>: the slot masks take 128 bits) with R = 4 and traces long enough for
@@ -1290,7 +1291,7 @@ def test_v2_errors(ctx):
               first_adv=np.zeros(0, np.int64))
     g = run_v2_gpu(ctx, tr, 100, 100 * MS)
     assert int(g["stats"]["status"][0]) == _abi.FOGNET_ERR_STATE
-    n = _abi.V2_MAX_NODES + 1  # (128 nodes per lane)
+    n = _abi.V2_MAX_NODES + 1  # (256 nodes per lane)
     big = dict(arrive=np.array([[10 * MS]]), req=np.array([[1]], np.int32), mips=np.full(n, 1000, np.int32),
                dl=np.ones(n, np.int64), ul=np.ones(n, np.int64), first_adv=np.ones(n, np.int64))
     with pytest.raises(fa.FognetError) as e:
