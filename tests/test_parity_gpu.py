@@ -1498,6 +1498,43 @@ def test_hier_region_pass_and_handover(ctx, monkeypatch):
         np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
 
 
+@pytest.mark.parametrize("resume", ["1", "0"])
+def test_hier_resume_at_first_escalation(ctx, monkeypatch, resume):
+    """EXT_HIER resume (replay_region.hip): twelve replications whose 6-node second region
+    takes most publishes from a replication-specific point on, so each escalates first at a
+    different publish (116 .. 1,589 in the oracle: anywhere in a 64-publish chunk, early and
+    late); the second region pass stops every region exactly before it and the sequential
+    kernel continues from there.  Outputs, records, per-node energy and the job histogram
+    equal the oracle's, as with FOGNET_HIER_RESUME=0 (restart from the first publish)."""
+    R, N, T = 12, 1030, 3000
+    tr = tg.make_batch(33, R, N, T, rho=0.01)
+    reg = np.zeros_like(tr["req"])
+    rng = np.random.default_rng(5)
+    for r, s0 in enumerate([0, 0, 0, 0, 0, 0, 200, 400, 600, 800, 1000, 1500]):
+        reg[r, s0:][rng.random(T - s0) < 0.5 + 0.04 * r] = 1
+    pb, pi = fa.power_model(tr["mips"])
+    tr = dict(tr, region=reg, p_busy=pb, p_idle=pi)
+    o = ol.run_batch(tr["arrive"], tr["req"], tr["mips"], tr["dl"], tr["ul"], tr["init"], threads=8, hist=True,
+                     policy=ol.POLICY_EXT_HIER, region=reg, hier_threshold_s=0, hier_up_tick=10**11,
+                     p_busy=pb, p_idle=pi)
+    esc = o["node"] // _abi.HIER_REGION_NODES != reg
+    first = np.where(esc.any(axis=1), esc.argmax(axis=1), -1)
+    assert (first > 0).all() and first.min() < 200 and len(set((first % 64).tolist())) > 6
+    monkeypatch.setenv("FOGNET_HIER_REGIONS", "1")
+    monkeypatch.setenv("FOGNET_HIER_RESUME", resume)
+    out = fa.run_batch(ctx, fa.as_device_trace(tr, torch.device("cuda", ctx.device)), policy="EXT_HIER",
+                       hier_threshold_s=0, hier_up_tick=10**11, hist=True)
+    torch.cuda.synchronize()
+    st = out.rep_stats()
+    g = dict(node=out.node.cpu().numpy(), status=out.status.cpu().numpy(), start=out.start_tick.cpu().numpy(),
+             done=out.done_tick.cpu().numpy(), stats=st)
+    assert (st["status"] == 0).all()
+    assert_parity(tr, g, o)
+    assert st.tobytes() == o["stats"].tobytes()
+    np.testing.assert_array_equal(out.node_energy.cpu().numpy(), o["node_energy"])
+    np.testing.assert_array_equal(out.hist.cpu().numpy(), o["hist"].sum(axis=0))
+
+
 @pytest.mark.parametrize("thr,up_s", [(0, 1), (3, 2), (0, 40), (2, 300)])
 def test_hier_overtaken_escalation_matches_oracle(ctx, thr, up_s):
     """EXT_HIER: publishes alternating between a saturated 6-node region and a
