@@ -487,7 +487,8 @@ constexpr uint32_t kViewBusySat = 0xFFFFFFFFu;
 // the same-tick rule compares the arrival's own insertion tick.
 // broken: the chain invariant failed (see below; a library bug, never an input).
 __device__ __forceinline__ bool apply_wide_advert(WideNode& h, const WideEntry* e, int64_t dl, int64_t ul, int64_t up,
-                                             int64_t& nxt_j, uint32_t& busy_j, bool& broken) {
+                                             int64_t& nxt_j, uint32_t& busy_j, bool& broken,
+                                             uint32_t* walk = nullptr) {
   // the entry after the head, loaded first: for the lane's cached node h is in
   // registers, so this load issues together with the group's view loads
   WideEntry nx{};
@@ -509,7 +510,9 @@ __device__ __forceinline__ bool apply_wide_advert(WideNode& h, const WideEntry* 
   if (arrives_before(h.tl_a, h.hd_done, dl + ((h.tl_S >> 31) ? up : 0), h.hd_S)) {
     c_arrived = h.tl_C;  // ... or everything up to the newest task (the common case)
   } else {
+    if (walk) *walk += 1u;  // (profile builds: backward walks, and their steps << 16)
     for (int32_t x = e[h.tl].prev; x != h.hd;) {  // newest first
+      if (walk) *walk += 1u << 16;
       const WideEntry ex = e[x];
       if (arrives_before(ex.a, h.hd_done, dl + (ex.pad ? up : 0), h.hd_S)) {
         c_arrived = ex.C;

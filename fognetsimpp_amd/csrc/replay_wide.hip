@@ -760,6 +760,8 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   // profile build only (tools/wide_prof.py): loop counters, written over the statistics
   uint64_t pf_iter = 0, pf_advit = 0, pf_adv = 0, pf_same = 0, pf_hit = 0, pf_gkey = 0, pf_scan = 0, pf_runs = 0;
   uint64_t pf_t[7] = {0, 0, 0, 0, 0, 0, 0};  // s_memtime ticks per segment (WTM)
+  uint32_t pf_walk = 0u;                      // backward walks of the adverts (+ steps << 16)
+#define PF_WALK (&pf_walk)
   uint64_t pf_last = __builtin_amdgcn_s_memtime();
 #define WTM(i)                                          \
   {                                                     \
@@ -769,6 +771,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
   }
 #else
 #define WTM(i)
+#define PF_WALK nullptr
 #endif
   // the decision is recomputed only after an advert changed the view
   // (adverts are the only view updates, BrokerBaseApp3.cc:123-130)
@@ -863,12 +866,12 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
           bool broken = false, fits = true;
           int64_t w_j = kNever;
           auto apply_due = [&](WideNode& hh, int64_t dl, int64_t ul) {
-            fits = apply_wide_advert(hh, e, dl, ul, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
+            fits = apply_wide_advert(hh, e, dl, ul, kHier ? A.hier_up : 0, nxt_j, busy_j, broken, PF_WALK);
             while (nxt_j < t && !broken) {
 #ifdef FOGNET_WIDE_PROF
               ++pf_same;
 #endif
-              fits &= apply_wide_advert(hh, e, dl, ul, kHier ? A.hier_up : 0, nxt_j, busy_j, broken);
+              fits &= apply_wide_advert(hh, e, dl, ul, kHier ? A.hier_up : 0, nxt_j, busy_j, broken, PF_WALK);
             }
             if constexpr (!kPerPublish) w_j = node_w(hh, nxt_j, dl);
           };
@@ -1293,6 +1296,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     pf_hit += shfl_xor_u64(pf_hit, m);
     pf_gkey += shfl_xor_u64(pf_gkey, m);
   }
+  const uint64_t pf_w1 = wave_sum_u64((uint64_t)(pf_walk & 0xFFFFu)), pf_w2 = wave_sum_u64((uint64_t)(pf_walk >> 16));
 #endif
   acc = wave_merge(acc);
   ab = wave_min_abort(ab);
@@ -1323,6 +1327,7 @@ __device__ __forceinline__ void replay_wide_rep(const ReplayArgs& A, int r, int 
     S->last_tick = (int64_t)pf_t[4];      // run horizon + FIFO + entries
     S->queue_sq_top = pf_t[5];            // record update
     S->busy_s = (int64_t)pf_t[6];         // chunk start: trace load + preconditions
+    S->n_started = (int64_t)(pf_w1 | (pf_w2 << 32));  // walks | steps << 32
 #endif
   }
   // a11 energy (fognet_hip.h): E_j = P_busy_j * B_j + P_idle_j * ((H - B_j 1e12) / 1e12)

@@ -6,7 +6,7 @@ import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fognetsimpp_amd import _abi
 _abi.LIB_PATH = os.environ.get("FOGNET_LIB", "build/live/wideprof/libfognet_hip.so")
-os.environ["FOGNET_HIER_REGIONS"] = "0"  # the sequential kernel, as the bench's timed launches run it
+os.environ["FOGNET_HIER_REGIONS"] = os.environ.get("REGIONS", "0")  # 0: the sequential kernel from the start; 1: resumed at the first escalation
 import fognetsimpp_amd as fa
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 T, N = 32_768, 10_000
@@ -28,3 +28,6 @@ seg = [("chunk_end", "queue_min_raw"), ("adverts", "queue_max_raw"), ("decision"
 tot = sum(st[k].astype(np.float64).sum() for _, k in seg)
 print("time split:", ", ".join("%s %.1f%%" % (n, 100 * st[k].astype(np.float64).sum() / tot) for n, k in seg),
       "| ticks per decision %.0f" % (tot / d))
+w = st["n_started"].astype(np.uint64)
+print("backward walks per decision %.4f, walk steps per decision %.3f" % ((w & np.uint64(0xFFFFFFFF)).astype(np.float64).sum() / d,
+                                                                        (w >> np.uint64(32)).astype(np.float64).sum() / d))
