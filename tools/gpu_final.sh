@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-end evidence, part PART (1: tests, smoke, C3 bench line + the kernel trace of that same
 # command; 2: PMC passes C3, C5 EXT_HIER, C5 REF_V3; 3: C5 lines (EXT_HIER light, REF_V3,
-# EXT_HIER saturating) + their kernel traces; 4: C4 and C1 lines).  Outputs under
+# EXT_HIER saturating) + their kernel traces; 4: C4 and C1 lines; 5: C4 and C1 kernel traces).  Outputs under
 # gpurun_out/final/.  Kernel statistics: tools/kstats.py over the kernel trace without the
 # warm-up dispatches (the timed steps only); tools/kprof_sidecar.py turns each into the
 # profiles/kernel_profile_<workload>.json that bench.py quotes (kernel_avg_ms_rocprof), refusing
@@ -56,6 +56,10 @@ case "${PART:-1}" in
   step bench_c1
   timeout -k 10 400 python bench.py --workload c1 --steps 2 --warmup 1 > $O/bench_c1.log 2>&1 || { tail $O/bench_c1.log; exit 1; }
   grep '^{' $O/bench_c1.log | tail -n 1 > $O/bench_c1.json
+  ;;
+5)
+  kt c4 replay_gen_kernel 1 --workload c4 --steps 3 --warmup 1 --no-cpu || exit 1
+  kt c1 replay_v2_rows_kernel 1 --workload c1 --steps 2 --warmup 1 --no-cpu || exit 1
   ;;
 esac
 step done
