@@ -519,6 +519,7 @@ def bench_c4(args, ctx, dev, dist, world, rank):
                       "response_ms_mean": summary["response_ms"].get("mean"), "energy_j": summary["energy_j"],
                       "max_pending": summary["max_pending"], "hist_counts": [int(hist[0].sum()), int(hist[1].sum())]},
         }
+        line["roofline"].update(rocprof_kernel_avg(args, line))  # (the committed kernel trace of this library)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -631,6 +632,7 @@ def bench_c1(args, ctx, dev, dist, world, rank):
             "stats": {"decisions": decisions, "events": events, "local": int(st["n_local"].sum()),
                       "forwarded": int(st["n_forwarded"].sum())},
         }
+        line["roofline"].update(rocprof_kernel_avg(args, line))  # (the committed kernel trace of this library)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
