@@ -117,3 +117,23 @@ def test_plain_c_client_on_gpu():
     p = subprocess.run([build_c_client()], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "all checks passed" in p.stdout
+
+
+def test_numeric_limits_match_header(tmp_path):
+    """The ctypes mirror's constants (limits, ABI version, histogram shape, policy ids) equal the
+    header's macros as the C compiler evaluates them."""
+    pairs = {"FOGNET_ABI_VERSION": abi.ABI_VERSION, "FOGNET_HIST_METRICS": abi.HIST_METRICS,
+             "FOGNET_HIST_BINS": abi.HIST_BINS, "FOGNET_HIER_REGION_NODES": abi.HIER_REGION_NODES,
+             "FOGNET_V2_MAX_NODES": abi.V2_MAX_NODES, "FOGNET_COMM_ID_BYTES": abi.COMM_ID_BYTES,
+             "FOGNET_TICKS_PER_SECOND": abi.TICKS_PER_SECOND, "FOGNET_FLAG_REF_ABORT": abi.FLAG_REF_ABORT,
+             "FOGNET_POLICY_REF_V3": abi.FOGNET_POLICY_REF_V3, "FOGNET_POLICY_EXT_HIER": abi.FOGNET_POLICY_EXT_HIER,
+             "FOGNET_ERR_UNSUPPORTED": abi.FOGNET_ERR_UNSUPPORTED}
+    src = tmp_path / "limits.c"
+    src.write_text("#include <stdio.h>\n#include \"fognet_hip.h\"\nint main(void){" +
+                   "".join(f'printf("{k} %lld\\n", (long long)({k}));' for k in pairs) + "return 0;}\n")
+    exe = tmp_path / "limits"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    got = dict(ln.split() for ln in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines())
+    for k, v in pairs.items():
+        assert int(got[k]) == v, k
