@@ -137,3 +137,13 @@ def test_numeric_limits_match_header(tmp_path):
     got = dict(ln.split() for ln in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines())
     for k, v in pairs.items():
         assert int(got[k]) == v, k
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No CPU fallback: without the built HIP library the package refuses to run."""
+    monkeypatch.setattr(abi, "_lib", None)
+    monkeypatch.setattr(abi, "LIB_PATH", str(tmp_path / "libfognet_hip.so"))
+    with pytest.raises(ImportError, match="no CPU fallback"):
+        abi.load()
+    with pytest.raises(ImportError):
+        abi.status_string(0)
